@@ -1,0 +1,194 @@
+"""ctypes wrapper over the CPU oracle (liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: the parity checker and the CPU baseline. Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module. The product path (tigerbeetle_amd / libtbc.so) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+KEY_TIMESTAMP, KEY_ID_U128, KEY_COMPOSITE_U64, KEY_COMPOSITE_U128 = 0, 1, 2, 3
+USAGE_GENERAL, USAGE_SECONDARY_INDEX = 0, 1
+
+
+def build() -> str:
+    """Compile the oracle in-tree (make)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+class Tree(ctypes.Structure):
+    _fields_ = [
+        ("tree_id", ctypes.c_uint16),
+        ("key_kind", ctypes.c_uint8),
+        ("usage", ctypes.c_uint8),
+        ("value_size", ctypes.c_uint32),
+        ("timestamp_offset", ctypes.c_uint32),
+        ("key_size", ctypes.c_uint32),
+        ("block_size", ctypes.c_uint32),
+        ("block_value_count_max", ctypes.c_uint32),
+        ("data_block_count_max", ctypes.c_uint32),
+        ("value_count_max", ctypes.c_uint32),
+        ("index_size", ctypes.c_uint32),
+        ("index_checksums_offset", ctypes.c_uint32),
+        ("index_keys_min_offset", ctypes.c_uint32),
+        ("index_keys_max_offset", ctypes.c_uint32),
+        ("index_addresses_offset", ctypes.c_uint32),
+    ]
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("count", ctypes.c_uint32)]
+
+
+class Job(ctypes.Structure):
+    _fields_ = [
+        ("tree", ctypes.POINTER(Tree)),
+        ("a_immutable", ctypes.c_int),
+        ("segments_a", ctypes.POINTER(Segment)),
+        ("segment_count_a", ctypes.c_uint32),
+        ("segments_b", ctypes.POINTER(Segment)),
+        ("segment_count_b", ctypes.c_uint32),
+        ("drop_tombstones", ctypes.c_int),
+        ("level_b", ctypes.c_uint8),
+        ("cluster_lo", ctypes.c_uint64),
+        ("cluster_hi", ctypes.c_uint64),
+        ("snapshot_min", ctypes.c_uint64),
+        ("addresses", ctypes.POINTER(ctypes.c_uint64)),
+        ("address_count", ctypes.c_uint32),
+        ("out_blocks", ctypes.c_void_p),
+        ("out_block_capacity", ctypes.c_uint32),
+        ("out_table_infos", ctypes.c_void_p),
+        ("out_table_capacity", ctypes.c_uint32),
+        ("out_value_count", ctypes.c_uint64),
+        ("out_data_block_count", ctypes.c_uint32),
+        ("out_table_count", ctypes.c_uint32),
+        ("out_block_count", ctypes.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.tbo_checksum.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        _lib.tbo_checksum.restype = None
+        _lib.tbo_has_aesni.restype = ctypes.c_int
+        _lib.tbo_force_portable.argtypes = [ctypes.c_int]
+        _lib.tbo_aegis_seed_state.argtypes = [ctypes.c_void_p]
+        _lib.tbo_tree_init.argtypes = [ctypes.POINTER(Tree), ctypes.c_uint16, ctypes.c_uint8,
+                                       ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_uint32]
+        _lib.tbo_tree_init.restype = ctypes.c_int
+        _lib.tbo_sort_values.argtypes = [ctypes.POINTER(Tree), ctypes.c_void_p, ctypes.c_uint32]
+        _lib.tbo_sort_values.restype = ctypes.c_int
+        _lib.tbo_compact.argtypes = [ctypes.POINTER(Job)]
+        _lib.tbo_compact.restype = ctypes.c_int
+        _lib.tbo_key.argtypes = [ctypes.POINTER(Tree), ctypes.c_void_p, ctypes.c_void_p]
+    return _lib
+
+
+def checksum(data: bytes | np.ndarray, portable: bool = False) -> int:
+    """vsr.checksum (src/vsr/checksum.zig:50) as a Python int (u128)."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    out = (ctypes.c_uint8 * 16)()
+    lib().tbo_force_portable(1 if portable else 0)
+    try:
+        lib().tbo_checksum(buf.ctypes.data if buf.size else None, buf.size, out)
+    finally:
+        lib().tbo_force_portable(0)
+    return int.from_bytes(bytes(out), "little")
+
+
+def seed_state() -> bytes:
+    out = (ctypes.c_uint8 * 128)()
+    lib().tbo_aegis_seed_state(out)
+    return bytes(out)
+
+
+def tree(tree_id, key_kind, usage, value_size, timestamp_offset, table_value_count_max,
+         block_size) -> Tree:
+    t = Tree()
+    rc = lib().tbo_tree_init(ctypes.byref(t), tree_id, key_kind, usage, value_size,
+                             timestamp_offset, table_value_count_max, block_size)
+    if rc != 0:
+        raise ValueError(f"tbo_tree_init failed: {rc}")
+    return t
+
+
+def sort_values(t: Tree, values: np.ndarray) -> np.ndarray:
+    """TableMemory.sort: stable sort by key; returns a sorted copy (rows = values)."""
+    v = np.ascontiguousarray(values, dtype=np.uint8).copy()
+    n = v.shape[0]
+    rc = lib().tbo_sort_values(ctypes.byref(t), v.ctypes.data, n)
+    if rc != 0:
+        raise RuntimeError(f"tbo_sort_values failed: {rc}")
+    return v
+
+
+class CompactionResult:
+    def __init__(self, status, blocks, table_infos, value_count, data_block_count):
+        self.status = status
+        self.blocks = blocks  # (block_count, block_size) uint8, acquire order
+        self.table_infos = table_infos  # (table_count, 128) uint8
+        self.value_count = value_count
+        self.data_block_count = data_block_count
+
+
+def compact(t: Tree, a_segments, b_segments, *, a_immutable: bool, drop_tombstones: bool,
+            level_b: int, cluster: int, snapshot_min: int, addresses) -> CompactionResult:
+    """One Compaction (A = immutable sorted table or disk-table blocks, B =
+    level-B blocks). Segments are 2-D uint8 arrays, one row per value."""
+    keep = []
+
+    def segs(lst):
+        arr = (Segment * max(1, len(lst)))()
+        for i, s in enumerate(lst):
+            s = np.ascontiguousarray(s, dtype=np.uint8)
+            keep.append(s)
+            arr[i].values = s.ctypes.data if s.size else None
+            arr[i].count = s.shape[0]
+        return arr
+
+    sa, sb = segs(a_segments), segs(b_segments)
+    addrs = np.ascontiguousarray(np.asarray(addresses, dtype=np.uint64))
+    cap = len(addrs)
+    out_blocks = np.zeros((max(cap, 1), t.block_size), dtype=np.uint8)
+    tables_cap = cap
+    out_infos = np.zeros((max(tables_cap, 1), 128), dtype=np.uint8)
+    job = Job()
+    job.tree = ctypes.pointer(t)
+    job.a_immutable = int(a_immutable)
+    job.segments_a = sa
+    job.segment_count_a = len(a_segments)
+    job.segments_b = sb
+    job.segment_count_b = len(b_segments)
+    job.drop_tombstones = int(drop_tombstones)
+    job.level_b = level_b
+    job.cluster_lo = cluster & ((1 << 64) - 1)
+    job.cluster_hi = cluster >> 64
+    job.snapshot_min = snapshot_min
+    job.addresses = addrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    job.address_count = cap
+    job.out_blocks = out_blocks.ctypes.data
+    job.out_block_capacity = cap
+    job.out_table_infos = out_infos.ctypes.data
+    job.out_table_capacity = tables_cap
+    rc = lib().tbo_compact(ctypes.byref(job))
+    return CompactionResult(rc, out_blocks[: job.out_block_count],
+                            out_infos[: job.out_table_count], job.out_value_count,
+                            job.out_data_block_count)
