@@ -1,0 +1,182 @@
+/*
+ * tbc.h — C ABI of the MI355X-native LSM compaction engine for TigerBeetle's
+ * forest ("tbc" = TigerBeetle compaction).
+ *
+ * This is the drop-in boundary a Zig host adapter `@cImport`s. It replaces
+ * the data-parallel internals of the reference's comptime-generic
+ * `CompactionType(Table, Tree, Storage)` (src/lsm/compaction.zig:56-60) and
+ * `TableMemoryType.sort` (src/lsm/table_memory.zig:140-154) while the
+ * `Tree`/`Compaction` surface the grooves use stays unchanged
+ * (see INTEGRATION.md for the adapter and the binding stub).
+ *
+ * Conventions (following the only existing C ABI of the reference,
+ * src/clients/c/tb_client.h:170-240):
+ *   - plain pointers and sizes, no C++ types, every call returns tbc_status;
+ *   - all device memory is either allocated through tbc_device_alloc or is a
+ *     HIP device pointer owned by the caller;
+ *   - nothing blocks except the explicitly synchronous calls (documented);
+ *     compaction batches are submitted and then polled from the host event
+ *     loop (the reference is single-threaded and never blocks:
+ *     src/storage.zig:108-131).
+ */
+#ifndef TBC_H
+#define TBC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TBC_ABI_VERSION 1u
+
+typedef enum tbc_status {
+    TBC_OK = 0,
+    TBC_PENDING = 1,              /* batch still running on the device */
+    TBC_ERR_INVALID_ARGUMENT = 2, /* a reference comptime/assert precondition is violated */
+    TBC_ERR_DEVICE = 3,           /* HIP runtime error (or no device) */
+    TBC_ERR_OUT_OF_MEMORY = 4,    /* static arena exhausted (reference panics: compaction.zig:307-318) */
+    TBC_ERR_CAPACITY = 5,         /* address list / output too small for the worst case */
+    TBC_ERR_INVARIANT = 6,        /* an input broke a reference invariant (e.g. unsorted table) */
+} tbc_status;
+
+/* Key of a tree's Value (src/lsm/groove.zig:22-76, src/lsm/composite_key.zig:7-70). */
+typedef enum tbc_key_kind {
+    TBC_KEY_TIMESTAMP = 0,      /* object tree: u64 key = timestamp & ~(1<<63) */
+    TBC_KEY_ID_U128 = 1,        /* IdTreeValue{id: u128, timestamp: u64, padding: u64} */
+    TBC_KEY_COMPOSITE_U64 = 2,  /* CompositeKey(u64){field: u64, timestamp: u64}, Key = u128 */
+    TBC_KEY_COMPOSITE_U128 = 3, /* CompositeKey(u128){field: u128, timestamp: u64, pad: u64}, Key = u256 */
+} tbc_key_kind;
+
+/* TableUsage (src/lsm/table.zig:18-32). */
+typedef enum tbc_usage {
+    TBC_USAGE_GENERAL = 0,
+    TBC_USAGE_SECONDARY_INDEX = 1,
+} tbc_usage;
+
+/* The comptime parameters of one `TableType` (src/lsm/table.zig:47-62). The
+ * derived layout (block_value_count_max, data_block_count_max, index layout)
+ * is computed exactly as table.zig:107-129 / schema.zig:119-157 do. */
+typedef struct tbc_tree {
+    uint16_t tree_id;  /* StateMachine.constants.tree_ids (src/state_machine.zig:78-111) */
+    uint8_t key_kind;  /* tbc_key_kind */
+    uint8_t usage;     /* tbc_usage */
+    uint32_t value_size;            /* @sizeOf(Value): 16, 32, 128 or 256 */
+    uint32_t timestamp_offset;      /* byte offset of the u64 timestamp (tombstone bit 63) */
+    uint32_t table_value_count_max; /* Table.value_count_max */
+} tbc_tree;
+
+/* Derived layout, as reported by tbc_tree_layout_get(). */
+typedef struct tbc_tree_layout {
+    uint32_t key_size;              /* @sizeOf(Key) */
+    uint32_t block_value_count_max; /* table.zig:116-119 */
+    uint32_t data_block_count_max;  /* table.zig:122 */
+    uint32_t index_size;            /* schema.zig:139-140 */
+    uint32_t index_checksums_offset;
+    uint32_t index_keys_min_offset;
+    uint32_t index_keys_max_offset;
+    uint32_t index_addresses_offset;
+} tbc_tree_layout;
+
+typedef struct tbc_config {
+    int32_t device;        /* HIP device ordinal */
+    uint32_t block_size;   /* constants.block_size (config.zig:139): 1 MiB prod, 4 KiB test_min */
+    uint64_t arena_bytes;  /* static device scratch arena; 0 = default (256 MiB) */
+    uint32_t flags;        /* TBC_CONFIG_* */
+    uint32_t reserved;
+} tbc_config;
+
+#define TBC_CONFIG_PROFILE 1u /* record hipEvents around every kernel (tbc_batch_kernel_times) */
+
+typedef struct tbc_engine tbc_engine;
+typedef struct tbc_batch tbc_batch;
+
+/* One input data block's values (device pointer), or a whole immutable table. */
+typedef struct tbc_segment {
+    const void *values; /* device pointer, 16-byte aligned */
+    uint32_t count;     /* number of values */
+    uint32_t reserved;
+} tbc_segment;
+
+/* One `Compaction.start(Context)` (src/lsm/compaction.zig:84-99, 280-404). */
+typedef struct tbc_compaction {
+    tbc_tree tree;
+    uint8_t a_immutable;     /* 1: table_info_a = .immutable (sorted TableMemory values, one segment) */
+    uint8_t drop_tombstones; /* Manifest.compaction_must_drop_tombstones (manifest.zig:547-574) */
+    uint8_t level_b;         /* Context.level_b (manifest label of the output tables) */
+    uint8_t reserved0;
+    uint32_t reserved1;
+    const tbc_segment *segments_a; /* host array; A's data blocks in key order (or 1 immutable segment) */
+    uint32_t segment_count_a;
+    uint32_t segment_count_b;
+    const tbc_segment *segments_b; /* host array; level-B tables' data blocks, ascending range_b order */
+    uint64_t cluster[2];           /* superblock.working.cluster (u128, little-endian words) */
+    uint64_t snapshot_min;         /* snapshot_min_for_table_output(op_min) (compaction.zig:981-985) */
+    const uint64_t *addresses;     /* host array: grid.acquire() sequence of the reservation */
+    uint32_t address_count;        /* >= (|B tables| + 1) * block_count_max, the reservation size */
+    uint32_t reserved2;
+    void *output_blocks;           /* device: address_count * block_size bytes; block i <-> addresses[i] */
+} tbc_compaction;
+
+/* Per-compaction result (after tbc_batch_poll returned TBC_OK). */
+typedef struct tbc_compaction_result {
+    uint64_t value_count;      /* values written across all output tables */
+    uint32_t data_block_count; /* data blocks written */
+    uint32_t table_count;      /* output tables (one index block each) */
+    uint32_t block_count;      /* data + index blocks = addresses consumed, in acquire order */
+    uint32_t status;           /* tbc_status of this compaction */
+} tbc_compaction_result;
+
+/* ---- engine ---------------------------------------------------------------- */
+uint32_t tbc_abi_version(void);
+tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine);
+void tbc_engine_deinit(tbc_engine *engine);
+tbc_status tbc_tree_layout_get(const tbc_engine *engine, const tbc_tree *tree, tbc_tree_layout *out_layout);
+
+/* ---- device memory (staging for the host adapter; synchronous copies) ------ */
+tbc_status tbc_device_alloc(tbc_engine *engine, uint64_t bytes, void **out_ptr);
+tbc_status tbc_device_free(tbc_engine *engine, void *ptr);
+tbc_status tbc_copy_to_device(tbc_engine *engine, void *dst, const void *src, uint64_t bytes);
+tbc_status tbc_copy_to_host(tbc_engine *engine, void *dst, const void *src, uint64_t bytes);
+tbc_status tbc_memset_device(tbc_engine *engine, void *dst, int value, uint64_t bytes);
+tbc_status tbc_synchronize(tbc_engine *engine);
+
+/* ---- vsr.checksum (src/vsr/checksum.zig:50-59) ------------------------------ */
+/* Synchronous batched AEGIS-128L checksums. messages/lengths are host arrays
+ * of device pointers; each message buffer must be readable up to its length
+ * rounded up to 4 bytes. Writes count * 16 bytes (u128 LE) to checksums_out (host). */
+tbc_status tbc_checksum_batch(tbc_engine *engine, const void *const *messages, const uint64_t *lengths,
+                              uint32_t count, uint8_t *checksums_out);
+
+/* ---- TableMemory.sort (src/lsm/table_memory.zig:140-154) ---------------------- */
+/* Synchronous stable ascending sort of `count` values (device memory) by key.
+ * A no-op when the keys are already non-decreasing (table_memory.zig:83-87). */
+tbc_status tbc_sort_values(tbc_engine *engine, const tbc_tree *tree, void *values, uint32_t count);
+/* Asynchronous variant: enqueued on the engine stream ahead of later batches. */
+tbc_status tbc_sort_values_async(tbc_engine *engine, const tbc_tree *tree, void *values, uint32_t count);
+
+/* ---- compaction ------------------------------------------------------------- */
+/* Enqueue `count` independent compactions (one half-bar's jobs) as one batch.
+ * All input/output device memory must stay valid until the batch completes. */
+tbc_status tbc_compaction_submit(tbc_engine *engine, const tbc_compaction *compactions, uint32_t count,
+                                 tbc_batch **out_batch);
+/* Non-blocking: TBC_PENDING while running, then TBC_OK or the first error. */
+tbc_status tbc_batch_poll(tbc_batch *batch);
+/* Blocking wait (tests / benchmarks only; the adapter polls). */
+tbc_status tbc_batch_wait(tbc_batch *batch);
+/* Results of compaction `index`; table_infos receives table_count entries of
+ * 128-byte schema.ManifestNode.TableInfo (src/lsm/schema.zig:489-509) encoded
+ * for Manifest.insert_table at level_b (manifest.zig:233-255). */
+tbc_status tbc_batch_result(tbc_batch *batch, uint32_t index, tbc_compaction_result *out_result,
+                            uint8_t *table_infos, uint32_t table_info_capacity);
+/* Per-kernel device times of the batch in microseconds (TBC_CONFIG_PROFILE).
+ * names/us are host arrays of `capacity` entries; returns the entry count in *out_count. */
+tbc_status tbc_batch_kernel_times(tbc_batch *batch, const char **names, double *us, uint32_t capacity,
+                                  uint32_t *out_count);
+void tbc_batch_release(tbc_batch *batch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TBC_H */

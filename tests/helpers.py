@@ -1,0 +1,125 @@
+"""Shared test helpers: run one compaction through the oracle and the GPU."""
+from __future__ import annotations
+
+import numpy as np
+
+from tigerbeetle_amd import trees, workloads
+from tigerbeetle_amd.abi import KEY_TIMESTAMP, USAGE_SECONDARY_INDEX
+
+HEADER = trees.HEADER_SIZE
+
+
+def oracle_tree(oracle, spec, block_size):
+    return oracle.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                       spec.value_count_max, block_size)
+
+
+def run_oracle(oracle, ji: workloads.JobInputs, block_size, addresses, *, level_b=1, cluster=0x1234,
+               snapshot_min=48):
+    t = oracle_tree(oracle, ji.tree, block_size)
+    vcm = t.block_value_count_max
+    return oracle.compact(t, ji.a_segments_host(vcm), ji.b_blocks_host(vcm), a_immutable=ji.a_immutable,
+                          drop_tombstones=ji.drop_tombstones, level_b=level_b, cluster=cluster,
+                          snapshot_min=snapshot_min, addresses=addresses)
+
+
+def model_merge(ji: workloads.JobInputs) -> np.ndarray:
+    """Global restatement of compaction.zig:483-804 semantics (Python, small
+    inputs): dedup A, then merge with B. Used to validate the oracle's chunked
+    loop and the GPU's element-wise formulation on the same inputs."""
+    tree = ji.tree
+    secondary = tree.usage == USAGE_SECONDARY_INDEX
+    vs = tree.value_size
+
+    def key(v):
+        limbs = workloads.keys_of(v[None, :], tree)
+        return tuple(int(l[0]) for l in reversed(limbs))
+
+    def tomb(v):
+        return bool(int(v.view(np.uint64)[tree.timestamp_offset // 8]) >> 63)
+
+    a = list(ji.a_values)
+    if ji.a_immutable:
+        out, i = [], 0
+        while i < len(a):
+            if i + 1 < len(a) and key(a[i]) == key(a[i + 1]):
+                i += 2 if secondary else 1
+            else:
+                out.append(a[i])
+                i += 1
+        a = out
+    b = [v for t in ji.b_tables for v in t]
+    res, i, j = [], 0, 0
+    while i < len(a) or j < len(b):
+        if j >= len(b) or (i < len(a) and key(a[i]) < key(b[j])):
+            if not (ji.drop_tombstones and tomb(a[i])):
+                res.append(a[i])
+            i += 1
+        elif i >= len(a) or key(a[i]) > key(b[j]):
+            res.append(b[j])
+            j += 1
+        else:
+            if not secondary and not (ji.drop_tombstones and tomb(a[i])):
+                res.append(a[i])
+            i += 1
+            j += 1
+    return np.array(res, dtype=np.uint8).reshape(-1, vs)
+
+
+def data_values_from_blocks(blocks: np.ndarray, value_size: int) -> np.ndarray:
+    """Concatenate the values of the data blocks (block_type 5) of an output."""
+    vals = []
+    for blk in blocks:
+        if blk[240] != 5:
+            continue
+        size = int(blk[96:100].view(np.uint32)[0])
+        vals.append(blk[HEADER:size].reshape(-1, value_size))
+    if not vals:
+        return np.zeros((0, value_size), dtype=np.uint8)
+    return np.concatenate(vals)
+
+
+def gpu_run(engine, jobs_inputs: list, block_size, addresses_list, *, level_b=1, cluster=0x1234,
+            snapshot_min=48):
+    """Submit several compactions as one batch; returns per job (result, infos, blocks)."""
+    from tigerbeetle_amd.engine import Job, stage_blocks
+    jobs, keep = [], []
+    for ji, addrs in zip(jobs_inputs, addresses_list):
+        lay = engine.layout(ji.tree)
+        vcm = lay.block_value_count_max
+        if ji.a_immutable:
+            if len(ji.a_values):
+                abuf = engine.upload(ji.a_values)
+                segs_a = [(abuf.ptr, len(ji.a_values))]
+                keep.append(abuf)
+            else:
+                segs_a = []
+        else:
+            blocks_a = workloads.split_blocks(ji.a_values, vcm)
+            abuf, segs_a = stage_blocks(engine, [blocks_a], ji.tree.value_size, block_size)
+            keep.append(abuf)
+        bbuf, segs_b = stage_blocks(engine, [workloads.split_blocks(t, vcm) for t in ji.b_tables],
+                                    ji.tree.value_size, block_size)
+        keep.append(bbuf)
+        out = engine.alloc(len(addrs) * block_size)
+        out.zero()
+        jobs.append(Job(ji.tree, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, level_b, cluster,
+                        snapshot_min, np.asarray(addrs, dtype=np.uint64), out))
+    batch = engine.submit(jobs)
+    batch.wait()
+    results = []
+    for i, job in enumerate(jobs):
+        r, infos = batch.result(i)
+        blocks = job.output.download(r.block_count * block_size).reshape(-1, block_size) \
+            if r.block_count else np.zeros((0, block_size), dtype=np.uint8)
+        results.append((r, infos, blocks))
+    times = batch.kernel_times() if hasattr(batch, "kernel_times") else {}
+    batch.release()
+    return results, times
+
+
+def disk_image(block: np.ndarray) -> np.ndarray:
+    """block[0..sector_ceil(size)] — the bytes the grid writes (grid.zig:686)."""
+    size = int(block[96:100].view(np.uint32)[0])
+    end = -(-size // trees.SECTOR_SIZE) * trees.SECTOR_SIZE
+    return block[:end]

@@ -1,0 +1,131 @@
+"""GPU parity: libtbc.so (HIP, gfx950) against the CPU oracle, bit-exact.
+
+Checksums are compared with the reference KATs (src/vsr/checksum.zig:94-195)
+and the oracle; compactions compare every output block's on-disk image
+(block[0..sector_ceil(size)], grid.zig:686 / storage_checker.zig:305-310)
+and every TableInfo (schema.zig:489-509) with the oracle's restatement of
+compaction.zig/table.zig.
+"""
+import numpy as np
+import pytest
+
+import zig_prng
+from helpers import disk_image, gpu_run, run_oracle
+from tigerbeetle_amd import trees, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def bswap128(x):
+    return int.from_bytes(x.to_bytes(16, "big"), "little")
+
+
+def test_checksum_test_vectors(engine):
+    got = engine.checksum([bytes(16), b""])
+    assert got[0] == bswap128(0xF72AD48DD05DD1656133101CD4BE3A26)
+    assert got[1] == 0x49F174618255402DE6E7E3C40D60CC83
+
+
+def test_checksum_stability(engine):
+    msgs = zig_prng.stability_messages()
+    cases = engine.checksum(msgs)
+    blob = b"".join(c.to_bytes(16, "little") for c in cases)
+    assert engine.checksum([blob])[0] == zig_prng.STABILITY_HASH
+
+
+def test_checksum_random_lengths(engine, oracle_lib):
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 15, 16, 17, 31, 32, 33, 240, 255, 256, 257, 1000, 4096, 65536 + 3, 1048320]
+    lens += [int(x) for x in rng.integers(1, 300_000, size=8)]
+    msgs = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    got = engine.checksum(msgs)
+    for m, g in zip(msgs, got):
+        assert g == oracle_lib.checksum(m), len(m)
+
+
+def _compare(oracle_lib, engine, cases, block_size, level_b=1):
+    """Run all cases as ONE batch on the GPU; compare each with the oracle."""
+    rng = np.random.default_rng(99)
+    inputs, addrs = [], []
+    for (spec, kw) in cases:
+        ji = workloads.make_job_inputs(spec, rng, **kw)
+        n = len(ji.a_values) + sum(len(t) for t in ji.b_tables)
+        addrs.append(workloads.addresses_for(workloads.worst_case_blocks(spec, n, block_size) + 3, rng,
+                                             int(rng.integers(1, 1000)), 0.1))
+        inputs.append(ji)
+    results, _ = gpu_run(engine, inputs, block_size, addrs, level_b=level_b)
+    for ji, a, (r, infos, blocks) in zip(inputs, addrs, results):
+        o = run_oracle(oracle_lib, ji, block_size, a, level_b=level_b)
+        assert o.status == 0
+        assert r.status == 0
+        assert (r.value_count, r.data_block_count, r.table_count, r.block_count) == \
+               (o.value_count, o.data_block_count, len(o.table_infos), len(o.blocks)), ji.tree.name
+        for i, (g, w) in enumerate(zip(blocks, o.blocks)):
+            gi, wi = disk_image(g), disk_image(w)
+            if not np.array_equal(gi, wi):
+                diff = np.nonzero(gi[: len(wi)] != wi[: len(gi)])[0]
+                raise AssertionError(f"{ji.tree.name}: block {i} differs at bytes {diff[:16]} "
+                                     f"(type {w[240]}, size {len(wi)})")
+        assert np.array_equal(infos, o.table_infos)
+
+
+SMALL = [
+    ("transfers.id", dict(n_a=2000, b_table_sizes=[700, 900, 300], a_immutable=False, overlap=0.3)),
+    ("transfers.id", dict(n_a=2500, b_table_sizes=[1200], a_immutable=True, dup_frac=0.2, tomb_frac=0.1,
+                          drop_tombstones=True, overlap=0.5)),
+    ("transfers.timestamp", dict(n_a=900, b_table_sizes=[100, 150, 90], a_immutable=True, dup_frac=0.3,
+                                 tomb_frac=0.2, overlap=0.4)),
+    ("transfers.timestamp", dict(n_a=700, b_table_sizes=[], a_immutable=False, tomb_frac=0.3,
+                                 drop_tombstones=True)),
+    ("transfers.debit_account_id", dict(n_a=3000, b_table_sizes=[800, 900], a_immutable=True, dup_frac=0.4,
+                                        drop_tombstones=True, overlap=0.3)),
+    ("accounts.ledger", dict(n_a=2600, b_table_sizes=[1500], a_immutable=True, dup_frac=0.3, overlap=0.5)),
+    ("posted.timestamp", dict(n_a=0, b_table_sizes=[900, 900], a_immutable=False, tomb_frac=0.1)),
+    ("account_history.timestamp", dict(n_a=300, b_table_sizes=[60, 90], a_immutable=True, dup_frac=0.2,
+                                       tomb_frac=0.2, drop_tombstones=True, overlap=0.3)),
+    ("transfers.amount", dict(n_a=1, b_table_sizes=[1], a_immutable=True, overlap=1.0)),
+    ("accounts.id", dict(n_a=5, b_table_sizes=[], a_immutable=True)),
+]
+
+
+def test_compaction_parity_test_min_blocks(engine_small, oracle_lib):
+    bs = 4096
+    cases = []
+    for name, kw in SMALL:
+        base = trees.BY_NAME[name]
+        # multi-block, multi-table outputs on 4 KiB blocks
+        spec = trees.with_table_size(base, 5 * (bs - 256) // base.value_size + 3)
+        cases.append((spec, kw))
+    _compare(oracle_lib, engine_small, cases, bs)
+
+
+def test_compaction_parity_production_blocks(engine, oracle_lib):
+    bs = 1 << 20
+    T = trees.BY_NAME
+    cases = [
+        (T["transfers.id"], dict(n_a=70_000, b_table_sizes=[262_080, 100_000], a_immutable=False, overlap=0.2)),
+        (T["transfers.debit_account_id"], dict(n_a=80_000, b_table_sizes=[60_000], a_immutable=True,
+                                                dup_frac=0.1, overlap=0.2, drop_tombstones=True)),
+        (T["accounts.timestamp"], dict(n_a=60_000, b_table_sizes=[50_000, 9_000], a_immutable=True,
+                                       dup_frac=0.5, tomb_frac=0.05, overlap=0.3, drop_tombstones=True)),
+        (T["accounts.user_data_32"], dict(n_a=140_000, b_table_sizes=[70_000], a_immutable=True, dup_frac=0.1,
+                                          overlap=0.1)),
+    ]
+    _compare(oracle_lib, engine, cases, bs, level_b=3)
+
+
+def test_batch_of_mixed_trees_is_independent(engine_small, oracle_lib):
+    # The same job alone and inside a batch gives identical bytes.
+    bs = 4096
+    spec = trees.with_table_size(trees.BY_NAME["transfers.code"], 1000)
+    rng = np.random.default_rng(3)
+    ji = workloads.make_job_inputs(spec, rng, n_a=1500, b_table_sizes=[400, 800], a_immutable=True,
+                                   dup_frac=0.2, overlap=0.3)
+    addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, 2700, bs) + 1, rng, 5)
+    alone, _ = gpu_run(engine_small, [ji], bs, [addrs])
+    other = workloads.make_job_inputs(trees.with_table_size(trees.BY_NAME["accounts.id"], 900), rng, n_a=800,
+                                      b_table_sizes=[300], a_immutable=False)
+    oaddrs = workloads.addresses_for(workloads.worst_case_blocks(other.tree, 1100, bs) + 1, rng, 5)
+    both, _ = gpu_run(engine_small, [other, ji], bs, [oaddrs, addrs])
+    assert np.array_equal(alone[0][2], both[1][2])
+    assert np.array_equal(alone[0][1], both[1][1])

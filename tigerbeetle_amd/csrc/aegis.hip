@@ -1,0 +1,548 @@
+// aegis.hip — AEGIS-128L block checksums and block finishing on gfx950.
+//
+// vsr.checksum (src/vsr/checksum.zig:38-85) is Zig 0.11 std
+// Aegis128LMac_128 with key = 0 and nonce = 0: the message is absorbed as
+// associated data, 32 bytes per State128L.update, zero-padded tail, then
+// finalised with LE64(len*8) || 0. It is sequential per message, so the
+// parallelism is (#messages x 32 lanes):
+//
+//   * one message per 32-lane group (two groups per wave64);
+//   * lane (p, c) owns column c (a little-endian dword) of AEGIS block p;
+//   * an AES round is four T-table lookups in LDS per lane, combined across
+//     the quad with DPP quad_perm (MixColumns/ShiftRows), no VGPR tables;
+//   * AEGIS' block rotation S'[i] = AESRound(S[i-1]) ^ S[i] is turned into a
+//     label rotation: quad p keeps its register and becomes block label+1,
+//     so the only cross-quad move is the round key S[label+1], fetched with
+//     ds_bpermute at the start of the step — off the dependency chain;
+//   * message words are prefetched 4 iterations (32 updates) ahead.
+//
+// Block finishing (Table.Builder.data_block_finish / index_block_finish,
+// src/lsm/table.zig:306-457) is fused here: body checksum, header fields,
+// header checksum, index-block body, TableInfo.
+#include <hip/hip_runtime.h>
+
+#include "tbc_internal.h"
+
+namespace tbc {
+
+// --------------------------------------------------------------------------
+// Compile-time AES T-tables and the AEGIS seed state.
+// --------------------------------------------------------------------------
+
+struct AesTables {
+    uint32_t t[4][256];
+};
+
+constexpr uint8_t xtime_c(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1B : 0)); }
+constexpr uint8_t rotl8_c(uint8_t x, int s) { return (uint8_t)((x << s) | (x >> (8 - s))); }
+
+struct Sbox {
+    uint8_t s[256];
+};
+
+constexpr Sbox make_sbox() {
+    Sbox sb{};
+    uint8_t p = 1, q = 1;
+    do {
+        p = (uint8_t)(p ^ (uint8_t)(p << 1) ^ ((p & 0x80) ? 0x1B : 0));
+        q ^= (uint8_t)(q << 1);
+        q ^= (uint8_t)(q << 2);
+        q ^= (uint8_t)(q << 4);
+        if (q & 0x80) q ^= 0x09;
+        uint8_t x = (uint8_t)(q ^ rotl8_c(q, 1) ^ rotl8_c(q, 2) ^ rotl8_c(q, 3) ^ rotl8_c(q, 4));
+        sb.s[p] = (uint8_t)(x ^ 0x63);
+    } while (p != 1);
+    sb.s[0] = 0x63;
+    return sb;
+}
+
+constexpr AesTables make_tables() {
+    AesTables t{};
+    Sbox sb = make_sbox();
+    for (int i = 0; i < 256; i++) {
+        uint32_t s = sb.s[i], s2 = xtime_c((uint8_t)s), s3 = s2 ^ s;
+        t.t[0][i] = s2 | (s << 8) | (s << 16) | (s3 << 24);
+        t.t[1][i] = s3 | (s2 << 8) | (s << 16) | (s << 24);
+        t.t[2][i] = s | (s3 << 8) | (s2 << 16) | (s << 24);
+        t.t[3][i] = s | (s << 8) | (s3 << 16) | (s2 << 24);
+    }
+    return t;
+}
+
+struct AegisSeed {
+    uint32_t s[8][4];
+};
+
+constexpr void aesenc_c(const AesTables &T, uint32_t out[4], const uint32_t in[4], const uint32_t rk[4]) {
+    for (int c = 0; c < 4; c++)
+        out[c] = T.t[0][in[c] & 0xff] ^ T.t[1][(in[(c + 1) & 3] >> 8) & 0xff] ^
+                 T.t[2][(in[(c + 2) & 3] >> 16) & 0xff] ^ T.t[3][in[(c + 3) & 3] >> 24] ^ rk[c];
+}
+
+// Aegis128LMac_128.init(key = 0): blocks [0, C1, C0, C1, 0, C0, C1, C0], then
+// 10 x update(0, 0) (checksum.zig:43-46 seed_state).
+constexpr AegisSeed make_seed() {
+    AesTables T = make_tables();
+    const uint8_t c0[16] = {0x00, 0x01, 0x01, 0x02, 0x03, 0x05, 0x08, 0x0d,
+                            0x15, 0x22, 0x37, 0x59, 0x90, 0xe9, 0x79, 0x62};
+    const uint8_t c1[16] = {0xdb, 0x3d, 0x18, 0x55, 0x6d, 0xc2, 0x2f, 0xf1,
+                            0x20, 0x11, 0x31, 0x42, 0x73, 0xb5, 0x28, 0xdd};
+    uint32_t C0[4] = {}, C1[4] = {};
+    for (int c = 0; c < 4; c++) {
+        C0[c] = c0[4 * c] | (c0[4 * c + 1] << 8) | (c0[4 * c + 2] << 16) | ((uint32_t)c0[4 * c + 3] << 24);
+        C1[c] = c1[4 * c] | (c1[4 * c + 1] << 8) | (c1[4 * c + 2] << 16) | ((uint32_t)c1[4 * c + 3] << 24);
+    }
+    AegisSeed st{};
+    for (int c = 0; c < 4; c++) {
+        st.s[1][c] = C1[c];
+        st.s[2][c] = C0[c];
+        st.s[3][c] = C1[c];
+        st.s[5][c] = C0[c];
+        st.s[6][c] = C1[c];
+        st.s[7][c] = C0[c];
+    }
+    for (int r = 0; r < 10; r++) {
+        uint32_t tmp[4] = {st.s[7][0], st.s[7][1], st.s[7][2], st.s[7][3]};
+        uint32_t n[4] = {};
+        for (int i = 7; i > 0; i--) {
+            aesenc_c(T, n, st.s[i - 1], st.s[i]);
+            for (int c = 0; c < 4; c++) st.s[i][c] = n[c];
+        }
+        aesenc_c(T, n, tmp, st.s[0]);
+        for (int c = 0; c < 4; c++) st.s[0][c] = n[c];
+    }
+    return st;
+}
+
+__constant__ AesTables c_aes = make_tables();
+__constant__ AegisSeed c_seed = make_seed();
+
+// --------------------------------------------------------------------------
+// Lane helpers.
+// --------------------------------------------------------------------------
+
+// quad_perm DPP: lane c of each quad reads lane sel[c] of the same quad.
+template <int S0, int S1, int S2, int S3>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+    constexpr int ctrl = S0 | (S1 << 2) | (S2 << 4) | (S3 << 6);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t bpermute(uint32_t byte_addr, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)byte_addr, (int)v);
+}
+
+// One AES round (no round key) of column c: T0[b0(c)] ^ T1[b1(c+1)] ^
+// T2[b2(c+2)] ^ T3[b3(c+3)]; each lane looks up its own column's four bytes
+// and the quad exchanges the partial products.
+__device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, uint32_t x) {
+    uint32_t t0 = sT[x & 0xff];
+    uint32_t t1 = sT[256 + ((x >> 8) & 0xff)];
+    uint32_t t2 = sT[512 + ((x >> 16) & 0xff)];
+    uint32_t t3 = sT[768 + (x >> 24)];
+    return t0 ^ quad_perm<1, 2, 3, 0>(t1) ^ quad_perm<2, 3, 0, 1>(t2) ^ quad_perm<3, 0, 1, 2>(t3);
+}
+
+__device__ __forceinline__ void load_tables(uint32_t *sT) {
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) sT[i] = (&c_aes.t[0][0])[i];
+}
+
+// Message sources: dword at a byte offset, zero beyond `len` (AegisMac.final
+// zero-pads the tail). Offsets are multiples of 4.
+struct GlobalMsg {
+    const uint8_t *base;
+    uint32_t len;
+    __device__ __forceinline__ uint32_t load(uint32_t off) const {
+        if (off >= len) return 0;
+        uint32_t v = *(const uint32_t *)(base + off);
+        uint32_t rem = len - off;
+        if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+        return v;
+    }
+};
+
+struct LdsMsg {
+    const uint32_t *base; // dword-aligned LDS pointer
+    uint32_t len;
+    __device__ __forceinline__ uint32_t load(uint32_t off) const {
+        if (off >= len) return 0;
+        uint32_t v = base[off >> 2];
+        uint32_t rem = len - off;
+        if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+        return v;
+    }
+};
+
+// AEGIS-128L MAC of one message per 32-lane group. Both groups of a wave
+// must have the same length (control flow is wave-uniform). Returns column c
+// of the 128-bit tag in every lane (c = lane & 3).
+template <class Msg>
+__device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &msg) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t g = lane & 31, half = lane & 32;
+    const uint32_t p = g >> 2, c = g & 3;
+    const uint32_t key_src = (half + (((p + 1) & 7) << 2) + c) << 2; // quad p+1, same column
+
+    uint32_t x = c_seed.s[p][c];
+    const uint32_t len = msg.len;
+    const uint32_t n_abs = (len + 31) >> 5;
+
+    // Which steps (u mod 4) inject a message word into this lane, and where
+    // that word sits inside each 256-byte (8-update) window.
+    const uint32_t k_lo = (3 - p) & 3;
+    const uint32_t lab_lo = (p + k_lo + 1) & 7; // 0 -> M0, 4 -> M1
+    const uint32_t off_lo = 32 * k_lo + 4 * (lab_lo + c);
+    const uint32_t off_hi = 32 * (k_lo + 4) + 4 * ((lab_lo ^ 4) + c);
+    bool need[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) need[k] = ((p + k + 1) & 3) == 0;
+
+#define AEGIS_STEP(K, WLO, WHI)                                                   \
+    do {                                                                          \
+        uint32_t key_ = bpermute(key_src, x);                                     \
+        uint32_t m_ = need[(K)&3] ? ((K) < 4 ? (WLO) : (WHI)) : 0u;               \
+        x = aes_col(sT, x) ^ (key_ ^ m_);                                         \
+    } while (0)
+
+    const uint32_t iters = n_abs >> 3;
+    uint32_t wlo[4], whi[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        wlo[d] = msg.load(256 * d + off_lo);
+        whi[d] = msg.load(256 * d + off_hi);
+    }
+    uint32_t it = 0;
+    for (; it + 4 <= iters; it += 4) {
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const uint32_t cl = wlo[d], ch = whi[d];
+            wlo[d] = msg.load(256 * (it + d + 4) + off_lo);
+            whi[d] = msg.load(256 * (it + d + 4) + off_hi);
+            AEGIS_STEP(0, cl, ch);
+            AEGIS_STEP(1, cl, ch);
+            AEGIS_STEP(2, cl, ch);
+            AEGIS_STEP(3, cl, ch);
+            AEGIS_STEP(4, cl, ch);
+            AEGIS_STEP(5, cl, ch);
+            AEGIS_STEP(6, cl, ch);
+            AEGIS_STEP(7, cl, ch);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        if (it + d < iters) {
+            const uint32_t cl = wlo[d], ch = whi[d];
+            AEGIS_STEP(0, cl, ch);
+            AEGIS_STEP(1, cl, ch);
+            AEGIS_STEP(2, cl, ch);
+            AEGIS_STEP(3, cl, ch);
+            AEGIS_STEP(4, cl, ch);
+            AEGIS_STEP(5, cl, ch);
+            AEGIS_STEP(6, cl, ch);
+            AEGIS_STEP(7, cl, ch);
+        }
+    }
+#undef AEGIS_STEP
+    // Remaining (< 8) absorb updates.
+    for (uint32_t u = iters * 8; u < n_abs; u++) {
+        const uint32_t lab = (p + u + 1) & 7;
+        const bool nd = (lab & 3) == 0;
+        uint32_t key = bpermute(key_src, x);
+        uint32_t m = nd ? msg.load(32 * u + 4 * (lab + c)) : 0u;
+        x = aes_col(sT, x) ^ (key ^ m);
+    }
+    // Finalise: tmp = (LE64(len*8) || 0) ^ S2; 7 x update(tmp, tmp).
+    const uint32_t q2 = (2 - n_abs) & 7;
+    const uint64_t bits = (uint64_t)len * 8;
+    uint32_t tmp = bpermute((half + (q2 << 2) + c) << 2, x);
+    tmp ^= c == 0 ? (uint32_t)bits : c == 1 ? (uint32_t)(bits >> 32) : 0u;
+    for (uint32_t f = 0; f < 7; f++) {
+        const uint32_t u = n_abs + f;
+        const bool nd = ((p + u + 1) & 3) == 0;
+        uint32_t key = bpermute(key_src, x);
+        x = aes_col(sT, x) ^ (key ^ (nd ? tmp : 0u));
+    }
+    // tag = S0 ^ ... ^ S6: xor over all 8 blocks, then remove block 7.
+    const uint32_t q7 = (7 - (n_abs + 7)) & 7;
+    uint32_t s7 = bpermute((half + (q7 << 2) + c) << 2, x);
+    uint32_t t = x;
+    t ^= (uint32_t)__shfl_xor((int)t, 4, 64);
+    t ^= (uint32_t)__shfl_xor((int)t, 8, 64);
+    t ^= (uint32_t)__shfl_xor((int)t, 16, 64);
+    return t ^ s7;
+}
+
+// --------------------------------------------------------------------------
+// Kernels.
+// --------------------------------------------------------------------------
+
+// tbc_checksum_batch: one message per wave (both groups compute it).
+__global__ __launch_bounds__(256) void k_checksum_batch(const uint64_t *ptrs, const uint64_t *lens, uint32_t count,
+                                                      uint8_t *out) {
+    __shared__ uint32_t sT[1024];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= count) return;
+    GlobalMsg m{(const uint8_t *)ptrs[wave], (uint32_t)lens[wave]};
+    uint32_t tag = aegis_mac32(sT, m);
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane < 4) ((uint32_t *)(out + 16 * (size_t)wave))[lane] = tag;
+}
+
+__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return *(const uint64_t *)p; }
+
+// Key (as 4 little-endian limbs) of a value; see composite_key.zig:48-50,
+// groove.zig:27-29, 59-61.
+__device__ __forceinline__ void value_key(const JobDesc &j, const uint8_t *v, uint64_t k[4]) {
+    k[1] = k[2] = k[3] = 0;
+    switch (j.key_kind) {
+    case kKeyTimestamp: k[0] = ld64(v + j.timestamp_offset) & ~kTombstoneBit; break;
+    case kKeyIdU128: k[0] = ld64(v); k[1] = ld64(v + 8); break;
+    case kKeyCompositeU64: k[0] = ld64(v + 8) & ~kTombstoneBit; k[1] = ld64(v); break;
+    default: k[0] = ld64(v + 16) & ~kTombstoneBit; k[1] = ld64(v); k[2] = ld64(v + 8); break;
+    }
+}
+
+// Header.Block dword `i` (message_header.zig:1153-1178) for a data or index block.
+struct HeaderFields {
+    uint64_t cluster_lo, cluster_hi, address, snapshot;
+    uint32_t size;
+    uint32_t meta0, meta1, meta2, meta3; // first 14 metadata bytes as dwords (u32,u32,u32,u16)
+    uint32_t block_type;
+};
+
+__device__ __forceinline__ uint32_t header_dword(const HeaderFields &h, uint32_t i, uint32_t tag_c) {
+    switch (i) {
+    case 8: case 9: case 10: case 11: return tag_c; // checksum_body (caller passes column i-8)
+    case 20: return (uint32_t)h.cluster_lo;
+    case 21: return (uint32_t)(h.cluster_lo >> 32);
+    case 22: return (uint32_t)h.cluster_hi;
+    case 23: return (uint32_t)(h.cluster_hi >> 32);
+    case 24: return h.size;
+    case 27: return 20u << 16; // version 0, command .block = 20 (vsr.zig:196), replica 0
+    case 32: return h.meta0;
+    case 33: return h.meta1;
+    case 34: return h.meta2;
+    case 35: return h.meta3;
+    case 56: return (uint32_t)h.address;
+    case 57: return (uint32_t)(h.address >> 32);
+    case 58: return (uint32_t)h.snapshot;
+    case 59: return (uint32_t)(h.snapshot >> 32);
+    case 60: return h.block_type;
+    default: return 0;
+    }
+}
+
+// Fill a 256-byte header in LDS (hdr: 64 dwords), checksum [16, 256), and
+// return the header checksum column in every lane.
+__device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *hdr, const HeaderFields &h,
+                                                  uint32_t body_tag) {
+    const uint32_t lane = threadIdx.x & 63, g = lane & 31;
+    // Lane g writes dwords g and g + 32; dwords 8..11 hold the body tag column g & 3.
+    hdr[g] = header_dword(h, g, body_tag);
+    hdr[g + 32] = header_dword(h, g + 32, body_tag);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    LdsMsg m{hdr + 4, kHeaderSize - 16};
+    uint32_t tag = aegis_mac32(sT, m);
+    return tag;
+}
+
+// Data blocks: data_block_finish (table.zig:306-384) for every output data
+// block. A wave checksums two full blocks; the last (possibly partial) block
+// of a job gets a wave of its own so both groups always share a length.
+__global__ __launch_bounds__(256) void k_data_blocks(const JobDesc *jobs, int njobs, const JobResultDev *res) {
+    __shared__ uint32_t sT[1024];
+    __shared__ uint32_t sHdr[4][2][64];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave_in_block = threadIdx.x >> 6;
+    const uint32_t wave = blockIdx.x * 4 + wave_in_block;
+    const int ji = find_job(jobs, njobs, wave, [](const JobDesc &d) { return d.dblock_base; });
+    const JobDesc &j = jobs[ji];
+    const uint32_t w = wave - j.dblock_base;
+    if (w >= j.dblock_max) return;
+    const uint32_t db = res[j.job_index].data_block_count;
+    const uint64_t n_out = res[j.job_index].value_count;
+    if (db == 0) return;
+    const uint32_t nfull = db - 1;
+    const uint32_t pair_waves = (nfull + 1) / 2;
+    uint32_t blk_lo, blk_hi;
+    if (w < pair_waves) {
+        blk_lo = 2 * w;
+        blk_hi = (2 * w + 1 < nfull) ? 2 * w + 1 : 2 * w;
+    } else if (w == pair_waves) {
+        blk_lo = blk_hi = db - 1;
+    } else {
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const bool upper = lane >= 32;
+    const uint32_t k = upper ? blk_hi : blk_lo;
+    const bool writer = !(upper && blk_hi == blk_lo);
+    const uint64_t first = (uint64_t)k * j.vcm;
+    const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
+    const uint32_t size = kHeaderSize + cnt * j.value_size;
+    const uint32_t slot = data_block_slot(k, j.dbcm);
+    uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
+
+    GlobalMsg body{blk + kHeaderSize, cnt * j.value_size};
+    const uint32_t body_tag = aegis_mac32(sT, body);
+
+    HeaderFields h;
+    h.cluster_lo = j.cluster_lo;
+    h.cluster_hi = j.cluster_hi;
+    h.address = j.addresses[slot];
+    h.snapshot = j.snapshot_min;
+    h.size = size;
+    h.meta0 = j.vcm;        // TableData.Metadata.value_count_max
+    h.meta1 = cnt;          // .value_count
+    h.meta2 = j.value_size; // .value_size
+    h.meta3 = j.tree_id;    // .tree_id (u16), reserved = 0
+    h.block_type = 5;       // BlockType.data (schema.zig:65)
+    uint32_t *hdr = sHdr[wave_in_block][upper ? 1 : 0];
+    const uint32_t hdr_tag = finish_header(sT, hdr, h, body_tag);
+    const uint32_t g = lane & 31;
+    if (g < 4) hdr[g] = hdr_tag;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (writer) {
+        uint32_t *dst = (uint32_t *)blk;
+        dst[g] = hdr[g];
+        dst[g + 32] = hdr[g + 32];
+        // Zero [size, sector_ceil(size)) (grid.zig:686).
+        const uint32_t end = (uint32_t)sector_ceil(size);
+        for (uint32_t o = size + 4 * g; o < end; o += 128) *(uint32_t *)(blk + o) = 0;
+    }
+}
+
+// Index blocks: index_block_finish (table.zig:403-457) + the TableInfo
+// manifest entry (manifest.zig:121-149, schema.zig:489-509). One table per
+// wave (both groups compute it; the lower group writes).
+constexpr uint32_t kIndexLdsBytes = 16384;
+
+__global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
+                                                     uint8_t *infos) {
+    __shared__ uint32_t sT[1024];
+    __shared__ uint32_t sIdx[kIndexLdsBytes / 4];
+    __shared__ uint64_t sKeys[2][4];
+    load_tables(sT);
+    const uint32_t wave = blockIdx.x;
+    const int ji = find_job(jobs, njobs, wave, [](const JobDesc &d) { return d.table_base; });
+    const JobDesc &j = jobs[ji];
+    const uint32_t t = wave - j.table_base;
+    const uint32_t lane = threadIdx.x & 63, g = lane & 31;
+    const uint32_t db = res[j.job_index].data_block_count;
+    const uint32_t tables = res[j.job_index].table_count;
+    if (t >= j.table_max || t >= tables) return;
+    const uint64_t n_out = res[j.job_index].value_count;
+    const uint32_t k0 = t * j.dbcm;
+    const uint32_t nblk = (db - k0) < j.dbcm ? (db - k0) : j.dbcm;
+    const uint32_t k_last = k0 + nblk - 1;
+    const uint32_t ks = j.key_size;
+    uint8_t *idx = (uint8_t *)sIdx;
+    for (uint32_t i = lane; i < j.index_size / 4; i += 64) sIdx[i] = 0;
+    __syncthreads();
+    for (uint32_t s = lane; s < nblk; s += 64) {
+        const uint32_t k = k0 + s;
+        const uint64_t first = (uint64_t)k * j.vcm;
+        const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
+        const uint32_t slot = data_block_slot(k, j.dbcm);
+        const uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
+        uint64_t kmin[4], kmax[4];
+        value_key(j, blk + kHeaderSize, kmin);
+        value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
+        uint64_t *cks = (uint64_t *)(idx + j.idx_checksums_off + 32 * s);
+        cks[0] = ld64(blk);
+        cks[1] = ld64(blk + 8);
+        for (uint32_t l = 0; l < ks / 8; l++) {
+            ((uint64_t *)(idx + j.idx_keys_min_off + ks * s))[l] = kmin[l];
+            ((uint64_t *)(idx + j.idx_keys_max_off + ks * s))[l] = kmax[l];
+        }
+        ((uint64_t *)(idx + j.idx_addresses_off))[s] = j.addresses[slot];
+        if (s == 0)
+            for (int l = 0; l < 4; l++) sKeys[0][l] = kmin[l];
+        if (s == nblk - 1)
+            for (int l = 0; l < 4; l++) sKeys[1][l] = kmax[l];
+    }
+    __syncthreads();
+    LdsMsg body{sIdx + kHeaderSize / 4, j.index_size - kHeaderSize};
+    const uint32_t body_tag = aegis_mac32(sT, body);
+    const uint32_t index_slot = index_block_slot(t, k_last);
+    HeaderFields h;
+    h.cluster_lo = j.cluster_lo;
+    h.cluster_hi = j.cluster_hi;
+    h.address = j.addresses[index_slot];
+    h.snapshot = j.snapshot_min;
+    h.size = j.index_size;
+    h.meta0 = nblk;       // TableIndex.Metadata.data_block_count
+    h.meta1 = j.dbcm;     // .data_block_count_max
+    h.meta2 = ks;         // .key_size
+    h.meta3 = j.tree_id;  // .tree_id
+    h.block_type = 4;     // BlockType.index (schema.zig:64)
+    __syncthreads();
+    const uint32_t hdr_tag = finish_header(sT, sIdx, h, body_tag);
+    __syncthreads();
+    if (lane < 4) sIdx[lane] = hdr_tag;
+    __syncthreads();
+    uint8_t *blk = j.out_blocks + (size_t)index_slot * j.block_size;
+    for (uint32_t i = lane; i < j.index_size / 4; i += 64) ((uint32_t *)blk)[i] = sIdx[i];
+    const uint32_t end = (uint32_t)sector_ceil(j.index_size);
+    for (uint32_t o = j.index_size + 4 * lane; o < end; o += 256) *(uint32_t *)(blk + o) = 0;
+
+    // ManifestNode.TableInfo (schema.zig:489-509).
+    if (lane < 32) {
+        const uint64_t vcount = (n_out - (uint64_t)k0 * j.vcm) < (uint64_t)nblk * j.vcm
+                                    ? (n_out - (uint64_t)k0 * j.vcm)
+                                    : (uint64_t)nblk * j.vcm;
+        uint32_t *info = (uint32_t *)(infos + (size_t)(j.info_base + t) * kTableInfoSize);
+        uint32_t v = 0;
+        const uint32_t i = g; // dwords 0..31
+        if (i < 8) {
+            const uint32_t l = i >> 1;
+            v = (4 * i < ks) ? (uint32_t)(sKeys[0][l] >> (32 * (i & 1))) : 0u;
+        } else if (i < 16) {
+            const uint32_t ii = i - 8, l = ii >> 1;
+            v = (4 * ii < ks) ? (uint32_t)(sKeys[1][l] >> (32 * (ii & 1))) : 0u;
+        } else if (i < 20) {
+            v = sIdx[i - 16]; // index block checksum
+        } else if (i == 24) v = (uint32_t)h.address;
+        else if (i == 25) v = (uint32_t)(h.address >> 32);
+        else if (i == 26) v = (uint32_t)j.snapshot_min;
+        else if (i == 27) v = (uint32_t)(j.snapshot_min >> 32);
+        else if (i == 28 || i == 29) v = 0xffffffffu; // snapshot_max = maxInt(u64)
+        else if (i == 30) v = (uint32_t)vcount;
+        else if (i == 31) v = (uint32_t)j.tree_id | ((uint32_t)((j.level_b & 0x3f) | (1u << 6)) << 16);
+        info[i] = v;
+    }
+}
+
+int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
+                          void *stream) {
+    if (count == 0) return 0;
+    const uint32_t blocks = (count + 3) / 4;
+    hipLaunchKernelGGL(k_checksum_batch, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_ptrs, d_lens, count,
+                       d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
+                  JobResultDev *d_results, uint8_t *d_infos, void *stream, void (*mark)(void *, const char *),
+                  void *mark_ctx) {
+    hipStream_t s = (hipStream_t)stream;
+    if (total_dblocks) {
+        hipLaunchKernelGGL(k_data_blocks, dim3((total_dblocks + 3) / 4), dim3(256), 0, s, d_jobs, njobs,
+                           (const JobResultDev *)d_results);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (mark) mark(mark_ctx, "data_blocks");
+    if (total_tables) {
+        hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(64), 0, s, d_jobs, njobs, d_results, d_infos);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (mark) mark(mark_ctx, "index_blocks");
+    return 0;
+}
+
+} // namespace tbc

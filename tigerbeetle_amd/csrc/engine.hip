@@ -1,0 +1,571 @@
+// engine.cpp — the C ABI (include/tbc.h) over the HIP kernels.
+//
+// The engine mirrors TigerBeetle's static-allocation discipline
+// (docs/TIGER_STYLE.md): one device arena and one pinned host arena are
+// allocated at init, every batch carves its descriptors, scratch and result
+// buffers out of them, and nothing is allocated on the hot path. A batch is
+// all of a half-bar's compactions (Forest.compact -> Groove.compact ->
+// Tree.compact, src/lsm/forest.zig:319-342) submitted at once; the host event
+// loop polls it (hipEventQuery) instead of blocking, like the reference's
+// callback loop (src/storage.zig:108-131).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/tbc.h"
+#include "tbc_internal.h"
+
+using namespace tbc;
+
+namespace {
+
+constexpr uint64_t kDefaultArena = 256ull << 20;
+constexpr uint64_t kPinnedArena = 64ull << 20;
+constexpr uint32_t kIndexLdsMax = 16384; // k_index_blocks LDS image
+constexpr int kMaxMarks = 16;
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+struct Arena {
+    uint8_t *base = nullptr;
+    uint64_t size = 0, top = 0;
+    uint32_t live = 0;
+    uint8_t *alloc(uint64_t bytes) {
+        uint64_t start = align_up(top, 256);
+        if (start + bytes > size) return nullptr;
+        top = start + bytes;
+        return base + start;
+    }
+};
+
+struct Layout {
+    uint32_t key_size, vcm, dbcm, index_size;
+    uint32_t cks_off, kmin_off, kmax_off, addr_off;
+};
+
+bool compute_layout(const tbc_tree *t, uint32_t block_size, Layout *L) {
+    if (!t || t->tree_id == 0 || t->key_kind > TBC_KEY_COMPOSITE_U128 || t->usage > TBC_USAGE_SECONDARY_INDEX)
+        return false;
+    const uint32_t vs = t->value_size;
+    if (vs < 16 || (vs & (vs - 1)) || t->timestamp_offset + 8 > vs || (t->timestamp_offset & 7)) return false;
+    if (t->table_value_count_max == 0) return false;
+    const uint32_t key_size = t->key_kind == TBC_KEY_TIMESTAMP ? 8 : t->key_kind == TBC_KEY_COMPOSITE_U128 ? 32 : 16;
+    // Value layouts fixed by the key kind (groove.zig:48-56, composite_key.zig:17-46).
+    if (t->key_kind == TBC_KEY_ID_U128 && (vs != 32 || t->timestamp_offset != 16)) return false;
+    if (t->key_kind == TBC_KEY_COMPOSITE_U64 && (vs != 16 || t->timestamp_offset != 8)) return false;
+    if (t->key_kind == TBC_KEY_COMPOSITE_U128 && (vs != 32 || t->timestamp_offset != 16)) return false;
+    const uint32_t body = block_size - kHeaderSize;
+    const uint32_t vcm = body / vs; // table.zig:116-119
+    if (vcm == 0) return false;
+    const uint32_t dbcm = (t->table_value_count_max + vcm - 1) / vcm; // table.zig:122
+    if (dbcm > body / (32 + 8)) return false;                          // constants.zig:567-574
+    L->key_size = key_size;
+    L->vcm = vcm;
+    L->dbcm = dbcm;
+    L->cks_off = kHeaderSize;
+    L->kmin_off = kHeaderSize + dbcm * 32;
+    L->kmax_off = L->kmin_off + dbcm * key_size;
+    L->addr_off = L->kmax_off + dbcm * key_size;
+    L->index_size = L->addr_off + dbcm * 8; // schema.zig:139-140
+    return L->index_size <= block_size;
+}
+
+} // namespace
+
+struct tbc_engine {
+    int device = 0;
+    uint32_t block_size = 0;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    Arena dev, host;
+    std::vector<hipEvent_t> event_pool;
+};
+
+struct tbc_batch {
+    tbc_engine *engine = nullptr;
+    uint32_t count = 0;
+    uint8_t *dev_mark = nullptr, *host_mark = nullptr; // arena tops to restore on release
+    uint64_t dev_top = 0, host_top = 0;
+    JobResultDev *h_results = nullptr;
+    uint8_t *h_infos = nullptr;
+    std::vector<uint32_t> info_base; // per original job index
+    std::vector<uint32_t> status;    // host-side validation status per job
+    hipEvent_t done = nullptr;
+    hipEvent_t marks[kMaxMarks] = {};
+    const char *mark_names[kMaxMarks] = {};
+    int nmarks = 0;
+    bool complete = false;
+    tbc_status result = TBC_PENDING;
+};
+
+static void mark_cb(void *ctx, const char *name) {
+    tbc_batch *b = (tbc_batch *)ctx;
+    if (!(b->engine->flags & TBC_CONFIG_PROFILE) || b->nmarks >= kMaxMarks) return;
+    hipEventRecord(b->marks[b->nmarks], b->engine->stream);
+    b->mark_names[b->nmarks++] = name;
+}
+
+extern "C" {
+
+uint32_t tbc_abi_version(void) { return TBC_ABI_VERSION; }
+
+tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
+    if (!config || !out_engine) return TBC_ERR_INVALID_ARGUMENT;
+    *out_engine = nullptr;
+    const uint32_t bs = config->block_size;
+    if (bs < kSectorSize || (bs & (bs - 1)) || bs % kSectorSize) return TBC_ERR_INVALID_ARGUMENT;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= config->device || config->device < 0)
+        return TBC_ERR_DEVICE;
+    if (hipSetDevice(config->device) != hipSuccess) return TBC_ERR_DEVICE;
+    tbc_engine *e = new (std::nothrow) tbc_engine();
+    if (!e) return TBC_ERR_OUT_OF_MEMORY;
+    e->device = config->device;
+    e->block_size = bs;
+    e->flags = config->flags;
+    e->dev.size = config->arena_bytes ? config->arena_bytes : kDefaultArena;
+    e->host.size = kPinnedArena;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return TBC_ERR_DEVICE;
+    }
+    if (hipMalloc((void **)&e->dev.base, e->dev.size) != hipSuccess) {
+        hipStreamDestroy(e->stream);
+        delete e;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    if (hipHostMalloc((void **)&e->host.base, e->host.size, hipHostMallocDefault) != hipSuccess) {
+        hipFree(e->dev.base);
+        hipStreamDestroy(e->stream);
+        delete e;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    *out_engine = e;
+    return TBC_OK;
+}
+
+void tbc_engine_deinit(tbc_engine *e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    hipStreamSynchronize(e->stream);
+    for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
+    hipHostFree(e->host.base);
+    hipFree(e->dev.base);
+    hipStreamDestroy(e->stream);
+    delete e;
+}
+
+tbc_status tbc_tree_layout_get(const tbc_engine *e, const tbc_tree *tree, tbc_tree_layout *out) {
+    if (!e || !tree || !out) return TBC_ERR_INVALID_ARGUMENT;
+    Layout L;
+    if (!compute_layout(tree, e->block_size, &L)) return TBC_ERR_INVALID_ARGUMENT;
+    out->key_size = L.key_size;
+    out->block_value_count_max = L.vcm;
+    out->data_block_count_max = L.dbcm;
+    out->index_size = L.index_size;
+    out->index_checksums_offset = L.cks_off;
+    out->index_keys_min_offset = L.kmin_off;
+    out->index_keys_max_offset = L.kmax_off;
+    out->index_addresses_offset = L.addr_off;
+    return TBC_OK;
+}
+
+tbc_status tbc_device_alloc(tbc_engine *e, uint64_t bytes, void **out_ptr) {
+    if (!e || !out_ptr) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    return hipMalloc(out_ptr, bytes ? bytes : 1) == hipSuccess ? TBC_OK : TBC_ERR_OUT_OF_MEMORY;
+}
+
+tbc_status tbc_device_free(tbc_engine *e, void *ptr) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    return hipFree(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    if (!bytes) return TBC_OK;
+    hipSetDevice(e->device);
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    if (!bytes) return TBC_OK;
+    hipSetDevice(e->device);
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    if (!bytes) return TBC_OK;
+    hipSetDevice(e->device);
+    if (hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_synchronize(tbc_engine *e) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const uint64_t *lengths, uint32_t count,
+                              uint8_t *checksums_out) {
+    if (!e || (count && (!messages || !lengths || !checksums_out))) return TBC_ERR_INVALID_ARGUMENT;
+    if (!count) return TBC_OK;
+    for (uint32_t i = 0; i < count; i++)
+        if (lengths[i] > 0xffffffffull || (lengths[i] && !messages[i])) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    const uint64_t dt = e->dev.top, ht = e->host.top;
+    uint8_t *d = e->dev.alloc(16ull * count + 16ull * count);
+    uint8_t *h = e->host.alloc(16ull * count + 16ull * count);
+    if (!d || !h) {
+        e->dev.top = dt;
+        e->host.top = ht;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    uint64_t *hp = (uint64_t *)h;
+    uint64_t *hl = hp + count;
+    for (uint32_t i = 0; i < count; i++) {
+        hp[i] = (uint64_t)(uintptr_t)messages[i];
+        hl[i] = lengths[i];
+    }
+    tbc_status st = TBC_OK;
+    if (hipMemcpyAsync(d, h, 16ull * count, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        launch_checksum_batch((const uint64_t *)d, (const uint64_t *)d + count, count, d + 16ull * count,
+                              e->stream) != 0 ||
+        hipMemcpyAsync(h + 16ull * count, d + 16ull * count, 16ull * count, hipMemcpyDeviceToHost, e->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        st = TBC_ERR_DEVICE;
+    if (st == TBC_OK) memcpy(checksums_out, h + 16ull * count, 16ull * count);
+    e->dev.top = dt;
+    e->host.top = ht;
+    return st;
+}
+
+tbc_status tbc_sort_values_async(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
+    if (!e || !tree || (count && !values)) return TBC_ERR_INVALID_ARGUMENT;
+    Layout L;
+    if (!compute_layout(tree, e->block_size, &L)) return TBC_ERR_INVALID_ARGUMENT;
+    if (count < 2) return TBC_OK;
+    hipSetDevice(e->device);
+    const uint64_t need = sort_scratch_bytes(tree->value_size, count);
+    const uint64_t dt = e->dev.top;
+    uint8_t *scratch = e->dev.alloc(need);
+    if (!scratch) return TBC_ERR_OUT_OF_MEMORY;
+    int rc = launch_sort(tree->key_kind, tree->value_size, tree->timestamp_offset, values, count, scratch, need,
+                         e->stream);
+    // Stream order protects the scratch: the next user of this arena range is
+    // enqueued on the same stream after the sort.
+    e->dev.top = dt;
+    return rc == 0 ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
+    tbc_status st = tbc_sort_values_async(e, tree, values, count);
+    if (st != TBC_OK) return st;
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
+    if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    hipSetDevice(e->device);
+    tbc_batch *b = new (std::nothrow) tbc_batch();
+    if (!b) return TBC_ERR_OUT_OF_MEMORY;
+    b->engine = e;
+    b->count = count;
+    b->info_base.resize(count);
+    b->status.assign(count, TBC_OK);
+
+    // Validate and describe each compaction (host side of Compaction.start).
+    std::vector<JobDesc> hj(count);
+    std::vector<uint32_t> order(count);
+    uint64_t seg_words = 0, addr_words = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        const tbc_compaction &c = jobs_in[i];
+        JobDesc &d = hj[i];
+        memset(&d, 0, sizeof d);
+        Layout L;
+        if (!compute_layout(&c.tree, e->block_size, &L) || L.index_size > kIndexLdsMax ||
+            (c.a_immutable && c.segment_count_a > 1) || !c.output_blocks ||
+            (c.segment_count_a && !c.segments_a) || (c.segment_count_b && !c.segments_b) ||
+            (c.address_count && !c.addresses)) {
+            delete b;
+            return TBC_ERR_INVALID_ARGUMENT;
+        }
+        uint64_t na = 0, nb = 0;
+        for (uint32_t s = 0; s < c.segment_count_a; s++) {
+            const tbc_segment &g = c.segments_a[s];
+            if (!g.count || !g.values || ((uintptr_t)g.values & 15)) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
+            na += g.count;
+        }
+        for (uint32_t s = 0; s < c.segment_count_b; s++) {
+            const tbc_segment &g = c.segments_b[s];
+            if (!g.count || !g.values || ((uintptr_t)g.values & 15)) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
+            nb += g.count;
+        }
+        if (na + nb > 0xffff0000ull) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
+        const uint64_t n = na + nb;
+        const uint64_t db_max = (n + L.vcm - 1) / L.vcm;
+        const uint64_t tables_max = (db_max + L.dbcm - 1) / L.dbcm;
+        if (db_max + tables_max > c.address_count) { delete b; return TBC_ERR_CAPACITY; }
+        d.key_kind = c.tree.key_kind;
+        d.usage = c.tree.usage;
+        d.value_size = c.tree.value_size;
+        d.timestamp_offset = c.tree.timestamp_offset;
+        d.key_size = L.key_size;
+        d.vcm = L.vcm;
+        d.dbcm = L.dbcm;
+        d.index_size = L.index_size;
+        d.idx_checksums_off = L.cks_off;
+        d.idx_keys_min_off = L.kmin_off;
+        d.idx_keys_max_off = L.kmax_off;
+        d.idx_addresses_off = L.addr_off;
+        d.block_size = e->block_size;
+        d.tree_id = c.tree.tree_id;
+        d.a_immutable = c.a_immutable ? 1 : 0;
+        d.drop_tombstones = c.drop_tombstones ? 1 : 0;
+        d.level_b = c.level_b;
+        d.cluster_lo = c.cluster[0];
+        d.cluster_hi = c.cluster[1];
+        d.snapshot_min = c.snapshot_min;
+        d.a.nseg = c.segment_count_a;
+        d.a.n = (uint32_t)na;
+        d.b.nseg = c.segment_count_b;
+        d.b.n = (uint32_t)nb;
+        d.address_count = c.address_count;
+        d.out_blocks = (uint8_t *)c.output_blocks;
+        d.tile_count = (uint32_t)((n + kMergeTile - 1) / kMergeTile);
+        d.dblock_max = db_max ? (uint32_t)((db_max - 1 + 1) / 2 + 1) : 0;
+        d.table_max = (uint32_t)tables_max;
+        d.job_index = i;
+        seg_words += 2ull * (c.segment_count_a + c.segment_count_b) + 2;
+        addr_words += c.address_count;
+        order[i] = i;
+    }
+    // Group jobs by key kind (one kernel instantiation per kind) and assign
+    // batch-wide bases in that order.
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hj[x].key_kind < hj[y].key_kind; });
+    std::vector<JobDesc> sj(count);
+    uint32_t tiles = 0, splits = 0, dblocks = 0, tables = 0, infos = 0;
+    for (uint32_t k = 0; k < count; k++) {
+        sj[k] = hj[order[k]];
+        JobDesc &d = sj[k];
+        d.tile_base = tiles;
+        d.split_base = splits;
+        d.dblock_base = dblocks;
+        d.table_base = tables;
+        d.info_base = infos;
+        b->info_base[d.job_index] = infos;
+        tiles += d.tile_count;
+        splits += d.tile_count + 1;
+        dblocks += d.dblock_max;
+        tables += d.table_max;
+        infos += d.table_max;
+    }
+
+    // Device layout of the batch.
+    const uint64_t sz_jobs = align_up(sizeof(JobDesc) * (uint64_t)count, 256);
+    const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
+    const uint64_t sz_addr = align_up(8 * addr_words, 256);
+    const uint64_t sz_in = sz_jobs + sz_segs + sz_addr;
+    const uint64_t sz_splits = align_up(4ull * splits, 256);
+    const uint64_t sz_tiles = align_up(4ull * tiles + 4, 256);
+    const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
+    const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
+    b->dev_top = e->dev.top;
+    b->host_top = e->host.top;
+    uint8_t *dbase = e->dev.alloc(sz_in + sz_splits + sz_tiles + sz_res + sz_infos);
+    uint8_t *hbase = e->host.alloc(sz_in + sz_res + sz_infos);
+    if (!dbase || !hbase) {
+        e->dev.top = b->dev_top;
+        e->host.top = b->host_top;
+        delete b;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    e->dev.live++;
+    e->host.live++;
+    uint8_t *d_in = dbase;
+    uint32_t *d_splits = (uint32_t *)(dbase + sz_in);
+    uint32_t *d_tiles = (uint32_t *)(dbase + sz_in + sz_splits);
+    JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
+    uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
+    b->h_results = (JobResultDev *)(hbase + sz_in);
+    b->h_infos = hbase + sz_in + sz_res;
+
+    // Fill the staging image: segment pointers/prefixes and addresses, with
+    // device addresses patched into the job descriptors.
+    uint8_t *h_in = hbase;
+    uint64_t *hseg = (uint64_t *)(h_in + sz_jobs);
+    const uint64_t seg_ptr_words = seg_words;
+    uint32_t *hpre = (uint32_t *)(hseg + seg_ptr_words);
+    uint64_t *haddr = (uint64_t *)(h_in + sz_jobs + sz_segs);
+    const uint64_t dev_seg = (uint64_t)(uintptr_t)(d_in + sz_jobs);
+    const uint64_t dev_pre = dev_seg + 8 * seg_ptr_words;
+    const uint64_t dev_addr = (uint64_t)(uintptr_t)(d_in + sz_jobs + sz_segs);
+    uint64_t sp = 0, ap = 0;
+    for (uint32_t k = 0; k < count; k++) {
+        JobDesc &d = sj[k];
+        const tbc_compaction &c = jobs_in[d.job_index];
+        for (int side = 0; side < 2; side++) {
+            const tbc_segment *segs = side == 0 ? c.segments_a : c.segments_b;
+            const uint32_t ns = side == 0 ? c.segment_count_a : c.segment_count_b;
+            Stream &st = side == 0 ? d.a : d.b;
+            st.seg_ptr = (const uint64_t *)(uintptr_t)(dev_seg + 8 * sp);
+            st.seg_pre = (const uint32_t *)(uintptr_t)(dev_pre + 4 * sp);
+            uint32_t pre = 0;
+            for (uint32_t s = 0; s < ns; s++) {
+                hseg[sp + s] = (uint64_t)(uintptr_t)segs[s].values;
+                hpre[sp + s] = pre;
+                pre += segs[s].count;
+            }
+            hpre[sp + ns] = pre;
+            sp += ns + 1;
+        }
+        d.addresses = (const uint64_t *)(uintptr_t)(dev_addr + 8 * ap);
+        memcpy(haddr + ap, c.addresses, 8ull * c.address_count);
+        ap += c.address_count;
+    }
+    memcpy(h_in, sj.data(), sizeof(JobDesc) * count);
+
+    for (int m = 0; m < kMaxMarks; m++) {
+        if (e->flags & TBC_CONFIG_PROFILE) {
+            if (e->event_pool.empty()) {
+                hipEvent_t ev;
+                hipEventCreate(&ev);
+                e->event_pool.push_back(ev);
+            }
+            b->marks[m] = e->event_pool.back();
+            e->event_pool.pop_back();
+        }
+    }
+    if (e->event_pool.empty()) {
+        hipEvent_t ev;
+        hipEventCreate(&ev);
+        e->event_pool.push_back(ev);
+    }
+    b->done = e->event_pool.back();
+    e->event_pool.pop_back();
+
+    hipStream_t s = e->stream;
+    bool ok = hipMemcpyAsync(d_in, h_in, sz_in, hipMemcpyHostToDevice, s) == hipSuccess;
+    ok = ok && hipMemsetAsync(d_res, 0, sz_res, s) == hipSuccess;
+    mark_cb(b, "start");
+    if (ok && count)
+        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, tiles, splits, d_splits, d_tiles, d_res, s,
+                          mark_cb, b) == 0;
+    if (ok && count)
+        ok = launch_blocks((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, s, mark_cb, b) == 0;
+    ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
+    ok = ok && hipEventRecord(b->done, s) == hipSuccess;
+    if (!ok) {
+        hipStreamSynchronize(s);
+        tbc_batch_release(b);
+        return TBC_ERR_DEVICE;
+    }
+    *out = b;
+    return TBC_OK;
+}
+
+static tbc_status batch_finish(tbc_batch *b) {
+    b->complete = true;
+    b->result = TBC_OK;
+    for (uint32_t i = 0; i < b->count; i++) {
+        JobResultDev &r = b->h_results[i];
+        if (r.invariant) r.status = TBC_ERR_INVARIANT;
+        if (r.status != TBC_OK && b->result == TBC_OK) b->result = (tbc_status)r.status;
+    }
+    return b->result;
+}
+
+tbc_status tbc_batch_poll(tbc_batch *b) {
+    if (!b) return TBC_ERR_INVALID_ARGUMENT;
+    if (b->complete) return b->result;
+    hipSetDevice(b->engine->device);
+    hipError_t q = hipEventQuery(b->done);
+    if (q == hipErrorNotReady) return TBC_PENDING;
+    if (q != hipSuccess) {
+        b->complete = true;
+        b->result = TBC_ERR_DEVICE;
+        return b->result;
+    }
+    return batch_finish(b);
+}
+
+tbc_status tbc_batch_wait(tbc_batch *b) {
+    if (!b) return TBC_ERR_INVALID_ARGUMENT;
+    if (b->complete) return b->result;
+    hipSetDevice(b->engine->device);
+    if (hipEventSynchronize(b->done) != hipSuccess) {
+        b->complete = true;
+        b->result = TBC_ERR_DEVICE;
+        return b->result;
+    }
+    return batch_finish(b);
+}
+
+tbc_status tbc_batch_result(tbc_batch *b, uint32_t index, tbc_compaction_result *out, uint8_t *table_infos,
+                            uint32_t table_info_capacity) {
+    if (!b || !out || index >= b->count) return TBC_ERR_INVALID_ARGUMENT;
+    if (!b->complete) return TBC_PENDING;
+    if (b->result == TBC_ERR_DEVICE) return TBC_ERR_DEVICE;
+    const JobResultDev &r = b->h_results[index];
+    out->value_count = r.value_count;
+    out->data_block_count = r.data_block_count;
+    out->table_count = r.table_count;
+    out->block_count = r.block_count;
+    out->status = r.status;
+    if (table_infos) {
+        if (table_info_capacity < r.table_count) return TBC_ERR_CAPACITY;
+        memcpy(table_infos, b->h_infos + (size_t)b->info_base[index] * kTableInfoSize,
+               (size_t)r.table_count * kTableInfoSize);
+    }
+    return TBC_OK;
+}
+
+tbc_status tbc_batch_kernel_times(tbc_batch *b, const char **names, double *us, uint32_t capacity,
+                                  uint32_t *out_count) {
+    if (!b || !out_count) return TBC_ERR_INVALID_ARGUMENT;
+    if (!b->complete) return TBC_PENDING;
+    uint32_t n = 0;
+    for (int m = 1; m < b->nmarks && n < capacity; m++) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, b->marks[m - 1], b->marks[m]) != hipSuccess) return TBC_ERR_DEVICE;
+        if (names) names[n] = b->mark_names[m];
+        if (us) us[n] = ms * 1000.0;
+        n++;
+    }
+    *out_count = n;
+    return TBC_OK;
+}
+
+void tbc_batch_release(tbc_batch *b) {
+    if (!b) return;
+    tbc_engine *e = b->engine;
+    hipSetDevice(e->device);
+    if (!b->complete && b->done) hipEventSynchronize(b->done);
+    for (int m = 0; m < kMaxMarks; m++)
+        if (b->marks[m]) e->event_pool.push_back(b->marks[m]);
+    if (b->done) e->event_pool.push_back(b->done);
+    if (b->h_results) {
+        // LIFO release restores the arena tops; otherwise reclaim when idle.
+        if (e->dev.live) e->dev.live--;
+        if (e->host.live) e->host.live--;
+        if (e->dev.live == 0) e->dev.top = 0;
+        else e->dev.top = std::min(e->dev.top, std::max(b->dev_top, e->dev.top));
+        if (e->host.live == 0) e->host.top = 0;
+    }
+    delete b;
+}
+
+} // extern "C"

@@ -1,0 +1,108 @@
+// tbc_internal.h — device/host shared definitions of the compaction engine.
+//
+// Layout of one batch in device memory (all in the engine's static arena):
+//   JobDesc[count]          per-compaction descriptor (tree layout, streams, bases)
+//   u64 seg_ptr[...]        per-stream segment value pointers
+//   u32 seg_pre[...]        per-stream segment prefix counts (nseg + 1 each)
+//   u64 addresses[...]      acquire-order block addresses per job
+//   u32 splits[...]         merge-path A-splits at every tile boundary (tiles + 1 per job)
+//   u32 tile_counts[...]    survivors per tile, then exclusive tile offsets
+//   JobResultDev[count]     device results (copied to pinned host memory at the end)
+//   u8  table_infos[...]    128-byte ManifestNode.TableInfo per output table
+#pragma once
+
+#include <stdint.h>
+
+namespace tbc {
+
+constexpr uint32_t kHeaderSize = 256;  // @sizeOf(vsr.Header) (message_header.zig:68)
+constexpr uint32_t kSectorSize = 4096; // constants.sector_size (constants.zig:418)
+constexpr uint32_t kTableInfoSize = 128;
+constexpr uint64_t kTombstoneBit = 1ull << 63;
+
+// Merge tile: merged-sequence positions handled by one workgroup.
+constexpr uint32_t kMergeTile = 1024;
+constexpr uint32_t kMergeThreads = 256;
+
+enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };
+
+struct Stream {
+    const uint64_t *seg_ptr; // device pointer of each segment's first value
+    const uint32_t *seg_pre; // prefix counts, nseg + 1 entries
+    uint32_t nseg;
+    uint32_t n; // total values
+};
+
+struct JobDesc {
+    // Tree layout (table.zig:107-129, schema.zig:119-157).
+    uint32_t key_kind, usage, value_size, timestamp_offset;
+    uint32_t key_size, vcm, dbcm, index_size;
+    uint32_t idx_checksums_off, idx_keys_min_off, idx_keys_max_off, idx_addresses_off;
+    uint32_t block_size;
+    uint16_t tree_id;
+    uint8_t a_immutable, drop_tombstones;
+    uint8_t level_b, pad0[3];
+    uint64_t cluster_lo, cluster_hi, snapshot_min;
+    Stream a, b;
+    const uint64_t *addresses;
+    uint32_t address_count;
+    uint32_t pad1;
+    uint8_t *out_blocks;
+    // Batch bases (global grid indices).
+    uint32_t tile_base, tile_count;      // merge tiles
+    uint32_t split_base;                 // tile_count + 1 splits
+    uint32_t dblock_base, dblock_max;    // data-block checksum groups (upper bound)
+    uint32_t table_base, table_max;      // index-block groups (upper bound)
+    uint32_t info_base;                  // first TableInfo slot in the batch's info buffer
+    uint32_t job_index;
+};
+
+struct JobResultDev {
+    uint64_t value_count;
+    uint32_t data_block_count;
+    uint32_t table_count;
+    uint32_t block_count;
+    uint32_t status;
+    uint32_t invariant; // nonzero if an input broke a reference invariant
+    uint32_t pad;
+};
+
+// Slot (= index into the acquire-order address list / output arena) of data
+// block `k`: every earlier table consumed dbcm data blocks plus one index block.
+__host__ __device__ inline uint32_t data_block_slot(uint32_t k, uint32_t dbcm) { return k + k / dbcm; }
+// Slot of the index block of table `t` whose last data block is `k_last`.
+__host__ __device__ inline uint32_t index_block_slot(uint32_t t, uint32_t k_last) { return k_last + t + 1; }
+
+__host__ __device__ inline uint64_t sector_ceil(uint64_t x) {
+    return (x + kSectorSize - 1) / kSectorSize * kSectorSize;
+}
+
+// Find the job owning global index `g` given a per-job base field (ascending).
+template <class F>
+__device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F base_of) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (base_of(jobs[mid]) <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+} // namespace tbc
+
+// Kernel launchers (implemented in the .hip translation units).
+struct hipStream_t_;
+namespace tbc {
+int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, uint32_t total_tiles,
+                 uint32_t total_splits, uint32_t *d_splits, uint32_t *d_tile_counts,
+                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
+                  JobResultDev *d_results, uint8_t *d_infos, void *stream,
+                  void (*mark)(void *, const char *), void *mark_ctx);
+int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
+                          void *stream);
+int launch_sort(uint32_t key_kind, uint32_t value_size, uint32_t timestamp_offset, void *values, uint32_t n,
+                void *scratch, uint64_t scratch_bytes, void *stream);
+uint64_t sort_scratch_bytes(uint32_t value_size, uint32_t n);
+} // namespace tbc

@@ -1,0 +1,235 @@
+"""Host-side driver of the GPU compaction engine over the C ABI.
+
+`Engine` owns one libtbc engine (a HIP stream plus static device/pinned
+arenas) on one GPU. It is the plumbing used by tests and the benchmark; the
+production host adapter is the Zig `@cImport` of include/tbc.h (see
+INTEGRATION.md) or the C++ mirror in tigerbeetle_amd/host/.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .abi import check, lib
+from .trees import BLOCK_SIZE, HEADER_SIZE, TreeSpec
+
+
+class DeviceBuffer:
+    """A device allocation (hipMalloc via tbc_device_alloc)."""
+
+    def __init__(self, engine: "Engine", nbytes: int):
+        self.engine = engine
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().tbc_device_alloc(engine.handle, max(1, self.nbytes), ctypes.byref(p)), "tbc_device_alloc")
+        self.ptr = p.value
+
+    def upload(self, array: np.ndarray, offset: int = 0) -> None:
+        a = np.ascontiguousarray(array)
+        assert offset + a.nbytes <= self.nbytes
+        check(lib().tbc_copy_to_device(self.engine.handle, self.ptr + offset, a.ctypes.data, a.nbytes),
+              "tbc_copy_to_device")
+
+    def download(self, nbytes: int | None = None, offset: int = 0) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, dtype=np.uint8)
+        check(lib().tbc_copy_to_host(self.engine.handle, out.ctypes.data, self.ptr + offset, n),
+              "tbc_copy_to_host")
+        return out
+
+    def zero(self) -> None:
+        check(lib().tbc_memset_device(self.engine.handle, self.ptr, 0, self.nbytes), "tbc_memset_device")
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().tbc_device_free(self.engine.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ptr and self.engine.handle:
+                self.free()
+        except Exception:
+            pass
+
+
+@dataclass
+class Job:
+    """One Compaction.start(Context) (src/lsm/compaction.zig:84-99)."""
+    tree: TreeSpec
+    segments_a: list  # [(device_ptr, count)]
+    segments_b: list
+    a_immutable: bool
+    drop_tombstones: bool
+    level_b: int
+    cluster: int
+    snapshot_min: int
+    addresses: np.ndarray  # uint64, acquire order
+    output: DeviceBuffer
+    _keep: list = field(default_factory=list)
+
+    def ctype(self) -> abi.Compaction:
+        c = abi.Compaction()
+        c.tree = self.tree.ctype()
+        c.a_immutable = int(self.a_immutable)
+        c.drop_tombstones = int(self.drop_tombstones)
+        c.level_b = self.level_b
+        sa = (abi.Segment * max(1, len(self.segments_a)))()
+        for i, (p, n) in enumerate(self.segments_a):
+            sa[i].values, sa[i].count = p, n
+        sb = (abi.Segment * max(1, len(self.segments_b)))()
+        for i, (p, n) in enumerate(self.segments_b):
+            sb[i].values, sb[i].count = p, n
+        addrs = np.ascontiguousarray(self.addresses, dtype=np.uint64)
+        self._keep = [sa, sb, addrs]
+        c.segments_a = ctypes.cast(sa, ctypes.POINTER(abi.Segment))
+        c.segment_count_a = len(self.segments_a)
+        c.segments_b = ctypes.cast(sb, ctypes.POINTER(abi.Segment))
+        c.segment_count_b = len(self.segments_b)
+        c.cluster[0] = self.cluster & ((1 << 64) - 1)
+        c.cluster[1] = self.cluster >> 64
+        c.snapshot_min = self.snapshot_min
+        c.addresses = addrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        c.address_count = len(addrs)
+        c.output_blocks = self.output.ptr
+        return c
+
+
+class Batch:
+    def __init__(self, engine: "Engine", handle: int, jobs: list):
+        self.engine, self.handle, self.jobs = engine, handle, jobs
+
+    def poll(self) -> int:
+        return lib().tbc_batch_poll(self.handle)
+
+    def wait(self) -> None:
+        check(lib().tbc_batch_wait(self.handle), "tbc_batch_wait")
+
+    def result(self, index: int):
+        r = abi.CompactionResult()
+        check(lib().tbc_batch_result(self.handle, index, ctypes.byref(r), None, 0), "tbc_batch_result")
+        infos = np.zeros((max(1, r.table_count), 128), dtype=np.uint8)
+        check(lib().tbc_batch_result(self.handle, index, ctypes.byref(r), infos.ctypes.data, r.table_count),
+              "tbc_batch_result")
+        return r, infos[: r.table_count]
+
+    def kernel_times(self) -> dict:
+        cap = 32
+        names = (ctypes.c_char_p * cap)()
+        us = (ctypes.c_double * cap)()
+        n = ctypes.c_uint32()
+        check(lib().tbc_batch_kernel_times(self.handle, names, us, cap, ctypes.byref(n)), "kernel_times")
+        out: dict = {}
+        for i in range(n.value):
+            k = names[i].decode()
+            out[k] = out.get(k, 0.0) + us[i]
+        return out
+
+    def release(self) -> None:
+        if self.handle:
+            lib().tbc_batch_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+class Engine:
+    def __init__(self, device: int = 0, block_size: int = BLOCK_SIZE, arena_bytes: int = 0,
+                 profile: bool = False):
+        cfg = abi.Config(device, block_size, arena_bytes, abi.CONFIG_PROFILE if profile else 0, 0)
+        h = ctypes.c_void_p()
+        check(lib().tbc_engine_init(ctypes.byref(cfg), ctypes.byref(h)), "tbc_engine_init")
+        self.handle = h.value
+        self.block_size = block_size
+
+    def close(self) -> None:
+        if self.handle:
+            lib().tbc_engine_deinit(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def layout(self, tree: TreeSpec) -> abi.TreeLayout:
+        out = abi.TreeLayout()
+        t = tree.ctype()
+        check(lib().tbc_tree_layout_get(self.handle, ctypes.byref(t), ctypes.byref(out)), "tbc_tree_layout_get")
+        return out
+
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def upload(self, array: np.ndarray, pad: int = 0) -> DeviceBuffer:
+        a = np.ascontiguousarray(array)
+        buf = DeviceBuffer(self, a.nbytes + pad)
+        if a.nbytes:
+            buf.upload(a)
+        return buf
+
+    def synchronize(self) -> None:
+        check(lib().tbc_synchronize(self.handle), "tbc_synchronize")
+
+    def checksum(self, messages: list) -> list:
+        """vsr.checksum of each message (bytes), computed on the GPU."""
+        bufs, ptrs, lens = [], [], []
+        for m in messages:
+            m = bytes(m)
+            b = self.upload(np.frombuffer(m + b"\0" * 4, dtype=np.uint8))
+            bufs.append(b)
+            ptrs.append(b.ptr)
+            lens.append(len(m))
+        n = len(messages)
+        P = (ctypes.c_void_p * max(1, n))(*ptrs)
+        L = (ctypes.c_uint64 * max(1, n))(*lens)
+        out = np.zeros(16 * max(1, n), dtype=np.uint8)
+        check(lib().tbc_checksum_batch(self.handle, P, L, n, out.ctypes.data), "tbc_checksum_batch")
+        return [int.from_bytes(out[16 * i:16 * i + 16].tobytes(), "little") for i in range(n)]
+
+    def checksum_device(self, ptrs: list, lens: list) -> np.ndarray:
+        n = len(ptrs)
+        P = (ctypes.c_void_p * max(1, n))(*ptrs)
+        L = (ctypes.c_uint64 * max(1, n))(*lens)
+        out = np.zeros(16 * max(1, n), dtype=np.uint8)
+        check(lib().tbc_checksum_batch(self.handle, P, L, n, out.ctypes.data), "tbc_checksum_batch")
+        return out[: 16 * n].reshape(n, 16)
+
+    def sort_values(self, tree: TreeSpec, buf: DeviceBuffer, count: int, sync: bool = True) -> None:
+        t = tree.ctype()
+        f = lib().tbc_sort_values if sync else lib().tbc_sort_values_async
+        check(f(self.handle, ctypes.byref(t), buf.ptr, count), "tbc_sort_values")
+
+    def submit(self, jobs: list) -> Batch:
+        arr = (abi.Compaction * max(1, len(jobs)))()
+        for i, j in enumerate(jobs):
+            arr[i] = j.ctype()
+        h = ctypes.c_void_p()
+        check(lib().tbc_compaction_submit(self.handle, arr, len(jobs), ctypes.byref(h)), "tbc_compaction_submit")
+        return Batch(self, h.value, jobs)
+
+
+def stage_blocks(engine: Engine, tables: list, value_size: int, block_size: int = BLOCK_SIZE):
+    """Place each input data block's values at +256 of its own block in one
+    device buffer (the grid's block layout) and return (buffer, segments)."""
+    nblocks = sum(len(t) for t in tables)
+    host = np.zeros((max(1, nblocks), block_size), dtype=np.uint8)
+    segs_host = []
+    k = 0
+    for table in tables:
+        for vals in table:
+            v = np.ascontiguousarray(vals, dtype=np.uint8).reshape(-1)
+            host[k, HEADER_SIZE:HEADER_SIZE + v.size] = v
+            segs_host.append((k, v.size // value_size))
+            k += 1
+    buf = engine.upload(host)
+    segs = [(buf.ptr + i * block_size + HEADER_SIZE, n) for i, n in segs_host]
+    return buf, segs
