@@ -125,36 +125,83 @@ __constant__ AegisSeed c_seed = make_seed();
 template <int S0, int S1, int S2, int S3>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
     constexpr int ctrl = S0 | (S1 << 2) | (S2 << 4) | (S3 << 6);
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xf, 0xf, true);
 }
 
 __device__ __forceinline__ uint32_t bpermute(uint32_t byte_addr, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)byte_addr, (int)v);
 }
 
-// One AES round (no round key) of column c: T0[b0(c)] ^ T1[b1(c+1)] ^
-// T2[b2(c+2)] ^ T3[b3(c+3)]; each lane looks up its own column's four bytes
-// and the quad exchanges the partial products.
-__device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, uint32_t x) {
-    uint32_t t0 = sT[x & 0xff];
-    uint32_t t1 = sT[256 + ((x >> 8) & 0xff)];
-    uint32_t t2 = sT[512 + ((x >> 16) & 0xff)];
-    uint32_t t3 = sT[768 + (x >> 24)];
-    return t0 ^ quad_perm<1, 2, 3, 0>(t1) ^ quad_perm<2, 3, 0, 1>(t2) ^ quad_perm<3, 0, 1, 2>(t3);
-}
+// T-tables in LDS, replicated once per bank so that a 32-lane group's lookups
+// never conflict (ds_read_b32 banks are (addr/4) mod 32 per 32-lane group):
+// entry T_r[b] for lane bank k lives at
+//     (r >> 1) * 64 KiB + b * 256 + (r & 1) * 128 + k * 4,
+// so one v_perm_b32 builds the address {k*4, b, region, 0} from the state
+// column and a per-lane base, and the (r & 1) half is the ds_read offset.
+constexpr uint32_t kTableBytes = 131072;
+constexpr uint32_t kTableDwords = kTableBytes / 4;
 
 __device__ __forceinline__ void load_tables(uint32_t *sT) {
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) sT[i] = (&c_aes.t[0][0])[i];
+    for (uint32_t i = threadIdx.x; i < kTableDwords; i += blockDim.x) {
+        const uint32_t r = ((i >> 14) << 1) | ((i >> 5) & 1);
+        const uint32_t b = (i >> 6) & 255;
+        sT[i] = c_aes.t[r][b];
+    }
 }
 
-// Message sources: dword at a byte offset, zero beyond `len` (AegisMac.final
-// zero-pads the tail). Offsets are multiples of 4.
+struct TableBase {
+    uint32_t lo, hi; // {k*4, -, 0, 0} and {k*4, -, 1, 0}
+    __device__ __forceinline__ TableBase() {
+        const uint32_t k = threadIdx.x & 31;
+        lo = k * 4;
+        hi = k * 4 | 0x10000u;
+    }
+};
+
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t *sT, uint32_t byte_off) {
+    return *(const uint32_t *)((const char *)sT + byte_off);
+}
+
+// One AES round (no round key) of column c: T0[b0(c)] ^ T1[b1(c+1)] ^
+// T2[b2(c+2)] ^ T3[b3(c+3)]; each lane looks up its own column's four bytes
+// and the quad exchanges the partial products. `acc` (the round key, already
+// xored with the message word) is folded in first so the chain ends with the
+// last lookup to return.
+__device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, const TableBase &tb, uint32_t x, uint32_t acc) {
+    // v_perm_b32 selector bytes: 0-3 pick src1 (base), 4-7 pick src0 (x).
+    const uint32_t a0 = __builtin_amdgcn_perm(x, tb.lo, 0x03020400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, tb.lo, 0x03020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, tb.hi, 0x03020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, tb.hi, 0x03020700u);
+    const uint32_t t0 = lds_u32(sT, a0);
+    const uint32_t t1 = lds_u32(sT, a1 + 128);
+    const uint32_t t2 = lds_u32(sT, a2);
+    const uint32_t t3 = lds_u32(sT, a3 + 128);
+    uint32_t r = acc ^ t0;
+    r ^= quad_perm<1, 2, 3, 0>(t1);
+    r ^= quad_perm<2, 3, 0, 1>(t2);
+    r ^= quad_perm<3, 0, 1, 2>(t3);
+    return r;
+}
+
+// Message sources. load_exact: dword at a byte offset, zero beyond `len`
+// (AegisMac.final zero-pads the tail); used only for the last partial
+// 32-byte block. load_fast: an unconditional, always in-bounds load (the
+// offset is clamped) used for whole blocks, so the prefetch ring stays in
+// flight instead of waiting right after each (divergent) load. Offsets are
+// multiples of 4; buffers are readable up to len rounded up to 4.
 struct GlobalMsg {
     const uint8_t *base;
     uint32_t len;
-    __device__ __forceinline__ uint32_t load(uint32_t off) const {
+    uint32_t max_off;
+    __device__ __forceinline__ GlobalMsg(const uint8_t *b, uint32_t l)
+        : base(b), len(l), max_off(l >= 4 ? (l & ~3u) - 4 : 0) {}
+    __device__ __forceinline__ uint32_t load_fast(uint32_t off) const {
+        return gld<uint32_t>(base + (off < max_off ? off : max_off));
+    }
+    __device__ __forceinline__ uint32_t load_exact(uint32_t off) const {
         if (off >= len) return 0;
-        uint32_t v = *(const uint32_t *)(base + off);
+        uint32_t v = gld<uint32_t>(base + off);
         uint32_t rem = len - off;
         if (rem < 4) v &= (1u << (8 * rem)) - 1u;
         return v;
@@ -164,7 +211,13 @@ struct GlobalMsg {
 struct LdsMsg {
     const uint32_t *base; // dword-aligned LDS pointer
     uint32_t len;
-    __device__ __forceinline__ uint32_t load(uint32_t off) const {
+    uint32_t max_off;
+    __device__ __forceinline__ LdsMsg(const uint32_t *b, uint32_t l)
+        : base(b), len(l), max_off(l >= 4 ? (l & ~3u) - 4 : 0) {}
+    __device__ __forceinline__ uint32_t load_fast(uint32_t off) const {
+        return base[(off < max_off ? off : max_off) >> 2];
+    }
+    __device__ __forceinline__ uint32_t load_exact(uint32_t off) const {
         if (off >= len) return 0;
         uint32_t v = base[off >> 2];
         uint32_t rem = len - off;
@@ -183,8 +236,11 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     const uint32_t p = g >> 2, c = g & 3;
     const uint32_t key_src = (half + (((p + 1) & 7) << 2) + c) << 2; // quad p+1, same column
 
+    const TableBase tb;
     uint32_t x = c_seed.s[p][c];
-    const uint32_t len = msg.len;
+    // Both groups of the wave share the length: make that provable so the
+    // loop control is scalar.
+    const uint32_t len = __builtin_amdgcn_readfirstlane(msg.len);
     const uint32_t n_abs = (len + 31) >> 5;
 
     // Which steps (u mod 4) inject a message word into this lane, and where
@@ -201,46 +257,48 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     do {                                                                          \
         uint32_t key_ = bpermute(key_src, x);                                     \
         uint32_t m_ = need[(K)&3] ? ((K) < 4 ? (WLO) : (WHI)) : 0u;               \
-        x = aes_col(sT, x) ^ (key_ ^ m_);                                         \
+        x = aes_col(sT, tb, x, key_ ^ m_);                                        \
     } while (0)
 
-    const uint32_t iters = n_abs >> 3;
-    uint32_t wlo[4], whi[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        wlo[d] = msg.load(256 * d + off_lo);
-        whi[d] = msg.load(256 * d + off_hi);
-    }
-    uint32_t it = 0;
-    for (; it + 4 <= iters; it += 4) {
+    // Whole 8-update windows of whole 32-byte blocks, in groups of 4 windows
+    // (32 updates, 1 KiB per message): the next group's words are loaded at
+    // the top of each group, a full group ahead of use, so the compiler's
+    // loop back-edge vmcnt(0) finds them landed. The rest (< 8 full blocks +
+    // the partial tail) runs below with exact loads.
+    const uint32_t iters = (len >> 5) >> 3;
+    const uint32_t groups = (iters + 3) >> 2;
+    uint32_t cur[8];
+    if (groups > 0) {
 #pragma unroll
         for (int d = 0; d < 4; d++) {
-            const uint32_t cl = wlo[d], ch = whi[d];
-            wlo[d] = msg.load(256 * (it + d + 4) + off_lo);
-            whi[d] = msg.load(256 * (it + d + 4) + off_hi);
-            AEGIS_STEP(0, cl, ch);
-            AEGIS_STEP(1, cl, ch);
-            AEGIS_STEP(2, cl, ch);
-            AEGIS_STEP(3, cl, ch);
-            AEGIS_STEP(4, cl, ch);
-            AEGIS_STEP(5, cl, ch);
-            AEGIS_STEP(6, cl, ch);
-            AEGIS_STEP(7, cl, ch);
+            cur[2 * d] = msg.load_fast(256 * d + off_lo);
+            cur[2 * d + 1] = msg.load_fast(256 * d + off_hi);
         }
     }
+    for (uint32_t grp = 0; grp < groups; grp++) {
+        uint32_t nxt[8];
+        const uint32_t base = 1024 * (grp + 1);
 #pragma unroll
-    for (int d = 0; d < 4; d++) {
-        if (it + d < iters) {
-            const uint32_t cl = wlo[d], ch = whi[d];
-            AEGIS_STEP(0, cl, ch);
-            AEGIS_STEP(1, cl, ch);
-            AEGIS_STEP(2, cl, ch);
-            AEGIS_STEP(3, cl, ch);
-            AEGIS_STEP(4, cl, ch);
-            AEGIS_STEP(5, cl, ch);
-            AEGIS_STEP(6, cl, ch);
-            AEGIS_STEP(7, cl, ch);
+        for (int d = 0; d < 4; d++) {
+            nxt[2 * d] = msg.load_fast(base + 256 * d + off_lo);
+            nxt[2 * d + 1] = msg.load_fast(base + 256 * d + off_hi);
         }
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            if (4 * grp + d < iters) {
+                const uint32_t cl = cur[2 * d], ch = cur[2 * d + 1];
+                AEGIS_STEP(0, cl, ch);
+                AEGIS_STEP(1, cl, ch);
+                AEGIS_STEP(2, cl, ch);
+                AEGIS_STEP(3, cl, ch);
+                AEGIS_STEP(4, cl, ch);
+                AEGIS_STEP(5, cl, ch);
+                AEGIS_STEP(6, cl, ch);
+                AEGIS_STEP(7, cl, ch);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
     }
 #undef AEGIS_STEP
     // Remaining (< 8) absorb updates.
@@ -248,8 +306,8 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
         const uint32_t lab = (p + u + 1) & 7;
         const bool nd = (lab & 3) == 0;
         uint32_t key = bpermute(key_src, x);
-        uint32_t m = nd ? msg.load(32 * u + 4 * (lab + c)) : 0u;
-        x = aes_col(sT, x) ^ (key ^ m);
+        uint32_t m = nd ? msg.load_exact(32 * u + 4 * (lab + c)) : 0u;
+        x = aes_col(sT, tb, x, key ^ m);
     }
     // Finalise: tmp = (LE64(len*8) || 0) ^ S2; 7 x update(tmp, tmp).
     const uint32_t q2 = (2 - n_abs) & 7;
@@ -260,7 +318,7 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
         const uint32_t u = n_abs + f;
         const bool nd = ((p + u + 1) & 3) == 0;
         uint32_t key = bpermute(key_src, x);
-        x = aes_col(sT, x) ^ (key ^ (nd ? tmp : 0u));
+        x = aes_col(sT, tb, x, key ^ (nd ? tmp : 0u));
     }
     // tag = S0 ^ ... ^ S6: xor over all 8 blocks, then remove block 7.
     const uint32_t q7 = (7 - (n_abs + 7)) & 7;
@@ -277,20 +335,20 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
 // --------------------------------------------------------------------------
 
 // tbc_checksum_batch: one message per wave (both groups compute it).
-__global__ __launch_bounds__(256) void k_checksum_batch(const uint64_t *ptrs, const uint64_t *lens, uint32_t count,
-                                                      uint8_t *out) {
-    __shared__ uint32_t sT[1024];
+__global__ __launch_bounds__(1024) void k_checksum_batch(const uint64_t *ptrs, const uint64_t *lens, uint32_t count,
+                                                       uint8_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
     load_tables(sT);
     __syncthreads();
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (wave >= count) return;
-    GlobalMsg m{(const uint8_t *)ptrs[wave], (uint32_t)lens[wave]};
+    GlobalMsg m((const uint8_t *)ptrs[wave], (uint32_t)lens[wave]);
     uint32_t tag = aegis_mac32(sT, m);
     const uint32_t lane = threadIdx.x & 63;
-    if (lane < 4) ((uint32_t *)(out + 16 * (size_t)wave))[lane] = tag;
+    if (lane < 4) gst<uint32_t>(out + 16 * (size_t)wave + 4 * lane, tag);
 }
 
-__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return *(const uint64_t *)p; }
+__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return gld<uint64_t>(p); }
 
 // Key (as 4 little-endian limbs) of a value; see composite_key.zig:48-50,
 // groove.zig:27-29, 59-61.
@@ -344,7 +402,7 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
     hdr[g + 32] = header_dword(h, g + 32, body_tag);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    LdsMsg m{hdr + 4, kHeaderSize - 16};
+    LdsMsg m(hdr + 4, kHeaderSize - 16);
     uint32_t tag = aegis_mac32(sT, m);
     return tag;
 }
@@ -352,13 +410,13 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
 // Data blocks: data_block_finish (table.zig:306-384) for every output data
 // block. A wave checksums two full blocks; the last (possibly partial) block
 // of a job gets a wave of its own so both groups always share a length.
-__global__ __launch_bounds__(256) void k_data_blocks(const JobDesc *jobs, int njobs, const JobResultDev *res) {
-    __shared__ uint32_t sT[1024];
-    __shared__ uint32_t sHdr[4][2][64];
+__global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, const JobResultDev *res) {
+    __shared__ uint32_t sT[kTableDwords];
+    __shared__ uint32_t sHdr[16][2][64];
     load_tables(sT);
     __syncthreads();
     const uint32_t wave_in_block = threadIdx.x >> 6;
-    const uint32_t wave = blockIdx.x * 4 + wave_in_block;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wave_in_block;
     const int ji = find_job(jobs, njobs, wave, [](const JobDesc &d) { return d.dblock_base; });
     const JobDesc &j = jobs[ji];
     const uint32_t w = wave - j.dblock_base;
@@ -387,13 +445,13 @@ __global__ __launch_bounds__(256) void k_data_blocks(const JobDesc *jobs, int nj
     const uint32_t slot = data_block_slot(k, j.dbcm);
     uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
 
-    GlobalMsg body{blk + kHeaderSize, cnt * j.value_size};
+    GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
     const uint32_t body_tag = aegis_mac32(sT, body);
 
     HeaderFields h;
     h.cluster_lo = j.cluster_lo;
     h.cluster_hi = j.cluster_hi;
-    h.address = j.addresses[slot];
+    h.address = gld<uint64_t>(j.addresses + slot);
     h.snapshot = j.snapshot_min;
     h.size = size;
     h.meta0 = j.vcm;        // TableData.Metadata.value_count_max
@@ -408,12 +466,11 @@ __global__ __launch_bounds__(256) void k_data_blocks(const JobDesc *jobs, int nj
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (writer) {
-        uint32_t *dst = (uint32_t *)blk;
-        dst[g] = hdr[g];
-        dst[g + 32] = hdr[g + 32];
+        gst<uint32_t>(blk + 4 * g, hdr[g]);
+        gst<uint32_t>(blk + 4 * (g + 32), hdr[g + 32]);
         // Zero [size, sector_ceil(size)) (grid.zig:686).
         const uint32_t end = (uint32_t)sector_ceil(size);
-        for (uint32_t o = size + 4 * g; o < end; o += 128) *(uint32_t *)(blk + o) = 0;
+        for (uint32_t o = size + 4 * g; o < end; o += 128) gst<uint32_t>(blk + o, 0u);
     }
 }
 
@@ -424,7 +481,7 @@ constexpr uint32_t kIndexLdsBytes = 16384;
 
 __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
                                                      uint8_t *infos) {
-    __shared__ uint32_t sT[1024];
+    __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sIdx[kIndexLdsBytes / 4];
     __shared__ uint64_t sKeys[2][4];
     load_tables(sT);
@@ -460,20 +517,20 @@ __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int nj
             ((uint64_t *)(idx + j.idx_keys_min_off + ks * s))[l] = kmin[l];
             ((uint64_t *)(idx + j.idx_keys_max_off + ks * s))[l] = kmax[l];
         }
-        ((uint64_t *)(idx + j.idx_addresses_off))[s] = j.addresses[slot];
+        ((uint64_t *)(idx + j.idx_addresses_off))[s] = gld<uint64_t>(j.addresses + slot);
         if (s == 0)
             for (int l = 0; l < 4; l++) sKeys[0][l] = kmin[l];
         if (s == nblk - 1)
             for (int l = 0; l < 4; l++) sKeys[1][l] = kmax[l];
     }
     __syncthreads();
-    LdsMsg body{sIdx + kHeaderSize / 4, j.index_size - kHeaderSize};
+    LdsMsg body(sIdx + kHeaderSize / 4, j.index_size - kHeaderSize);
     const uint32_t body_tag = aegis_mac32(sT, body);
     const uint32_t index_slot = index_block_slot(t, k_last);
     HeaderFields h;
     h.cluster_lo = j.cluster_lo;
     h.cluster_hi = j.cluster_hi;
-    h.address = j.addresses[index_slot];
+    h.address = gld<uint64_t>(j.addresses + index_slot);
     h.snapshot = j.snapshot_min;
     h.size = j.index_size;
     h.meta0 = nblk;       // TableIndex.Metadata.data_block_count
@@ -487,9 +544,9 @@ __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int nj
     if (lane < 4) sIdx[lane] = hdr_tag;
     __syncthreads();
     uint8_t *blk = j.out_blocks + (size_t)index_slot * j.block_size;
-    for (uint32_t i = lane; i < j.index_size / 4; i += 64) ((uint32_t *)blk)[i] = sIdx[i];
+    for (uint32_t i = lane; i < j.index_size / 4; i += 64) gst<uint32_t>(blk + 4 * i, sIdx[i]);
     const uint32_t end = (uint32_t)sector_ceil(j.index_size);
-    for (uint32_t o = j.index_size + 4 * lane; o < end; o += 256) *(uint32_t *)(blk + o) = 0;
+    for (uint32_t o = j.index_size + 4 * lane; o < end; o += 256) gst<uint32_t>(blk + o, 0u);
 
     // ManifestNode.TableInfo (schema.zig:489-509).
     if (lane < 32) {
@@ -514,16 +571,23 @@ __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int nj
         else if (i == 28 || i == 29) v = 0xffffffffu; // snapshot_max = maxInt(u64)
         else if (i == 30) v = (uint32_t)vcount;
         else if (i == 31) v = (uint32_t)j.tree_id | ((uint32_t)((j.level_b & 0x3f) | (1u << 6)) << 16);
-        info[i] = v;
+        gst<uint32_t>(info + i, v);
     }
+}
+
+// One workgroup per CU (the tables take 128 KiB of LDS): spread the waves
+// over all 256 CUs, at most 16 waves per workgroup.
+static uint32_t waves_per_block(uint32_t waves) {
+    uint32_t w = (waves + 255) / 256;
+    return w < 1 ? 1 : (w > 16 ? 16 : w);
 }
 
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream) {
     if (count == 0) return 0;
-    const uint32_t blocks = (count + 3) / 4;
-    hipLaunchKernelGGL(k_checksum_batch, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_ptrs, d_lens, count,
-                       d_out);
+    const uint32_t wpb = waves_per_block(count);
+    hipLaunchKernelGGL(k_checksum_batch, dim3((count + wpb - 1) / wpb), dim3(64 * wpb), 0, (hipStream_t)stream,
+                       d_ptrs, d_lens, count, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -532,8 +596,9 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint
                   void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     if (total_dblocks) {
-        hipLaunchKernelGGL(k_data_blocks, dim3((total_dblocks + 3) / 4), dim3(256), 0, s, d_jobs, njobs,
-                           (const JobResultDev *)d_results);
+        const uint32_t wpb = waves_per_block(total_dblocks);
+        hipLaunchKernelGGL(k_data_blocks, dim3((total_dblocks + wpb - 1) / wpb), dim3(64 * wpb), 0, s, d_jobs,
+                           njobs, (const JobResultDev *)d_results);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "data_blocks");

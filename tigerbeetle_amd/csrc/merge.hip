@@ -53,7 +53,7 @@ template <int KL> __device__ __forceinline__ bool key_lt(const Key<KL> &a, const
     return a.l[0] < b.l[0];
 }
 
-__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return *(const uint64_t *)p; }
+__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return gld<uint64_t>(p); }
 
 // key_from_value (composite_key.zig:48-50, groove.zig:27-29, 59-61).
 template <int KIND>
@@ -84,14 +84,14 @@ __device__ __forceinline__ uint32_t seg_search(const Stream &s, uint32_t idx) {
     uint32_t lo = 0, hi = s.nseg - 1;
     while (lo < hi) {
         uint32_t mid = (lo + hi + 1) >> 1;
-        if (s.seg_pre[mid] <= idx) lo = mid;
+        if (gld<uint32_t>(s.seg_pre + mid) <= idx) lo = mid;
         else hi = mid - 1;
     }
     return lo;
 }
 
 __device__ __forceinline__ const uint8_t *elem_ptr(const Stream &s, uint32_t seg, uint32_t idx, uint32_t vs) {
-    return (const uint8_t *)s.seg_ptr[seg] + (size_t)(idx - s.seg_pre[seg]) * vs;
+    return (const uint8_t *)gld<uint64_t>(s.seg_ptr + seg) + (size_t)(idx - gld<uint32_t>(s.seg_pre + seg)) * vs;
 }
 
 // --------------------------------------------------------------------------
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         uint32_t tb = 0;
         if (valid) {
             uint32_t seg = is_a ? sh.seg_a : sh.seg_b;
-            while (seg + 1 < s.nseg && s.seg_pre[seg + 1] <= (uint32_t)idx) seg++;
+            while (seg + 1 < s.nseg && gld<uint32_t>(s.seg_pre + seg + 1) <= (uint32_t)idx) seg++;
             p = elem_ptr(s, seg, (uint32_t)idx, vs);
             k = load_key<KIND>(p, ts);
             if (is_a) tb = load_tomb(p, ts);
@@ -325,13 +325,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     for (uint32_t c = tid; c < cnt * cpv; c += kMergeThreads) {
         const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
         const uint32_t e = sh.out[v] & 0x7fffffffu;
-        const uint4 val = *(const uint4 *)(sh.ptr[e] + 16 * part);
+        const u32x4 val = gld<u32x4>(sh.ptr[e] + 16 * part);
         const uint32_t rel = o_start + v;
         const uint32_t kb = k_start + rel / vcm;
         const uint32_t ob = rel - (kb - k_start) * vcm;
         uint8_t *dst = j.out_blocks + (size_t)data_block_slot(kb, j.dbcm) * j.block_size + kHeaderSize +
                        (size_t)ob * vs + 16 * part;
-        *(uint4 *)dst = val;
+        gst<u32x4>(dst, val);
     }
 }
 

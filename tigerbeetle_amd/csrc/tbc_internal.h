@@ -77,6 +77,14 @@ __host__ __device__ inline uint64_t sector_ceil(uint64_t x) {
     return (x + kSectorSize - 1) / kSectorSize * kSectorSize;
 }
 
+// Global-address-space accessors. Pointers that reach a kernel through a
+// struct are generic (flat); flat loads also count against lgkmcnt, so an LDS
+// wait would wait for HBM too. These force global_load/global_store.
+#define TBC_GLOBAL __attribute__((address_space(1)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <class T> __device__ __forceinline__ T gld(const void *p) { return *(const TBC_GLOBAL T *)p; }
+template <class T> __device__ __forceinline__ void gst(void *p, const T &v) { *(TBC_GLOBAL T *)p = v; }
+
 // Find the job owning global index `g` given a per-job base field (ascending).
 template <class F>
 __device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F base_of) {
