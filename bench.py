@@ -224,9 +224,7 @@ def main() -> None:
     W_index = tables * index_size
     alg_bytes = {
         "merge_partition": (args.jobs * 2400) * 2 * 21 * 32,
-        "merge_count": R,                     # every input value's key line read once
-        "merge_scan": args.jobs * 2400 * 8,
-        "merge_write": R + out_values * spec.value_size,
+        "merge": R + out_values * spec.value_size,  # read every input value once, write every survivor
         "data_blocks": W_data + data_blocks * 256,  # read bodies, write headers
         "index_blocks": W_index + data_blocks * 64,
     }

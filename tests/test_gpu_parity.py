@@ -129,3 +129,67 @@ def test_batch_of_mixed_trees_is_independent(engine_small, oracle_lib):
     both, _ = gpu_run(engine_small, [other, ji], bs, [oaddrs, addrs])
     assert np.array_equal(alone[0][2], both[1][2])
     assert np.array_equal(alone[0][1], both[1][1])
+
+
+@pytest.mark.parametrize("name", ["transfers.timestamp", "transfers.id", "accounts.ledger",
+                                  "transfers.debit_account_id", "posted.timestamp", "account_history.timestamp"])
+def test_sort_values_stable(engine, oracle_lib, name):
+    """TableMemory.sort (table_memory.zig:140-154): stable, bit-exact vs the oracle."""
+    spec = trees.BY_NAME[name]
+    rng = np.random.default_rng(11)
+    n = 70_001
+    limbs = workloads.random_keys(spec, n, rng, field_max=300)
+    limbs[0] = rng.integers(1, 5000, size=n, dtype=np.uint64)  # many equal keys: stability matters
+    tomb = rng.random(n) < 0.1
+    vals = workloads.values_from_keys(spec, limbs, tomb, rng)
+    # Put the insertion order into bytes the key does not cover so that any
+    # instability would show up in the output bytes.
+    if spec.key_kind == 0:
+        w = vals.view(np.uint64)
+        w[:, (spec.timestamp_offset // 8 + 1) % (spec.value_size // 8)] = np.arange(n, dtype=np.uint64)
+    elif spec.value_size == 32 and spec.key_kind == 1:
+        vals.view(np.uint64)[:, 3] = np.arange(n, dtype=np.uint64)
+    t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                        spec.value_count_max, 1 << 20)
+    want = oracle_lib.sort_values(t, vals)
+    buf = engine.upload(vals)
+    engine.sort_values(spec, buf, n)
+    got = buf.download(vals.nbytes).reshape(n, spec.value_size)
+    assert np.array_equal(got, want)
+
+
+def test_sort_values_already_sorted_is_noop(engine):
+    spec = trees.BY_NAME["transfers.id"]
+    rng = np.random.default_rng(12)
+    limbs = workloads.unique_sorted_keys(spec, 5000, rng)
+    vals = workloads.values_from_keys(spec, limbs, np.zeros(5000, dtype=bool), rng)
+    buf = engine.upload(vals)
+    engine.sort_values(spec, buf, 5000)
+    assert np.array_equal(buf.download(vals.nbytes).reshape(5000, 32), vals)
+
+
+def test_immutable_compaction_after_device_sort(engine, oracle_lib):
+    """Bar end: sort the mutable table on the device, then compact it as the
+    immutable table A (tree.zig:979-999 -> compaction.zig:483-559)."""
+    from helpers import disk_image, run_oracle
+    from tigerbeetle_amd.engine import Job, stage_blocks
+    bs = 1 << 20
+    spec = trees.BY_NAME["transfers.credit_account_id"]
+    rng = np.random.default_rng(13)
+    ji = workloads.make_job_inputs(spec, rng, n_a=50_000, b_table_sizes=[40_000], a_immutable=True,
+                                   dup_frac=0.2, overlap=0.3, drop_tombstones=True, field_max=2000)
+    shuffled = workloads.shuffle_for_memtable(ji.a_values, rng, spec)
+    abuf = engine.upload(shuffled)
+    engine.sort_values(spec, abuf, len(shuffled), sync=False)
+    bbuf, segs_b = stage_blocks(engine, [workloads.split_blocks(t, 32760) for t in ji.b_tables], 32, bs)
+    addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, 90_000, bs) + 2, rng, 3)
+    out = engine.alloc(len(addrs) * bs)
+    batch = engine.submit([Job(spec, [(abuf.ptr, len(shuffled))], segs_b, True, True, 1, 7, 48, addrs, out)])
+    batch.wait()
+    r, infos = batch.result(0)
+    blocks = out.download(r.block_count * bs).reshape(-1, bs)
+    o = run_oracle(oracle_lib, ji, bs, addrs, cluster=7)
+    assert r.block_count == len(o.blocks)
+    for g, w in zip(blocks, o.blocks):
+        assert np.array_equal(disk_image(g), disk_image(w))
+    assert np.array_equal(infos, o.table_infos)

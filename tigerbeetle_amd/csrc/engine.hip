@@ -379,8 +379,8 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
     const uint64_t sz_addr = align_up(8 * addr_words, 256);
     const uint64_t sz_in = sz_jobs + sz_segs + sz_addr;
-    const uint64_t sz_splits = align_up(4ull * splits, 256);
-    const uint64_t sz_tiles = align_up(4ull * tiles + 4, 256);
+    const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
+    const uint64_t sz_tiles = align_up(8ull * tiles + 4ull * count + 8, 256); // status granules + tile counters
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
     b->dev_top = e->dev.top;
@@ -396,8 +396,9 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     e->dev.live++;
     e->host.live++;
     uint8_t *d_in = dbase;
-    uint32_t *d_splits = (uint32_t *)(dbase + sz_in);
-    uint32_t *d_tiles = (uint32_t *)(dbase + sz_in + sz_splits);
+    SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
+    uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
+    uint32_t *d_counters = (uint32_t *)(d_status + tiles);
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
     b->h_results = (JobResultDev *)(hbase + sz_in);
@@ -459,10 +460,11 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
 
     hipStream_t s = e->stream;
     bool ok = hipMemcpyAsync(d_in, h_in, sz_in, hipMemcpyHostToDevice, s) == hipSuccess;
-    ok = ok && hipMemsetAsync(d_res, 0, sz_res, s) == hipSuccess;
+    // Status granules, tile counters and results must start zeroed (contiguous).
+    ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");
     if (ok && count)
-        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, tiles, splits, d_splits, d_tiles, d_res, s,
+        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, d_counters, d_res, s,
                           mark_cb, b) == 0;
     if (ok && count)
         ok = launch_blocks((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, s, mark_cb, b) == 0;

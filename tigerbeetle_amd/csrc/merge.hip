@@ -96,11 +96,12 @@ __device__ __forceinline__ const uint8_t *elem_ptr(const Stream &s, uint32_t seg
 
 // --------------------------------------------------------------------------
 // Merge-path partition: for every tile boundary d = t * kMergeTile, the number
-// of A elements among the first d merged elements.
+// i of A elements among the first d merged elements, plus the segments that
+// hold A[max(i-1, 0)] and B[min(d-i, nb-1)] (where the tile starts reading).
 // --------------------------------------------------------------------------
 template <int KIND>
 __global__ __launch_bounds__(256) void k_partition(const JobDesc *jobs, int njobs, uint32_t split_offset,
-                                                   uint32_t nsplits, uint32_t *splits) {
+                                                   uint32_t nsplits, SplitDesc *splits) {
     const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
     if (gid >= nsplits) return;
     const uint32_t gsplit = split_offset + gid;
@@ -120,37 +121,61 @@ __global__ __launch_bounds__(256) void k_partition(const JobDesc *jobs, int njob
         if (key_le(load_key<KIND>(pa, ts), load_key<KIND>(pb, ts))) lo = mid + 1;
         else hi = mid;
     }
-    splits[gsplit] = lo;
+    SplitDesc s;
+    s.i = lo;
+    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
+    const uint32_t jb = d - lo;
+    s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
+    s.pad = 0;
+    splits[gsplit] = s;
 }
 
 // --------------------------------------------------------------------------
-// Tile kernel: survivors of merged positions [d0, d1). COUNT: per-tile
-// survivor count. WRITE: copy survivors to their output slots.
+// One pass per tile (merged positions [d0, d1)): load keys, decide
+// survivors, exclusive-scan them, learn the tile's global output offset by
+// decoupled look-back over its job's earlier tiles, and copy the survivors
+// straight into their output data-block slots.
+//
+// Tiles take ids from an atomic counter in start order, so a tile only ever
+// waits on tiles that are already running (no deadlock). Each tile publishes
+// one 8-byte status granule {flag:2, count:62}: 1 = own count, 2 = inclusive
+// prefix (single aligned 8-byte agent-scope store: untorn, no payload behind
+// it; MI355X guide §Workgroup dispatch, hand-off granules).
 // --------------------------------------------------------------------------
+constexpr uint32_t kSegWindow = 16;
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kCountMask = (1ull << 62) - 1;
+
 template <int KL> struct TileShared {
     uint64_t key[KL][kMergeTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
     const uint8_t *ptr[kMergeTile + 3];
-    uint8_t tomb[kMergeTile + 2];
+    uint8_t tomb[kMergeTile + 4];
     uint32_t pos[kMergeTile];  // merged position -> entry (0xffffffff = dropped)
     uint32_t out[kMergeTile];  // output order -> entry
+    uint32_t seg_pre[2][kSegWindow + 1];
+    uint64_t seg_ptr[2][kSegWindow];
     uint32_t wave_sums[kMergeThreads / 64];
-    uint32_t seg_a, seg_b, count;
+    uint32_t tile, count;
+    uint64_t offset;
 };
 
-template <int KIND, bool WRITE>
+template <int KIND>
 __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, int njobs, uint32_t tile_offset,
-                                                              const uint32_t *splits, uint32_t *tile_counts) {
+                                                              uint32_t *tile_counter, const SplitDesc *splits,
+                                                              uint64_t *status, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t gtile = tile_offset + blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid == 0) sh.tile = tile_offset + atomicAdd(tile_counter, 1u);
+    __syncthreads();
+    const uint32_t gtile = sh.tile;
     const int ji = find_job(jobs, njobs, gtile, [](const JobDesc &d) { return d.tile_base; });
     const JobDesc &j = jobs[ji];
     const uint32_t t = gtile - j.tile_base;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * kMergeTile;
     const uint32_t d1 = (d0 + kMergeTile) < n ? d0 + kMergeTile : n;
-    const uint32_t i0 = splits[j.split_base + t], i1 = splits[j.split_base + t + 1];
+    const SplitDesc s0 = splits[j.split_base + t];
+    const uint32_t i0 = s0.i, i1 = splits[j.split_base + t + 1].i;
     const uint32_t j0 = d0 - i0, j1 = d1 - i1;
     const uint32_t na = i1 - i0, nb = j1 - j0;
     const uint32_t vs = j.value_size, ts = j.timestamp_offset;
@@ -158,35 +183,58 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     const bool secondary = j.usage == 1;
     const bool drop = j.drop_tombstones != 0;
 
-    if (tid == 0) {
-        sh.seg_a = na_all ? seg_search(j.a, i0 > 0 ? i0 - 1 : 0) : 0;
-        sh.seg_b = nb_all ? seg_search(j.b, j0 < nb_all ? j0 : (nb_all ? nb_all - 1 : 0)) : 0;
+    // Segment windows (the few input data blocks this tile touches).
+    if (tid < 2 * (kSegWindow + 1)) {
+        const uint32_t side = tid / (kSegWindow + 1), k = tid % (kSegWindow + 1);
+        const Stream &s = side == 0 ? j.a : j.b;
+        const uint32_t seg = (side == 0 ? s0.seg_a : s0.seg_b) + k;
+        sh.seg_pre[side][k] = seg <= s.nseg && s.nseg ? gld<uint32_t>(s.seg_pre + seg) : 0xffffffffu;
+        if (k < kSegWindow) sh.seg_ptr[side][k] = seg < s.nseg ? gld<uint64_t>(s.seg_ptr + seg) : 0;
     }
     __syncthreads();
 
-    // Load keys: entries [0, na+2) = A[i0-1 .. i1], entries [na+2, na+2+nb+1) = B[j0 .. j1].
+    // Load keys: entries [0, ea) = A[i0-1 .. i1], entries [ea, ea+eb) = B[j0 .. j1].
     const uint32_t ea = na + 2, eb = nb + 1;
-    for (uint32_t e = tid; e < ea + eb; e += kMergeThreads) {
-        const bool is_a = e < ea;
-        const Stream &s = is_a ? j.a : j.b;
-        const int64_t idx = is_a ? (int64_t)i0 - 1 + e : (int64_t)j0 + (e - ea);
-        const bool valid = idx >= 0 && idx < (int64_t)s.n;
+    constexpr uint32_t kPerLoad = (kMergeTile + 3 + kMergeThreads - 1) / kMergeThreads;
+    const uint8_t *ptrs[kPerLoad];
+#pragma unroll
+    for (uint32_t r = 0; r < kPerLoad; r++) {
+        const uint32_t e = tid + r * kMergeThreads;
+        const uint8_t *p = nullptr;
+        if (e < ea + eb) {
+            const bool is_a = e < ea;
+            const uint32_t side = is_a ? 0 : 1;
+            const Stream &s = is_a ? j.a : j.b;
+            const int64_t idx = is_a ? (int64_t)i0 - 1 + e : (int64_t)j0 + (e - ea);
+            if (idx >= 0 && idx < (int64_t)s.n) {
+                uint32_t k = 0;
+                while (k + 1 < kSegWindow && sh.seg_pre[side][k + 1] <= (uint32_t)idx) k++;
+                if (k + 1 == kSegWindow && sh.seg_pre[side][k + 1] <= (uint32_t)idx) {
+                    const uint32_t seg = seg_search(s, (uint32_t)idx); // tiny segments: global fallback
+                    p = elem_ptr(s, seg, (uint32_t)idx, vs);
+                } else {
+                    p = (const uint8_t *)sh.seg_ptr[side][k] + (size_t)((uint32_t)idx - sh.seg_pre[side][k]) * vs;
+                }
+            }
+        }
+        ptrs[r] = p;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kPerLoad; r++) {
+        const uint32_t e = tid + r * kMergeThreads;
+        if (e >= ea + eb) continue;
         Key<KL> k;
 #pragma unroll
         for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
-        const uint8_t *p = nullptr;
         uint32_t tb = 0;
-        if (valid) {
-            uint32_t seg = is_a ? sh.seg_a : sh.seg_b;
-            while (seg + 1 < s.nseg && gld<uint32_t>(s.seg_pre + seg + 1) <= (uint32_t)idx) seg++;
-            p = elem_ptr(s, seg, (uint32_t)idx, vs);
-            k = load_key<KIND>(p, ts);
-            if (is_a) tb = load_tomb(p, ts);
+        if (ptrs[r]) {
+            k = load_key<KIND>(ptrs[r], ts);
+            if (e < ea) tb = load_tomb(ptrs[r], ts);
         }
 #pragma unroll
         for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
-        if (WRITE) sh.ptr[e] = p;
-        if (is_a) sh.tomb[e] = (uint8_t)tb;
+        sh.ptr[e] = ptrs[r];
+        if (e < ea) sh.tomb[e] = (uint8_t)tb;
     }
     __syncthreads();
 
@@ -216,7 +264,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         return len;
     };
 
-    uint32_t local = 0;
     for (uint32_t q = tid; q < na + nb; q += kMergeThreads) {
         uint32_t pos, entry;
         bool surv;
@@ -260,29 +307,12 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
             bool a_exists = prev_valid && key_eq(entry_key(lo), kb);
             if (a_exists && immutable && secondary) a_exists = (run_len(i0 + lo - 1) & 1) != 0;
             surv = !a_exists;
-            entry |= 0x80000000u;
         }
-        local += surv ? 1u : 0u;
-        if (WRITE) sh.pos[pos] = surv ? entry : 0xffffffffu;
+        sh.pos[pos] = surv ? entry : 0xffffffffu;
     }
-
-    if (!WRITE) {
-        // Block reduction of survivor counts.
-        uint32_t v = local;
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((tid & 63) == 0) sh.wave_sums[tid >> 6] = v;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t s = 0;
-            for (uint32_t w = 0; w < kMergeThreads / 64; w++) s += sh.wave_sums[w];
-            tile_counts[gtile] = s;
-        }
-        return;
-    }
-
     __syncthreads();
-    // Exclusive scan of survivor flags in merged order; each thread owns 4
-    // consecutive positions.
+
+    // Exclusive scan of survivor flags in merged order (4 positions per thread).
     const uint32_t total_pos = na + nb;
     constexpr uint32_t kPer = kMergeTile / kMergeThreads;
     uint32_t f[kPer];
@@ -293,8 +323,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         f[k] = (pidx < total_pos && sh.pos[pidx] != 0xffffffffu) ? 1u : 0u;
         sum += f[k];
     }
-    // Wave inclusive scan.
-    const uint32_t lane = tid & 63;
     uint32_t incl = sum;
     for (int o = 1; o < 64; o <<= 1) {
         uint32_t y = __shfl_up(incl, o, 64);
@@ -304,84 +332,96 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     __syncthreads();
     uint32_t wave_off = 0;
     for (uint32_t w = 0; w < (tid >> 6); w++) wave_off += sh.wave_sums[w];
-    if (tid == kMergeThreads - 1) sh.count = wave_off + incl;
     uint32_t o = wave_off + incl - sum;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; k++) {
         const uint32_t pidx = tid * kPer + k;
         if (f[k]) sh.out[o++] = sh.pos[pidx];
     }
+    if (tid == kMergeThreads - 1) {
+        // Decoupled look-back (one lane): this tile's global output offset.
+        const uint32_t cnt = wave_off + incl;
+        sh.count = cnt;
+        uint64_t *st = status + j.tile_base;
+        uint64_t prefix = 0;
+        if (t == 0) {
+            __hip_atomic_store(st, kFlagIncl | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st + t, kFlagAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t k = t - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const uint64_t s = __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t flag = s & ~kCountMask;
+                if (flag == 0) {
+                    if (++spins > (1u << 26)) { // bounded: report instead of hanging
+                        res[j.job_index].invariant = 0xdead;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                prefix += s & kCountMask;
+                if (flag == kFlagIncl || k == 0) break;
+                k--;
+            }
+            __hip_atomic_store(st + t, kFlagIncl | (prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sh.offset = prefix;
+        if (t + 1 == j.tile_count) {
+            // Output shape (write_blocks, compaction.zig:806-850): full data
+            // blocks except the last, full tables except the last.
+            const uint64_t total = prefix + cnt;
+            const uint32_t db = (uint32_t)((total + j.vcm - 1) / j.vcm);
+            const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
+            JobResultDev &r = res[j.job_index];
+            r.value_count = total;
+            r.data_block_count = db;
+            r.table_count = tables;
+            r.block_count = db + tables;
+        }
+    }
     __syncthreads();
 
     // Copy survivors, 16 bytes per lane, to data block k = g / vcm, slot
     // k + k / dbcm (table.zig:306-384 block order, compaction.zig:819-835 acquire order).
     const uint32_t cnt = sh.count;
-    const uint64_t g0 = tile_counts[gtile];
+    const uint64_t g0 = sh.offset;
     const uint32_t cpv = vs >> 4;
     const uint32_t cpv_shift = __builtin_ctz(cpv);
     const uint32_t vcm = j.vcm;
     const uint32_t k_start = (uint32_t)(g0 / vcm);
     const uint32_t o_start = (uint32_t)(g0 - (uint64_t)k_start * vcm);
-    for (uint32_t c = tid; c < cnt * cpv; c += kMergeThreads) {
-        const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
-        const uint32_t e = sh.out[v] & 0x7fffffffu;
-        const u32x4 val = gld<u32x4>(sh.ptr[e] + 16 * part);
-        const uint32_t rel = o_start + v;
-        const uint32_t kb = k_start + rel / vcm;
-        const uint32_t ob = rel - (kb - k_start) * vcm;
-        uint8_t *dst = j.out_blocks + (size_t)data_block_slot(kb, j.dbcm) * j.block_size + kHeaderSize +
-                       (size_t)ob * vs + 16 * part;
-        gst<u32x4>(dst, val);
-    }
-}
-
-// Per-job exclusive scan of tile counts; derives the output shape
-// (write_blocks, compaction.zig:806-850: full data blocks except the last,
-// full tables except the last).
-__global__ __launch_bounds__(256) void k_merge_scan(const JobDesc *jobs, uint32_t *tile_counts, JobResultDev *res) {
-    __shared__ uint32_t wave_sums[4];
-    __shared__ uint64_t carry;
-    const JobDesc &j = jobs[blockIdx.x];
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < j.tile_count; base += 256) {
-        const uint32_t i = base + tid;
-        const uint32_t v = i < j.tile_count ? tile_counts[j.tile_base + i] : 0;
-        uint32_t incl = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= (uint32_t)o) incl += y;
+    const uint32_t chunks = cnt * cpv;
+    constexpr uint32_t kUnroll = 4;
+    for (uint32_t c0 = tid; c0 < chunks; c0 += kMergeThreads * kUnroll) {
+        u32x4 val[kUnroll];
+        uint8_t *dst[kUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kUnroll; u++) {
+            const uint32_t c = c0 + u * kMergeThreads;
+            dst[u] = nullptr;
+            if (c < chunks) {
+                const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
+                const uint32_t e = sh.out[v];
+                val[u] = gld<u32x4>(sh.ptr[e] + 16 * part);
+                const uint32_t rel = o_start + v;
+                const uint32_t kb = k_start + rel / vcm;
+                const uint32_t ob = rel - (kb - k_start) * vcm;
+                dst[u] = j.out_blocks + (size_t)data_block_slot(kb, j.dbcm) * j.block_size + kHeaderSize +
+                         (size_t)ob * vs + 16 * part;
+            }
         }
-        if (lane == 63) wave_sums[tid >> 6] = incl;
-        __syncthreads();
-        uint32_t woff = 0;
-        for (uint32_t w = 0; w < (tid >> 6); w++) woff += wave_sums[w];
-        const uint64_t c0 = carry;
-        if (i < j.tile_count) tile_counts[j.tile_base + i] = (uint32_t)(c0 + woff + incl - v);
-        __syncthreads();
-        if (tid == 255) carry = c0 + woff + incl;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const uint64_t total = carry;
-        const uint32_t db = (uint32_t)((total + j.vcm - 1) / j.vcm);
-        const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
-        JobResultDev r;
-        r.value_count = total;
-        r.data_block_count = db;
-        r.table_count = tables;
-        r.block_count = db + tables;
-        r.status = 0;
-        r.invariant = 0;
-        r.pad = 0;
-        res[j.job_index] = r;
+#pragma unroll
+        for (uint32_t u = 0; u < kUnroll; u++)
+            if (dst[u]) gst<u32x4>(dst[u], val[u]);
     }
 }
 
 template <int KIND>
 static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
-                       uint32_t *d_splits, uint32_t *d_tile_counts, hipStream_t s) {
+                       SplitDesc *d_splits, uint64_t *d_status, uint32_t *d_counters, JobResultDev *d_res,
+                       hipStream_t s) {
     const JobDesc &f = h_jobs[first];
     const JobDesc &l = h_jobs[first + count - 1];
     const uint32_t split_off = f.split_base;
@@ -391,21 +431,17 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
     if (phase == 0)
         hipLaunchKernelGGL(k_partition<KIND>, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs + first, count,
                            split_off, nsplits, d_splits);
-    else if (phase == 1 && ntiles)
-        hipLaunchKernelGGL((k_merge_tile<KIND, false>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs + first,
-                           count, tile_off, (const uint32_t *)d_splits, d_tile_counts);
-    else if (phase == 2 && ntiles)
-        hipLaunchKernelGGL((k_merge_tile<KIND, true>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs + first,
-                           count, tile_off, (const uint32_t *)d_splits, d_tile_counts);
+    else if (ntiles)
+        hipLaunchKernelGGL(k_merge_tile<KIND>, dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs + first, count,
+                           tile_off, d_counters + first, (const SplitDesc *)d_splits, d_status, d_res);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Jobs must be grouped by key kind (contiguous runs) by the caller.
-int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, uint32_t total_tiles,
-                 uint32_t total_splits, uint32_t *d_splits, uint32_t *d_tile_counts, JobResultDev *d_results,
-                 void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
-    (void)total_tiles;
-    (void)total_splits;
+// Jobs must be grouped by key kind (contiguous runs) by the caller. d_status
+// (one u64 per tile) and d_counters (one u32 per job) must be zero.
+int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
+                 uint64_t *d_status, uint32_t *d_counters, JobResultDev *d_results, void *stream,
+                 void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     auto for_each_kind = [&](auto fn) {
         int first = 0;
@@ -420,23 +456,18 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, uint32
     auto phase = [&](int ph) {
         return for_each_kind([&](uint32_t kind, int first, int count) {
             switch (kind) {
-            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_tile_counts, s);
-            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_tile_counts, s);
-            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_tile_counts, s);
-            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_tile_counts, s);
+            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
+            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
+            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
+            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
             }
         });
     };
     if (phase(0)) return -1;
     if (mark) mark(mark_ctx, "merge_partition");
     if (phase(1)) return -1;
-    if (mark) mark(mark_ctx, "merge_count");
-    hipLaunchKernelGGL(k_merge_scan, dim3(njobs), dim3(256), 0, s, d_jobs, d_tile_counts, d_results);
-    if (hipGetLastError() != hipSuccess) return -1;
-    if (mark) mark(mark_ctx, "merge_scan");
-    int rc = phase(2);
-    if (mark) mark(mark_ctx, "merge_write");
-    return rc;
+    if (mark) mark(mark_ctx, "merge");
+    return 0;
 }
 
 } // namespace tbc

@@ -57,6 +57,13 @@ struct JobDesc {
     uint32_t job_index;
 };
 
+struct SplitDesc {
+    uint32_t i;     // A elements before the tile boundary (merge path)
+    uint32_t seg_a; // segment of A[max(i-1, 0)]
+    uint32_t seg_b; // segment of B[min(d-i, nb-1)]
+    uint32_t pad;
+};
+
 struct JobResultDev {
     uint64_t value_count;
     uint32_t data_block_count;
@@ -102,9 +109,9 @@ __device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F bas
 // Kernel launchers (implemented in the .hip translation units).
 struct hipStream_t_;
 namespace tbc {
-int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, uint32_t total_tiles,
-                 uint32_t total_splits, uint32_t *d_splits, uint32_t *d_tile_counts,
-                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
+                 uint64_t *d_status, uint32_t *d_counters, JobResultDev *d_results, void *stream,
+                 void (*mark)(void *, const char *), void *mark_ctx);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
                   JobResultDev *d_results, uint8_t *d_infos, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx);
