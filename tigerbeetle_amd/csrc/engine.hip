@@ -378,7 +378,8 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     const uint64_t sz_jobs = align_up(sizeof(JobDesc) * (uint64_t)count, 256);
     const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
     const uint64_t sz_addr = align_up(8 * addr_words, 256);
-    const uint64_t sz_in = sz_jobs + sz_segs + sz_addr;
+    const uint64_t sz_order = align_up(sizeof(TileRef) * (uint64_t)tiles, 256);
+    const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order;
     const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
     const uint64_t sz_tiles = align_up(8ull * tiles + 4ull * count + 8, 256); // status granules + tile counters
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
@@ -438,6 +439,22 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         ap += c.address_count;
     }
     memcpy(h_in, sj.data(), sizeof(JobDesc) * count);
+    // Tile order: per key kind (contiguous jobs), round-robin over the jobs.
+    TileRef *horder = (TileRef *)(h_in + sz_jobs + sz_segs + sz_addr);
+    const TileRef *d_order = (const TileRef *)(d_in + sz_jobs + sz_segs + sz_addr);
+    {
+        uint32_t o = 0, first = 0;
+        while (first < count) {
+            uint32_t last = first;
+            while (last + 1 < count && sj[last + 1].key_kind == sj[first].key_kind) last++;
+            uint32_t max_tiles = 0;
+            for (uint32_t k = first; k <= last; k++) max_tiles = std::max(max_tiles, sj[k].tile_count);
+            for (uint32_t r = 0; r < max_tiles; r++)
+                for (uint32_t k = first; k <= last; k++)
+                    if (r < sj[k].tile_count) horder[o++] = TileRef{k, r};
+            first = last + 1;
+        }
+    }
 
     for (int m = 0; m < kMaxMarks; m++) {
         if (e->flags & TBC_CONFIG_PROFILE) {
@@ -464,8 +481,8 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");
     if (ok && count)
-        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, d_counters, d_res, s,
-                          mark_cb, b) == 0;
+        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, d_counters, d_order,
+                          d_res, s, mark_cb, b) == 0;
     if (ok && count)
         ok = launch_blocks((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, s, mark_cb, b) == 0;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;

@@ -159,18 +159,21 @@ template <int KL> struct TileShared {
 };
 
 template <int KIND>
-__global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, int njobs, uint32_t tile_offset,
-                                                              uint32_t *tile_counter, const SplitDesc *splits,
-                                                              uint64_t *status, JobResultDev *res) {
+__global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
+                                                              uint32_t order_offset, uint32_t *tile_counter,
+                                                              const SplitDesc *splits, uint64_t *status,
+                                                              JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) sh.tile = tile_offset + atomicAdd(tile_counter, 1u);
+    // Tiles start in counter order, so a tile waits only on running tiles.
+    // The order table interleaves the batch's jobs, which keeps each job's
+    // look-back chain short however many tiles are in flight.
+    if (tid == 0) sh.tile = order_offset + atomicAdd(tile_counter, 1u);
     __syncthreads();
-    const uint32_t gtile = sh.tile;
-    const int ji = find_job(jobs, njobs, gtile, [](const JobDesc &d) { return d.tile_base; });
-    const JobDesc &j = jobs[ji];
-    const uint32_t t = gtile - j.tile_base;
+    const TileRef ref = order[sh.tile];
+    const JobDesc &j = jobs[ref.job];
+    const uint32_t t = ref.tile;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * kMergeTile;
     const uint32_t d1 = (d0 + kMergeTile) < n ? d0 + kMergeTile : n;
@@ -338,47 +341,61 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         const uint32_t pidx = tid * kPer + k;
         if (f[k]) sh.out[o++] = sh.pos[pidx];
     }
-    if (tid == kMergeThreads - 1) {
-        // Decoupled look-back (one lane): this tile's global output offset.
-        const uint32_t cnt = wave_off + incl;
-        sh.count = cnt;
+    if (tid >= kMergeThreads - 64) {
+        // Decoupled look-back by the last wave: each probe reads the status
+        // granules of 64 predecessors at once (closest first), sums their
+        // counts up to the closest inclusive prefix, and moves 64 further
+        // back only if all 64 were aggregates.
+        const uint32_t cnt = __shfl(wave_off + incl, 63, 64);
         uint64_t *st = status + j.tile_base;
         uint64_t prefix = 0;
         if (t == 0) {
-            __hip_atomic_store(st, kFlagIncl | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(st, kFlagIncl | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(st + t, kFlagAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t k = t - 1;
+            if (lane == 0) __hip_atomic_store(st + t, kFlagAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t base = (int64_t)t - 1;
             uint32_t spins = 0;
             for (;;) {
-                const uint64_t s = __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int64_t k = base - (int64_t)lane;
+                const uint64_t s = k >= 0 ? __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : kFlagIncl;
                 const uint64_t flag = s & ~kCountMask;
-                if (flag == 0) {
-                    if (++spins > (1u << 26)) { // bounded: report instead of hanging
-                        res[j.job_index].invariant = 0xdead;
+                const uint64_t incl_mask = __ballot(flag == kFlagIncl);
+                const uint64_t wait_mask = __ballot(flag == 0);
+                const uint32_t first = incl_mask ? (uint32_t)__builtin_ctzll(incl_mask) : 64u;
+                const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+                if (wait_mask & need) {
+                    if (++spins > (1u << 24)) { // bounded: report instead of hanging
+                        if (lane == 0) res[j.job_index].invariant = 0xdead;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                prefix += s & kCountMask;
-                if (flag == kFlagIncl || k == 0) break;
-                k--;
+                uint64_t c = lane <= first ? (s & kCountMask) : 0;
+                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+                prefix += c;
+                if (first < 64) break;
+                base -= 64;
             }
-            __hip_atomic_store(st + t, kFlagIncl | (prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(st + t, kFlagIncl | (prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        sh.offset = prefix;
-        if (t + 1 == j.tile_count) {
-            // Output shape (write_blocks, compaction.zig:806-850): full data
-            // blocks except the last, full tables except the last.
-            const uint64_t total = prefix + cnt;
-            const uint32_t db = (uint32_t)((total + j.vcm - 1) / j.vcm);
-            const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
-            JobResultDev &r = res[j.job_index];
-            r.value_count = total;
-            r.data_block_count = db;
-            r.table_count = tables;
-            r.block_count = db + tables;
+        if (lane == 0) {
+            sh.count = cnt;
+            sh.offset = prefix;
+            if (t + 1 == j.tile_count) {
+                // Output shape (write_blocks, compaction.zig:806-850): full data
+                // blocks except the last, full tables except the last.
+                const uint64_t total = prefix + cnt;
+                const uint32_t db = (uint32_t)((total + j.vcm - 1) / j.vcm);
+                const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
+                JobResultDev &r = res[j.job_index];
+                r.value_count = total;
+                r.data_block_count = db;
+                r.table_count = tables;
+                r.block_count = db + tables;
+            }
         }
     }
     __syncthreads();
@@ -420,8 +437,8 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
 
 template <int KIND>
 static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
-                       SplitDesc *d_splits, uint64_t *d_status, uint32_t *d_counters, JobResultDev *d_res,
-                       hipStream_t s) {
+                       SplitDesc *d_splits, uint64_t *d_status, uint32_t *d_counters, const TileRef *d_order,
+                       JobResultDev *d_res, hipStream_t s) {
     const JobDesc &f = h_jobs[first];
     const JobDesc &l = h_jobs[first + count - 1];
     const uint32_t split_off = f.split_base;
@@ -432,16 +449,16 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
         hipLaunchKernelGGL(k_partition<KIND>, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs + first, count,
                            split_off, nsplits, d_splits);
     else if (ntiles)
-        hipLaunchKernelGGL(k_merge_tile<KIND>, dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs + first, count,
-                           tile_off, d_counters + first, (const SplitDesc *)d_splits, d_status, d_res);
+        hipLaunchKernelGGL(k_merge_tile<KIND>, dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,
+                           d_counters + first, (const SplitDesc *)d_splits, d_status, d_res);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // Jobs must be grouped by key kind (contiguous runs) by the caller. d_status
 // (one u64 per tile) and d_counters (one u32 per job) must be zero.
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
-                 uint64_t *d_status, uint32_t *d_counters, JobResultDev *d_results, void *stream,
-                 void (*mark)(void *, const char *), void *mark_ctx) {
+                 uint64_t *d_status, uint32_t *d_counters, const TileRef *d_order, JobResultDev *d_results,
+                 void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     auto for_each_kind = [&](auto fn) {
         int first = 0;
@@ -456,10 +473,10 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     auto phase = [&](int ph) {
         return for_each_kind([&](uint32_t kind, int first, int count) {
             switch (kind) {
-            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
-            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
-            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
-            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_results, s);
+            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
+            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
+            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
+            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
             }
         });
     };

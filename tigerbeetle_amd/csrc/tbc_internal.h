@@ -64,6 +64,13 @@ struct SplitDesc {
     uint32_t pad;
 };
 
+// One entry of the batch's tile order: tiles of the jobs of one key kind,
+// interleaved round-robin (job index into the batch's JobDesc array, tile).
+struct TileRef {
+    uint32_t job;
+    uint32_t tile;
+};
+
 struct JobResultDev {
     uint64_t value_count;
     uint32_t data_block_count;
@@ -110,8 +117,8 @@ __device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F bas
 struct hipStream_t_;
 namespace tbc {
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
-                 uint64_t *d_status, uint32_t *d_counters, JobResultDev *d_results, void *stream,
-                 void (*mark)(void *, const char *), void *mark_ctx);
+                 uint64_t *d_status, uint32_t *d_counters, const TileRef *d_order, JobResultDev *d_results,
+                 void *stream, void (*mark)(void *, const char *), void *mark_ctx);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
                   JobResultDev *d_results, uint8_t *d_infos, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx);
