@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from tigerbeetle_amd import Engine, Job, trees  # noqa: E402
+from tigerbeetle_amd.shard import plan_shards, reduce_step  # noqa: E402
 
 METRIC = "compacted input MB/s per GPU and per node (1/2/4/8) + % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -67,7 +68,7 @@ def blocks_of(table: np.ndarray, vcm: int) -> list:
 class Workload:
     """All jobs of one GPU staged in HBM as 1 MiB grid blocks."""
 
-    def __init__(self, eng: Engine, rank: int, jobs: int, bs: int):
+    def __init__(self, eng: Engine, job_ids: list, bs: int):
         self.spec = trees.BY_NAME["transfers.id"]
         self.bs = bs
         lay = self.spec.layout(bs)
@@ -75,8 +76,8 @@ class Workload:
         self.block_count_max = lay["block_count_max"]
         self.jobs, self.bufs = [], []
         self.input_values = 0
-        for j in range(jobs):
-            a, b_tables = gen_job(rank * 1000 + j)
+        for j, gid in enumerate(job_ids):
+            a, b_tables = gen_job(gid)
             tables = [blocks_of(a, self.vcm)] + [blocks_of(t, self.vcm) for t in b_tables]
             nblk = sum(len(t) for t in tables)
             host = np.zeros((nblk, bs), dtype=np.uint8)
@@ -163,7 +164,10 @@ def main() -> None:
 
     bs = 1 << 20
     eng = Engine(device=local, block_size=bs, profile=True)
-    wl = Workload(eng, rank, args.jobs, bs)
+    # Weak scaling: args.jobs jobs per GPU; the global job set is sharded by
+    # bytes (all jobs are the same size here), no data-path collective.
+    plan = plan_shards([1] * (args.jobs * world), world)
+    wl = Workload(eng, plan[rank], bs)
     eng.synchronize()
 
     def step():
@@ -197,16 +201,7 @@ def main() -> None:
     b.release()
     assert res0.value_count == 9 * TABLE and res0.table_count == 9, (res0.value_count, res0.table_count)
 
-    t_max = dt
-    total_bytes = wl.input_bytes
-    if dist:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
-        nb = torch.tensor([float(total_bytes)], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(nb, op=dist.ReduceOp.SUM)
-        total_bytes = int(nb.item())
+    total_bytes, t_max = reduce_step(dist, wl.input_bytes, dt, device=f"cuda:{local}" if dist else None)
     step_s = t_max / args.steps
     value = total_bytes / step_s / 1e6
 
