@@ -199,7 +199,8 @@ def main() -> None:
     b = step()
     res0, _ = b.result(0)
     b.release()
-    assert res0.value_count == 9 * TABLE and res0.table_count == 9, (res0.value_count, res0.table_count)
+    if not os.environ.get("TBC_LIB"):  # ablation builds (timing only) skip the shape check
+        assert res0.value_count == 9 * TABLE and res0.table_count == 9, (res0.value_count, res0.table_count)
 
     total_bytes, t_max = reduce_step(dist, wl.input_bytes, dt, device=f"cuda:{local}" if dist else None)
     step_s = t_max / args.steps

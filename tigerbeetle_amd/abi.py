@@ -11,7 +11,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtbc.so")
+LIB_PATH = os.environ.get("TBC_LIB") or os.path.join(HERE, "libtbc.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "tbc.h")
 
 TBC_OK = 0

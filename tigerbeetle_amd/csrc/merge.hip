@@ -23,6 +23,10 @@
 
 #include "tbc_internal.h"
 
+#ifndef TBC_ABLATE
+#define TBC_ABLATE 0 // timing experiments only: 1 = no copy, 2 = no look-back wait, 4 = no key loads
+#endif
+
 namespace tbc {
 
 template <int KIND> struct KeyLimbs { static constexpr int value = KIND == kKeyTimestamp ? 1 : KIND == kKeyCompositeU128 ? 3 : 2; };
@@ -149,7 +153,6 @@ template <int KL> struct TileShared {
     uint64_t key[KL][kMergeTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
     const uint8_t *ptr[kMergeTile + 3];
     uint8_t tomb[kMergeTile + 4];
-    uint32_t pos[kMergeTile];  // merged position -> entry (0xffffffff = dropped)
     uint32_t out[kMergeTile];  // output order -> entry
     uint32_t seg_pre[2][kSegWindow + 1];
     uint64_t seg_ptr[2][kSegWindow];
@@ -231,8 +234,12 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
         uint32_t tb = 0;
         if (ptrs[r]) {
+#if TBC_ABLATE & 4
+            k.l[0] = (uint64_t)(uintptr_t)ptrs[r];
+#else
             k = load_key<KIND>(ptrs[r], ts);
             if (e < ea) tb = load_tomb(ptrs[r], ts);
+#endif
         }
 #pragma unroll
         for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
@@ -267,65 +274,62 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         return len;
     };
 
-    for (uint32_t q = tid; q < na + nb; q += kMergeThreads) {
-        uint32_t pos, entry;
-        bool surv;
-        if (q < na) {
-            // A element ia = i0 + q at entry q + 1.
-            const uint32_t ia = i0 + q;
-            entry = q + 1;
-            const Key<KL> ka = entry_key(entry);
-            // lower_bound over in-tile B entries: count of B < ka.
-            uint32_t lo = 0, hi = nb;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (key_lt(entry_key(ea + mid), ka)) lo = mid + 1;
-                else hi = mid;
-            }
-            pos = q + lo;
-            bool dedup = true;
-            if (immutable) {
-                const bool next_eq = (ia + 1 < na_all) && key_eq(entry_key(entry + 1), ka);
-                dedup = !next_eq;
-                if (dedup && secondary) dedup = (run_len(ia) & 1) != 0;
-            }
-            const bool b_valid = lo < nb || j1 < nb_all;
-            const bool eq_b = b_valid && key_eq(entry_key(ea + lo), ka);
-            surv = dedup && !(drop && sh.tomb[entry]) && !(secondary && eq_b);
-        } else {
-            // B element jb = j0 + qb at entry ea + qb.
-            const uint32_t qb = q - na;
-            entry = ea + qb;
-            const Key<KL> kb = entry_key(entry);
-            // upper_bound over in-tile A entries [1, na]: count of A <= kb.
-            uint32_t lo = 0, hi = na;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (key_le(entry_key(1 + mid), kb)) lo = mid + 1;
-                else hi = mid;
-            }
-            pos = qb + lo;
-            // Previous A (global index i0 + lo - 1) is entry lo.
-            const bool prev_valid = (i0 + lo) >= 1;
-            bool a_exists = prev_valid && key_eq(entry_key(lo), kb);
-            if (a_exists && immutable && secondary) a_exists = (run_len(i0 + lo - 1) & 1) != 0;
-            surv = !a_exists;
-        }
-        sh.pos[pos] = surv ? entry : 0xffffffffu;
-    }
-    __syncthreads();
-
-    // Exclusive scan of survivor flags in merged order (4 positions per thread).
-    const uint32_t total_pos = na + nb;
+    // Each thread owns merged positions [kPer*tid, kPer*tid + kPer): one
+    // merge-path search in LDS for its start, then a sequential merge (A
+    // first on equal keys) applying the survivor rules to each element.
     constexpr uint32_t kPer = kMergeTile / kMergeThreads;
-    uint32_t f[kPer];
+    const uint32_t total_pos = na + nb;
+    const uint32_t d = kPer * tid < total_pos ? kPer * tid : total_pos;
+    uint32_t a, b;
+    {
+        uint32_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key_le(entry_key(1 + mid), entry_key(ea + d - 1 - mid))) lo = mid + 1;
+            else hi = mid;
+        }
+        a = lo;
+        b = d - lo;
+    }
+    uint32_t f[kPer], ent[kPer];
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; k++) {
-        const uint32_t pidx = tid * kPer + k;
-        f[k] = (pidx < total_pos && sh.pos[pidx] != 0xffffffffu) ? 1u : 0u;
+        f[k] = 0;
+        ent[k] = 0;
+        if (d + k >= total_pos) continue;
+        const bool take_a = a < na && (b >= nb || key_le(entry_key(1 + a), entry_key(ea + b)));
+        bool surv;
+        if (take_a) {
+            // A element ia = i0 + a at entry a + 1; B[b] (entry ea + b) is the next B.
+            const uint32_t ia = i0 + a, e = a + 1;
+            const Key<KL> ka = entry_key(e);
+            bool dedup = true;
+            if (immutable) {
+                const bool next_eq = (ia + 1 < na_all) && key_eq(entry_key(e + 1), ka);
+                dedup = !next_eq;
+                if (dedup && secondary) dedup = (run_len(ia) & 1) != 0;
+            }
+            const bool b_valid = b < nb || j1 < nb_all;
+            const bool eq_b = b_valid && key_eq(entry_key(ea + b), ka);
+            surv = dedup && !(drop && sh.tomb[e]) && !(secondary && eq_b);
+            ent[k] = e;
+            a++;
+        } else {
+            // B element jb = j0 + b at entry ea + b; the previous A (global
+            // index i0 + a - 1) is entry a.
+            const uint32_t e = ea + b;
+            const Key<KL> kb = entry_key(e);
+            bool a_exists = (i0 + a) >= 1 && key_eq(entry_key(a), kb);
+            if (a_exists && immutable && secondary) a_exists = (run_len(i0 + a - 1) & 1) != 0;
+            surv = !a_exists;
+            ent[k] = e;
+            b++;
+        }
+        f[k] = surv ? 1u : 0u;
         sum += f[k];
     }
+    // Block exclusive scan of the survivor counts (threads in merged order).
     uint32_t incl = sum;
     for (int o = 1; o < 64; o <<= 1) {
         uint32_t y = __shfl_up(incl, o, 64);
@@ -335,22 +339,41 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     __syncthreads();
     uint32_t wave_off = 0;
     for (uint32_t w = 0; w < (tid >> 6); w++) wave_off += sh.wave_sums[w];
-    uint32_t o = wave_off + incl - sum;
+    {
+        uint32_t o = wave_off + incl - sum;
 #pragma unroll
-    for (uint32_t k = 0; k < kPer; k++) {
-        const uint32_t pidx = tid * kPer + k;
-        if (f[k]) sh.out[o++] = sh.pos[pidx];
+        for (uint32_t k = 0; k < kPer; k++)
+            if (f[k]) sh.out[o++] = ent[k];
     }
+    if (tid == kMergeThreads - 1) sh.count = wave_off + incl;
+    __syncthreads();
+
+    // Issue the first round of copy loads before the look-back: sources do
+    // not depend on the tile's output offset, so their latency overlaps it.
+    const uint32_t cnt = sh.count;
+    const uint32_t cpv = vs >> 4;
+    const uint32_t cpv_shift = __builtin_ctz(cpv);
+    const uint32_t chunks = (TBC_ABLATE & 1) ? 0 : cnt * cpv;
+    constexpr uint32_t kUnroll = 4;
+    u32x4 pre[kUnroll];
+#pragma unroll
+    for (uint32_t u = 0; u < kUnroll; u++) {
+        const uint32_t c = tid + u * kMergeThreads;
+        if (c < chunks) {
+            const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
+            pre[u] = gld<u32x4>(sh.ptr[sh.out[v]] + 16 * part);
+        }
+    }
+
     if (tid >= kMergeThreads - 64) {
         // Decoupled look-back by the last wave: each probe reads the status
         // granules of 64 predecessors at once (closest first), sums their
         // counts up to the closest inclusive prefix, and moves 64 further
         // back only if all 64 were aggregates.
-        const uint32_t cnt = __shfl(wave_off + incl, 63, 64);
         uint64_t *st = status + j.tile_base;
         uint64_t prefix = 0;
-        if (t == 0) {
-            if (lane == 0) __hip_atomic_store(st, kFlagIncl | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 || (TBC_ABLATE & 2)) {
+            if (lane == 0) __hip_atomic_store(st + t, kFlagIncl | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (lane == 0) __hip_atomic_store(st + t, kFlagAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             int64_t base = (int64_t)t - 1;
@@ -382,7 +405,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
                 __hip_atomic_store(st + t, kFlagIncl | (prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) {
-            sh.count = cnt;
             sh.offset = prefix;
             if (t + 1 == j.tile_count) {
                 // Output shape (write_blocks, compaction.zig:806-850): full data
@@ -402,36 +424,38 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
 
     // Copy survivors, 16 bytes per lane, to data block k = g / vcm, slot
     // k + k / dbcm (table.zig:306-384 block order, compaction.zig:819-835 acquire order).
-    const uint32_t cnt = sh.count;
     const uint64_t g0 = sh.offset;
-    const uint32_t cpv = vs >> 4;
-    const uint32_t cpv_shift = __builtin_ctz(cpv);
     const uint32_t vcm = j.vcm;
     const uint32_t k_start = (uint32_t)(g0 / vcm);
     const uint32_t o_start = (uint32_t)(g0 - (uint64_t)k_start * vcm);
-    const uint32_t chunks = cnt * cpv;
-    constexpr uint32_t kUnroll = 4;
-    for (uint32_t c0 = tid; c0 < chunks; c0 += kMergeThreads * kUnroll) {
+    auto dst_of = [&](uint32_t c) {
+        const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
+        const uint32_t rel = o_start + v;
+        const uint32_t kb = k_start + rel / vcm;
+        const uint32_t ob = rel - (kb - k_start) * vcm;
+        return j.out_blocks + (size_t)data_block_slot(kb, j.dbcm) * j.block_size + kHeaderSize + (size_t)ob * vs +
+               16 * part;
+    };
+#pragma unroll
+    for (uint32_t u = 0; u < kUnroll; u++) {
+        const uint32_t c = tid + u * kMergeThreads;
+        if (c < chunks) gst<u32x4>(dst_of(c), pre[u]);
+    }
+    for (uint32_t c0 = tid + kUnroll * kMergeThreads; c0 < chunks; c0 += kMergeThreads * kUnroll) {
         u32x4 val[kUnroll];
-        uint8_t *dst[kUnroll];
 #pragma unroll
         for (uint32_t u = 0; u < kUnroll; u++) {
             const uint32_t c = c0 + u * kMergeThreads;
-            dst[u] = nullptr;
             if (c < chunks) {
                 const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
-                const uint32_t e = sh.out[v];
-                val[u] = gld<u32x4>(sh.ptr[e] + 16 * part);
-                const uint32_t rel = o_start + v;
-                const uint32_t kb = k_start + rel / vcm;
-                const uint32_t ob = rel - (kb - k_start) * vcm;
-                dst[u] = j.out_blocks + (size_t)data_block_slot(kb, j.dbcm) * j.block_size + kHeaderSize +
-                         (size_t)ob * vs + 16 * part;
+                val[u] = gld<u32x4>(sh.ptr[sh.out[v]] + 16 * part);
             }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < kUnroll; u++)
-            if (dst[u]) gst<u32x4>(dst[u], val[u]);
+        for (uint32_t u = 0; u < kUnroll; u++) {
+            const uint32_t c = c0 + u * kMergeThreads;
+            if (c < chunks) gst<u32x4>(dst_of(c), val[u]);
+        }
     }
 }
 

@@ -21,8 +21,11 @@ constexpr uint32_t kTableInfoSize = 128;
 constexpr uint64_t kTombstoneBit = 1ull << 63;
 
 // Merge tile: merged-sequence positions handled by one workgroup.
-constexpr uint32_t kMergeTile = 1024;
-constexpr uint32_t kMergeThreads = 256;
+#ifndef TBC_MERGE_TILE
+#define TBC_MERGE_TILE 2048
+#endif
+constexpr uint32_t kMergeTile = TBC_MERGE_TILE;
+constexpr uint32_t kMergeThreads = kMergeTile / 4;
 
 enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };
 
