@@ -14,11 +14,13 @@
 //     label rotation: quad p keeps its register and becomes block label+1,
 //     so the only cross-quad move is the round key S[label+1], fetched with
 //     ds_bpermute at the start of the step — off the dependency chain;
-//   * message words are prefetched 4 iterations (32 updates) ahead.
+//   * message words are prefetched a 1 KiB group (32 updates) ahead.
 //
 // Block finishing (Table.Builder.data_block_finish / index_block_finish,
-// src/lsm/table.zig:306-457) is fused here: body checksum, header fields,
-// header checksum, index-block body, TableInfo.
+// src/lsm/table.zig:306-457) is fused here: body assembly (the values are
+// gathered through the merge's route and stored as they are absorbed, so the
+// copy costs no pass of its own), body checksum, header fields, header
+// checksum, index-block body, TableInfo.
 #include <hip/hip_runtime.h>
 
 #include "tbc_internal.h"
@@ -184,45 +186,79 @@ __device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, const TableBase 
     return r;
 }
 
-// Message sources. load_exact: dword at a byte offset, zero beyond `len`
-// (AegisMac.final zero-pads the tail); used only for the last partial
-// 32-byte block. load_fast: an unconditional, always in-bounds load (the
-// offset is clamped) used for whole blocks, so the prefetch ring stays in
-// flight instead of waiting right after each (divergent) load. Offsets are
-// multiples of 4; buffers are readable up to len rounded up to 4.
+// Message sources. Whole 32-byte blocks are read in two stages so that a
+// source with an indirection can run its first stage further ahead:
+//   addr(off)  where the dword at byte `off` lives (the offset is clamped, so
+//              it is always in bounds and the prefetch ring never waits on a
+//              divergent branch);
+//   word(a)    the dword itself;
+//   exact(off) the dword at `off`, zero beyond `len` (AegisMac.final
+//              zero-pads the tail), for the last partial 32-byte block;
+//   sink(off, w) called once for every absorbed dword below `len` (a source
+//              that also materialises the message stores it there).
+// Offsets are multiples of 4; buffers are readable up to len rounded up to 4.
 struct GlobalMsg {
+    using Addr = const uint8_t *;
     const uint8_t *base;
     uint32_t len;
     uint32_t max_off;
     __device__ __forceinline__ GlobalMsg(const uint8_t *b, uint32_t l)
         : base(b), len(l), max_off(l >= 4 ? (l & ~3u) - 4 : 0) {}
-    __device__ __forceinline__ uint32_t load_fast(uint32_t off) const {
-        return gld<uint32_t>(base + (off < max_off ? off : max_off));
-    }
-    __device__ __forceinline__ uint32_t load_exact(uint32_t off) const {
+    __device__ __forceinline__ Addr addr(uint32_t off) const { return base + (off < max_off ? off : max_off); }
+    __device__ __forceinline__ uint32_t word(Addr a) const { return gld<uint32_t>(a); }
+    __device__ __forceinline__ uint32_t exact(uint32_t off) const {
         if (off >= len) return 0;
         uint32_t v = gld<uint32_t>(base + off);
         uint32_t rem = len - off;
         if (rem < 4) v &= (1u << (8 * rem)) - 1u;
         return v;
     }
+    __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
 };
 
 struct LdsMsg {
+    using Addr = uint32_t;
     const uint32_t *base; // dword-aligned LDS pointer
     uint32_t len;
     uint32_t max_off;
     __device__ __forceinline__ LdsMsg(const uint32_t *b, uint32_t l)
         : base(b), len(l), max_off(l >= 4 ? (l & ~3u) - 4 : 0) {}
-    __device__ __forceinline__ uint32_t load_fast(uint32_t off) const {
-        return base[(off < max_off ? off : max_off) >> 2];
-    }
-    __device__ __forceinline__ uint32_t load_exact(uint32_t off) const {
+    __device__ __forceinline__ Addr addr(uint32_t off) const { return off < max_off ? off : max_off; }
+    __device__ __forceinline__ uint32_t word(Addr a) const { return base[a >> 2]; }
+    __device__ __forceinline__ uint32_t exact(uint32_t off) const {
         if (off >= len) return 0;
         uint32_t v = base[off >> 2];
         uint32_t rem = len - off;
         if (rem < 4) v &= (1u << (8 * rem)) - 1u;
         return v;
+    }
+    __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
+};
+
+// A data block body that does not exist yet: value i of the block is wherever
+// route[i] points (an input value chosen by the merge), and every absorbed
+// dword is also stored into the output block — the copy rides on the
+// checksum chain, whose LDS latency leaves the wave's memory pipe idle.
+// len is a whole number of values (16 B or more each), so no dword is partial.
+struct RoutedMsg {
+    using Addr = const uint8_t *;
+    const uint64_t *route;
+    uint8_t *dst;
+    uint32_t len;
+    uint32_t max_off;
+    uint32_t vs_shift, vs_mask;
+    bool store;
+    __device__ __forceinline__ RoutedMsg(const uint64_t *r, uint8_t *d, uint32_t l, uint32_t vs, bool st)
+        : route(r), dst(d), len(l), max_off(l >= 4 ? l - 4 : 0), vs_shift(__builtin_ctz(vs)), vs_mask(vs - 1),
+          store(st) {}
+    __device__ __forceinline__ Addr addr(uint32_t off) const {
+        off = off < max_off ? off : max_off;
+        return (const uint8_t *)gld<uint64_t>(route + (off >> vs_shift)) + (off & vs_mask);
+    }
+    __device__ __forceinline__ uint32_t word(Addr a) const { return gld<uint32_t>(a); }
+    __device__ __forceinline__ uint32_t exact(uint32_t off) const { return off < len ? word(addr(off)) : 0u; }
+    __device__ __forceinline__ void sink(uint32_t off, uint32_t w) const {
+        if (store) gst<uint32_t>(dst + off, w);
     }
 };
 
@@ -261,27 +297,39 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     } while (0)
 
     // Whole 8-update windows of whole 32-byte blocks, in groups of 4 windows
-    // (32 updates, 1 KiB per message): the next group's words are loaded at
-    // the top of each group, a full group ahead of use, so the compiler's
-    // loop back-edge vmcnt(0) finds them landed. The rest (< 8 full blocks +
-    // the partial tail) runs below with exact loads.
+    // (32 updates, 1 KiB per message). At the top of group g the words of
+    // group g+1 are loaded (a full group ahead of use, so the compiler's loop
+    // back-edge vmcnt(0) finds them landed) and the addresses of group g+2
+    // resolved (for a routed message that is a load too). The rest (< 8 full
+    // blocks + the partial tail) runs below with exact loads.
     const uint32_t iters = (len >> 5) >> 3;
     const uint32_t groups = (iters + 3) >> 2;
-    uint32_t cur[8];
-    if (groups > 0) {
+    typename Msg::Addr ad[8];
+    auto resolve = [&](uint32_t base) {
 #pragma unroll
         for (int d = 0; d < 4; d++) {
-            cur[2 * d] = msg.load_fast(256 * d + off_lo);
-            cur[2 * d + 1] = msg.load_fast(256 * d + off_hi);
+            ad[2 * d] = msg.addr(base + 256 * d + off_lo);
+            ad[2 * d + 1] = msg.addr(base + 256 * d + off_hi);
         }
+    };
+    uint32_t cur[8];
+    if (groups > 0) {
+        resolve(0);
+#pragma unroll
+        for (int i = 0; i < 8; i++) cur[i] = msg.word(ad[i]);
+        resolve(1024);
     }
     for (uint32_t grp = 0; grp < groups; grp++) {
         uint32_t nxt[8];
-        const uint32_t base = 1024 * (grp + 1);
+#pragma unroll
+        for (int i = 0; i < 8; i++) nxt[i] = msg.word(ad[i]);
+        resolve(1024 * (grp + 2));
 #pragma unroll
         for (int d = 0; d < 4; d++) {
-            nxt[2 * d] = msg.load_fast(base + 256 * d + off_lo);
-            nxt[2 * d + 1] = msg.load_fast(base + 256 * d + off_hi);
+            if (4 * grp + d < iters) {
+                msg.sink(1024 * grp + 256 * d + off_lo, cur[2 * d]);
+                msg.sink(1024 * grp + 256 * d + off_hi, cur[2 * d + 1]);
+            }
         }
 #pragma unroll
         for (int d = 0; d < 4; d++) {
@@ -306,7 +354,9 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
         const uint32_t lab = (p + u + 1) & 7;
         const bool nd = (lab & 3) == 0;
         uint32_t key = bpermute(key_src, x);
-        uint32_t m = nd ? msg.load_exact(32 * u + 4 * (lab + c)) : 0u;
+        const uint32_t off = 32 * u + 4 * (lab + c);
+        uint32_t m = nd ? msg.exact(off) : 0u;
+        if (nd && off < len) msg.sink(off, m);
         x = aes_col(sT, tb, x, key ^ m);
     }
     // Finalise: tmp = (LE64(len*8) || 0) ^ S2; 7 x update(tmp, tmp).
@@ -445,7 +495,9 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
     const uint32_t slot = data_block_slot(k, j.dbcm);
     uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
 
-    GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
+    // The body is assembled here: values gathered through the merge's route
+    // and stored into the block as they are absorbed.
+    RoutedMsg body(j.route + first, blk + kHeaderSize, cnt * j.value_size, j.value_size, writer);
     const uint32_t body_tag = aegis_mac32(sT, body);
 
     HeaderFields h;

@@ -84,7 +84,27 @@ struct tbc_engine {
     hipStream_t stream = nullptr;
     Arena dev, host;
     std::vector<hipEvent_t> event_pool;
+    // Route buffer (8 bytes per input value of a batch). Batches run in stream
+    // order, so one buffer serves them all; it only grows (after a stream
+    // drain), which a steady-state caller sees once.
+    uint64_t *route = nullptr;
+    uint64_t route_words = 0;
 };
+
+static bool ensure_route(tbc_engine *e, uint64_t words) {
+    if (words <= e->route_words) return true;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return false;
+    if (e->route) hipFree(e->route);
+    e->route = nullptr;
+    e->route_words = 0;
+    const uint64_t want = align_up(words, 1ull << 20);
+    if (hipMalloc((void **)&e->route, want * 8) != hipSuccess) {
+        e->route = nullptr;
+        return false;
+    }
+    e->route_words = want;
+    return true;
+}
 
 struct tbc_batch {
     tbc_engine *engine = nullptr;
@@ -156,6 +176,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
     hipHostFree(e->host.base);
     hipFree(e->dev.base);
+    if (e->route) hipFree(e->route);
     hipStreamDestroy(e->stream);
     delete e;
 }
@@ -356,11 +377,20 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     // Group jobs by key kind (one kernel instantiation per kind) and assign
     // batch-wide bases in that order.
     std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hj[x].key_kind < hj[y].key_kind; });
+    uint64_t route_words = 0;
+    for (uint32_t i = 0; i < count; i++) route_words += (uint64_t)hj[i].a.n + hj[i].b.n;
+    if (!ensure_route(e, route_words)) {
+        delete b;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
     std::vector<JobDesc> sj(count);
     uint32_t tiles = 0, splits = 0, dblocks = 0, tables = 0, infos = 0;
+    uint64_t route_at = 0;
     for (uint32_t k = 0; k < count; k++) {
         sj[k] = hj[order[k]];
         JobDesc &d = sj[k];
+        d.route = e->route + route_at;
+        route_at += (uint64_t)d.a.n + d.b.n;
         d.tile_base = tiles;
         d.split_base = splits;
         d.dblock_base = dblocks;

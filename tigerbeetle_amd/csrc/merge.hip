@@ -16,15 +16,17 @@
 //   B[j] is written       iff A has no dedup survivor with the same key
 //                          (B tombstones are never dropped, :775-779).
 //
-// Kernels: merge-path split per tile boundary -> per-tile survivor count ->
-// per-job exclusive scan (also yields data-block / table counts) -> per-tile
-// write of survivors straight into their output data-block slots.
+// Kernels: merge-path split per tile boundary -> per tile: survivor flags,
+// block scan, decoupled look-back for the job-global output offset (the last
+// tile also yields the data-block / table counts) -> the route (one source
+// pointer per output value, in output order). k_data_blocks then gathers the
+// values through the route into the output blocks as it checksums them.
 #include <hip/hip_runtime.h>
 
 #include "tbc_internal.h"
 
 #ifndef TBC_ABLATE
-#define TBC_ABLATE 0 // timing experiments only: 1 = no copy, 2 = no look-back wait, 4 = no key loads
+#define TBC_ABLATE 0 // timing experiments only: 2 = no look-back wait, 4 = no key loads
 #endif
 
 namespace tbc {
@@ -348,21 +350,15 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     if (tid == kMergeThreads - 1) sh.count = wave_off + incl;
     __syncthreads();
 
-    // Issue the first round of copy loads before the look-back: sources do
-    // not depend on the tile's output offset, so their latency overlaps it.
+    // Source pointers of this tile's survivors, in output order; read from
+    // LDS before the look-back so only the stores wait for the tile's offset.
     const uint32_t cnt = sh.count;
-    const uint32_t cpv = vs >> 4;
-    const uint32_t cpv_shift = __builtin_ctz(cpv);
-    const uint32_t chunks = (TBC_ABLATE & 1) ? 0 : cnt * cpv;
-    constexpr uint32_t kUnroll = 4;
-    u32x4 pre[kUnroll];
+    constexpr uint32_t kRoutePer = kMergeTile / kMergeThreads;
+    uint64_t src[kRoutePer];
 #pragma unroll
-    for (uint32_t u = 0; u < kUnroll; u++) {
-        const uint32_t c = tid + u * kMergeThreads;
-        if (c < chunks) {
-            const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
-            pre[u] = gld<u32x4>(sh.ptr[sh.out[v]] + 16 * part);
-        }
+    for (uint32_t u = 0; u < kRoutePer; u++) {
+        const uint32_t o = tid + u * kMergeThreads;
+        src[u] = o < cnt ? (uint64_t)(uintptr_t)sh.ptr[sh.out[o]] : 0;
     }
 
     if (tid >= kMergeThreads - 64) {
@@ -422,40 +418,14 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     }
     __syncthreads();
 
-    // Copy survivors, 16 bytes per lane, to data block k = g / vcm, slot
-    // k + k / dbcm (table.zig:306-384 block order, compaction.zig:819-835 acquire order).
-    const uint64_t g0 = sh.offset;
-    const uint32_t vcm = j.vcm;
-    const uint32_t k_start = (uint32_t)(g0 / vcm);
-    const uint32_t o_start = (uint32_t)(g0 - (uint64_t)k_start * vcm);
-    auto dst_of = [&](uint32_t c) {
-        const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
-        const uint32_t rel = o_start + v;
-        const uint32_t kb = k_start + rel / vcm;
-        const uint32_t ob = rel - (kb - k_start) * vcm;
-        return j.out_blocks + (size_t)data_block_slot(kb, j.dbcm) * j.block_size + kHeaderSize + (size_t)ob * vs +
-               16 * part;
-    };
+    // Route: output position g of the job -> pointer to the surviving value.
+    // The value bytes are moved by k_data_blocks, which gathers them through
+    // the route while its (latency-bound) AEGIS chain runs (aegis.hip, RoutedMsg).
+    uint64_t *route = j.route + sh.offset;
 #pragma unroll
-    for (uint32_t u = 0; u < kUnroll; u++) {
-        const uint32_t c = tid + u * kMergeThreads;
-        if (c < chunks) gst<u32x4>(dst_of(c), pre[u]);
-    }
-    for (uint32_t c0 = tid + kUnroll * kMergeThreads; c0 < chunks; c0 += kMergeThreads * kUnroll) {
-        u32x4 val[kUnroll];
-#pragma unroll
-        for (uint32_t u = 0; u < kUnroll; u++) {
-            const uint32_t c = c0 + u * kMergeThreads;
-            if (c < chunks) {
-                const uint32_t v = c >> cpv_shift, part = c & (cpv - 1);
-                val[u] = gld<u32x4>(sh.ptr[sh.out[v]] + 16 * part);
-            }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kUnroll; u++) {
-            const uint32_t c = c0 + u * kMergeThreads;
-            if (c < chunks) gst<u32x4>(dst_of(c), val[u]);
-        }
+    for (uint32_t u = 0; u < kRoutePer; u++) {
+        const uint32_t o = tid + u * kMergeThreads;
+        if (o < cnt) gst<uint64_t>(route + o, src[u]);
     }
 }
 

@@ -5,10 +5,12 @@
 //   u64 seg_ptr[...]        per-stream segment value pointers
 //   u32 seg_pre[...]        per-stream segment prefix counts (nseg + 1 each)
 //   u64 addresses[...]      acquire-order block addresses per job
-//   u32 splits[...]         merge-path A-splits at every tile boundary (tiles + 1 per job)
-//   u32 tile_counts[...]    survivors per tile, then exclusive tile offsets
+//   SplitDesc splits[...]   merge-path A-splits at every tile boundary (tiles + 1 per job)
+//   u64 status[...]         per-tile look-back granules; u32 tile counters per job
 //   JobResultDev[count]     device results (copied to pinned host memory at the end)
 //   u8  table_infos[...]    128-byte ManifestNode.TableInfo per output table
+// plus the engine's route buffer (grown on demand, outside the arena):
+//   u64 route[...]          per job, output position -> source value pointer
 #pragma once
 
 #include <stdint.h>
@@ -51,6 +53,7 @@ struct JobDesc {
     uint32_t address_count;
     uint32_t pad1;
     uint8_t *out_blocks;
+    uint64_t *route; // output position -> source value pointer (a.n + b.n entries)
     // Batch bases (global grid indices).
     uint32_t tile_base, tile_count;      // merge tiles
     uint32_t split_base;                 // tile_count + 1 splits
