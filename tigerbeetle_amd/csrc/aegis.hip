@@ -186,6 +186,16 @@ __device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, const TableBase 
     return r;
 }
 
+// One AEGIS update step of lane (p, c): S'[label+1] = AESRound(S[label]) ^
+// S[label+1] ^ m, with the round key S[label+1] = x of quad p+1.
+struct StepBpermute {
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t key_src,
+                                                    uint32_t x, uint32_t m) {
+        const uint32_t key = bpermute(key_src, x);
+        return aes_col(sT, tb, x, key ^ m);
+    }
+};
+
 // Message sources. Whole 32-byte blocks are read in two stages so that a
 // source with an indirection can run its first stage further ahead:
 //   addr(off)  where the dword at byte `off` lives (the offset is clamped, so
@@ -258,14 +268,56 @@ struct RoutedMsg {
     __device__ __forceinline__ uint32_t word(Addr a) const { return gld<uint32_t>(a); }
     __device__ __forceinline__ uint32_t exact(uint32_t off) const { return off < len ? word(addr(off)) : 0u; }
     __device__ __forceinline__ void sink(uint32_t off, uint32_t w) const {
-        if (store) gst<uint32_t>(dst + off, w);
+        if (store && off < len) gst<uint32_t>(dst + off, w);
     }
 };
 
-// AEGIS-128L MAC of one message per 32-lane group. Both groups of a wave
-// must have the same length (control flow is wave-uniform). Returns column c
-// of the 128-bit tag in every lane (c = lane & 3).
-template <class Msg>
+// One AEGIS update step with the round key fetched by VALU lane moves instead
+// of LDS: row_ror:12 brings quad p+1 within a 16-lane row, and quads 3 and 7
+// of a 32-lane group take it from the other row of the pair, which
+// permlane16_swap supplies. The four table reads are issued first; the key
+// and message word are folded in under their latency (tools/aegis_lab.hip:
+// 59 vs 64 ns per update at one wave per SIMD).
+__device__ __forceinline__ uint32_t key_valu(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x12C, 0xf, 0xf, false); // row_ror:12
+    const auto sw = __builtin_amdgcn_permlane16_swap(r, r, false, false);
+    const uint32_t other = (lane & 16) ? sw[0] : sw[1];
+    return ((lane & 15) >= 12) ? other : r;
+}
+
+struct StepValuKey {
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t, uint32_t x,
+                                                    uint32_t m) {
+        const uint32_t a0 = __builtin_amdgcn_perm(x, tb.lo, 0x03020400u);
+        const uint32_t a1 = __builtin_amdgcn_perm(x, tb.lo, 0x03020500u);
+        const uint32_t a2 = __builtin_amdgcn_perm(x, tb.hi, 0x03020600u);
+        const uint32_t a3 = __builtin_amdgcn_perm(x, tb.hi, 0x03020700u);
+        const uint32_t t0 = lds_u32(sT, a0);
+        const uint32_t t1 = lds_u32(sT, a1 + 128);
+        const uint32_t t2 = lds_u32(sT, a2);
+        const uint32_t t3 = lds_u32(sT, a3 + 128);
+        uint32_t r = (key_valu(x) ^ m) ^ t0;
+        r ^= quad_perm<1, 2, 3, 0>(t1);
+        r ^= quad_perm<2, 3, 0, 1>(t2);
+        r ^= quad_perm<3, 0, 1, 2>(t3);
+        return r;
+    }
+};
+
+// AEGIS-128L MAC of one message per 32-lane group. The two groups of a wave
+// may absorb messages of different lengths: both lengths are read into
+// scalars, so the control flow stays wave-uniform. Returns column c of the
+// 128-bit tag in every lane (c = lane & 3).
+//
+// Schedule, in 8-update windows (256 message bytes): whole windows of the
+// shorter message run in the lean loop (`fast`, pure absorb); the windows
+// where the shorter message ends (its partial tail and 7 finalisation
+// updates) run per-step mode selection (`slow`); then the longer message
+// continues in the lean loop (the finished group's lanes compute junk, its
+// tag is already captured) and ends the same way. Every load stays inside
+// its own group's message (addresses are clamped to it).
+template <class Msg, class Step = StepValuKey>
 __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &msg) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t g = lane & 31, half = lane & 32;
@@ -274,10 +326,11 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
 
     const TableBase tb;
     uint32_t x = c_seed.s[p][c];
-    // Both groups of the wave share the length: make that provable so the
-    // loop control is scalar.
-    const uint32_t len = __builtin_amdgcn_readfirstlane(msg.len);
+    const uint32_t len = msg.len; // this group's length
     const uint32_t n_abs = (len + 31) >> 5;
+    const uint32_t len_0 = __builtin_amdgcn_readlane(len, 0), len_1 = __builtin_amdgcn_readlane(len, 32);
+    const uint32_t abs_0 = (len_0 + 31) >> 5, abs_1 = (len_1 + 31) >> 5;
+    const uint32_t len_s = len_0 < len_1 ? len_0 : len_1, len_l = len_0 < len_1 ? len_1 : len_0;
 
     // Which steps (u mod 4) inject a message word into this lane, and where
     // that word sits inside each 256-byte (8-update) window.
@@ -291,111 +344,136 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
 
 #define AEGIS_STEP(K, WLO, WHI)                                                   \
     do {                                                                          \
-        uint32_t key_ = bpermute(key_src, x);                                     \
         uint32_t m_ = need[(K)&3] ? ((K) < 4 ? (WLO) : (WHI)) : 0u;               \
-        x = aes_col(sT, tb, x, key_ ^ m_);                                        \
+        x = Step::step(sT, tb, key_src, x, m_);                                   \
     } while (0)
 
-    // Whole 8-update windows of whole 32-byte blocks, in groups of 4 windows
-    // (32 updates, 1 KiB per message). At the top of group g the words of
-    // group g+1 are loaded (a full group ahead of use, so the compiler's loop
-    // back-edge vmcnt(0) finds them landed) and the addresses of group g+2
-    // resolved (for a routed message that is a load too). The rest (< 8 full
-    // blocks + the partial tail) runs below with exact loads.
-    const uint32_t iters = (len >> 5) >> 3;
-    const uint32_t groups = (iters + 3) >> 2;
-    typename Msg::Addr ad[8];
-    auto resolve = [&](uint32_t base) {
+    // Lean loop over windows [w0, w1) of whole 32-byte blocks of both
+    // messages, in groups of 4 windows (32 updates, 1 KiB per message). At
+    // the top of each group the words of the next group are loaded (a full
+    // group ahead of use, so the compiler's loop back-edge vmcnt(0) finds
+    // them landed) and the addresses of the group after resolved (for a
+    // routed message that is a load too).
+    auto fast = [&](uint32_t w0, uint32_t w1) {
+        if (w0 >= w1) return;
+        const uint32_t groups = (w1 - w0 + 3) >> 2;
+        typename Msg::Addr ad[8];
+        auto resolve = [&](uint32_t base) {
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-            ad[2 * d] = msg.addr(base + 256 * d + off_lo);
-            ad[2 * d + 1] = msg.addr(base + 256 * d + off_hi);
-        }
-    };
-    uint32_t cur[8];
-    if (groups > 0) {
-        resolve(0);
+            for (int d = 0; d < 4; d++) {
+                ad[2 * d] = msg.addr(base + 256 * d + off_lo);
+                ad[2 * d + 1] = msg.addr(base + 256 * d + off_hi);
+            }
+        };
+        uint32_t cur[8];
+        resolve(256 * w0);
 #pragma unroll
         for (int i = 0; i < 8; i++) cur[i] = msg.word(ad[i]);
-        resolve(1024);
-    }
-    for (uint32_t grp = 0; grp < groups; grp++) {
-        uint32_t nxt[8];
+        resolve(256 * w0 + 1024);
+        for (uint32_t grp = 0; grp < groups; grp++) {
+            const uint32_t wg = w0 + 4 * grp;
+            uint32_t nxt[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) nxt[i] = msg.word(ad[i]);
-        resolve(1024 * (grp + 2));
+            for (int i = 0; i < 8; i++) nxt[i] = msg.word(ad[i]);
+            resolve(256 * wg + 2048);
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-            if (4 * grp + d < iters) {
-                msg.sink(1024 * grp + 256 * d + off_lo, cur[2 * d]);
-                msg.sink(1024 * grp + 256 * d + off_hi, cur[2 * d + 1]);
+            for (int d = 0; d < 4; d++) {
+                if (wg + d < w1) {
+                    msg.sink(256 * (wg + d) + off_lo, cur[2 * d]);
+                    msg.sink(256 * (wg + d) + off_hi, cur[2 * d + 1]);
+                }
             }
-        }
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-            if (4 * grp + d < iters) {
-                const uint32_t cl = cur[2 * d], ch = cur[2 * d + 1];
-                AEGIS_STEP(0, cl, ch);
-                AEGIS_STEP(1, cl, ch);
-                AEGIS_STEP(2, cl, ch);
-                AEGIS_STEP(3, cl, ch);
-                AEGIS_STEP(4, cl, ch);
-                AEGIS_STEP(5, cl, ch);
-                AEGIS_STEP(6, cl, ch);
-                AEGIS_STEP(7, cl, ch);
+            for (int d = 0; d < 4; d++) {
+                if (wg + d < w1) {
+                    const uint32_t cl = cur[2 * d], ch = cur[2 * d + 1];
+                    AEGIS_STEP(0, cl, ch);
+                    AEGIS_STEP(1, cl, ch);
+                    AEGIS_STEP(2, cl, ch);
+                    AEGIS_STEP(3, cl, ch);
+                    AEGIS_STEP(4, cl, ch);
+                    AEGIS_STEP(5, cl, ch);
+                    AEGIS_STEP(6, cl, ch);
+                    AEGIS_STEP(7, cl, ch);
+                }
             }
-        }
 #pragma unroll
-        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
-    }
+            for (int i = 0; i < 8; i++) cur[i] = nxt[i];
+        }
+    };
 #undef AEGIS_STEP
-    // Remaining (< 8) absorb updates.
-    for (uint32_t u = iters * 8; u < n_abs; u++) {
-        const uint32_t lab = (p + u + 1) & 7;
-        const bool nd = (lab & 3) == 0;
-        uint32_t key = bpermute(key_src, x);
-        const uint32_t off = 32 * u + 4 * (lab + c);
-        uint32_t m = nd ? msg.exact(off) : 0u;
-        if (nd && off < len) msg.sink(off, m);
-        x = aes_col(sT, tb, x, key ^ m);
+
+    // Windows [w0, w1) with per-step modes: absorb (exact words, zero past
+    // len), finalise (tmp = (LE64(len*8) || 0) ^ S2, injected 7 times), or
+    // frozen once the group's 7 finalisation updates are done; the tag
+    // (S0 ^ ... ^ S6) is captured right after the last one.
+    uint32_t tmp = 0, tag = 0;
+    auto slow = [&](uint32_t w0, uint32_t w1) {
+        for (uint32_t w = w0; w < w1; w++) {
+            const uint32_t o_lo = 256 * w + off_lo, o_hi = 256 * w + off_hi;
+            const uint32_t wl = msg.exact(o_lo), wh = msg.exact(o_hi);
+            if (o_lo < len) msg.sink(o_lo, wl);
+            if (o_hi < len) msg.sink(o_hi, wh);
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) {
+                const uint32_t u = 8 * w + k;
+                if (u == abs_0 || u == abs_1) { // a group starts finalising (scalar test)
+                    const uint32_t q2 = (2 - n_abs) & 7;
+                    const uint64_t bits = (uint64_t)len * 8;
+                    uint32_t t = bpermute((half + (q2 << 2) + c) << 2, x);
+                    t ^= c == 0 ? (uint32_t)bits : c == 1 ? (uint32_t)(bits >> 32) : 0u;
+                    if (u == n_abs) tmp = t;
+                }
+                const uint32_t word = u < n_abs ? (k < 4 ? wl : wh) : tmp;
+                const uint32_t xn = Step::step(sT, tb, key_src, x, need[k & 3] ? word : 0u);
+                x = u < n_abs + 7 ? xn : x;
+                if (u + 1 == abs_0 + 7 || u + 1 == abs_1 + 7) { // a group has finished (scalar test)
+                    const uint32_t q7 = (7 - (n_abs + 7)) & 7;
+                    const uint32_t s7 = bpermute((half + (q7 << 2) + c) << 2, x);
+                    uint32_t t = x;
+                    t ^= (uint32_t)__shfl_xor((int)t, 4, 64);
+                    t ^= (uint32_t)__shfl_xor((int)t, 8, 64);
+                    t ^= (uint32_t)__shfl_xor((int)t, 16, 64);
+                    if (u + 1 == n_abs + 7) tag = t ^ s7;
+                }
+            }
+        }
+    };
+
+    const uint32_t win_s = len_s >> 8, win_l = len_l >> 8;    // whole windows
+    const uint32_t end_s = (((len_s + 31) >> 5) + 14) >> 3;    // windows until finalised
+    const uint32_t end_l = (((len_l + 31) >> 5) + 14) >> 3;
+    fast(0, win_s);
+    if (end_s <= win_l) {
+        slow(win_s, end_s);
+        fast(end_s, win_l);
+        slow(win_l, end_l);
+    } else {
+        slow(win_s, end_l);
     }
-    // Finalise: tmp = (LE64(len*8) || 0) ^ S2; 7 x update(tmp, tmp).
-    const uint32_t q2 = (2 - n_abs) & 7;
-    const uint64_t bits = (uint64_t)len * 8;
-    uint32_t tmp = bpermute((half + (q2 << 2) + c) << 2, x);
-    tmp ^= c == 0 ? (uint32_t)bits : c == 1 ? (uint32_t)(bits >> 32) : 0u;
-    for (uint32_t f = 0; f < 7; f++) {
-        const uint32_t u = n_abs + f;
-        const bool nd = ((p + u + 1) & 3) == 0;
-        uint32_t key = bpermute(key_src, x);
-        x = aes_col(sT, tb, x, key ^ (nd ? tmp : 0u));
-    }
-    // tag = S0 ^ ... ^ S6: xor over all 8 blocks, then remove block 7.
-    const uint32_t q7 = (7 - (n_abs + 7)) & 7;
-    uint32_t s7 = bpermute((half + (q7 << 2) + c) << 2, x);
-    uint32_t t = x;
-    t ^= (uint32_t)__shfl_xor((int)t, 4, 64);
-    t ^= (uint32_t)__shfl_xor((int)t, 8, 64);
-    t ^= (uint32_t)__shfl_xor((int)t, 16, 64);
-    return t ^ s7;
+    return tag;
 }
 
 // --------------------------------------------------------------------------
 // Kernels.
 // --------------------------------------------------------------------------
 
-// tbc_checksum_batch: one message per wave (both groups compute it).
+// tbc_checksum_batch: two messages per wave, one per 32-lane group (an odd
+// last message is computed by both groups, written once). Every pointer must
+// be readable (the host substitutes a valid one for empty messages).
 __global__ __launch_bounds__(1024) void k_checksum_batch(const uint64_t *ptrs, const uint64_t *lens, uint32_t count,
                                                        uint8_t *out) {
     __shared__ uint32_t sT[kTableDwords];
     load_tables(sT);
     __syncthreads();
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (wave >= count) return;
-    GlobalMsg m((const uint8_t *)ptrs[wave], (uint32_t)lens[wave]);
-    uint32_t tag = aegis_mac32(sT, m);
+    if (2 * wave >= count) return;
     const uint32_t lane = threadIdx.x & 63;
-    if (lane < 4) gst<uint32_t>(out + 16 * (size_t)wave + 4 * lane, tag);
+    const uint32_t mine = 2 * wave + (lane >> 5);
+    const uint32_t i = mine < count ? mine : mine - 1;
+    GlobalMsg m((const uint8_t *)ptrs[i], (uint32_t)lens[i]);
+    uint32_t tag = aegis_mac32(sT, m);
+    if ((lane & 31) < 4 && mine < count) gst<uint32_t>(out + 16 * (size_t)i + 4 * (lane & 3), tag);
 }
 
 __device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return gld<uint64_t>(p); }
@@ -458,37 +536,38 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
 }
 
 // Data blocks: data_block_finish (table.zig:306-384) for every output data
-// block. A wave checksums two full blocks; the last (possibly partial) block
-// of a job gets a wave of its own so both groups always share a length.
-__global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, const JobResultDev *res) {
+// block. Blocks are numbered batch-wide by their upper bound (job base + k);
+// wave w takes blocks 2w and 2w+1, one per 32-lane group, whatever their
+// lengths (aegis_mac32 takes two lengths), so a batch needs only
+// ceil(blocks / 2) waves -- one per SIMD for config 2's 2,044 blocks. A group
+// whose block does not exist (dedup left fewer blocks than the bound)
+// mirrors its partner's block without writing, so all its loads stay valid.
+__global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
+                                                      const JobResultDev *res) {
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[16][2][64];
     load_tables(sT);
     __syncthreads();
     const uint32_t wave_in_block = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wave_in_block;
-    const int ji = find_job(jobs, njobs, wave, [](const JobDesc &d) { return d.dblock_base; });
-    const JobDesc &j = jobs[ji];
-    const uint32_t w = wave - j.dblock_base;
-    if (w >= j.dblock_max) return;
-    const uint32_t db = res[j.job_index].data_block_count;
-    const uint64_t n_out = res[j.job_index].value_count;
-    if (db == 0) return;
-    const uint32_t nfull = db - 1;
-    const uint32_t pair_waves = (nfull + 1) / 2;
-    uint32_t blk_lo, blk_hi;
-    if (w < pair_waves) {
-        blk_lo = 2 * w;
-        blk_hi = (2 * w + 1 < nfull) ? 2 * w + 1 : 2 * w;
-    } else if (w == pair_waves) {
-        blk_lo = blk_hi = db - 1;
-    } else {
-        return;
-    }
     const uint32_t lane = threadIdx.x & 63;
     const bool upper = lane >= 32;
-    const uint32_t k = upper ? blk_hi : blk_lo;
-    const bool writer = !(upper && blk_hi == blk_lo);
+    auto locate = [&](uint32_t m, int &ji_, uint32_t &k_) {
+        ji_ = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
+        k_ = m - jobs[ji_].dblock_base;
+        return m < total && k_ < res[jobs[ji_].job_index].data_block_count;
+    };
+    const uint32_t mine = 2 * wave + (upper ? 1u : 0u);
+    int ji;
+    uint32_t k;
+    const bool live = locate(mine, ji, k);
+    const bool live_lo = __builtin_amdgcn_readlane((int)live, 0) != 0;
+    const bool live_hi = __builtin_amdgcn_readlane((int)live, 32) != 0;
+    if (!live_lo && !live_hi) return;
+    if (!live) locate(mine ^ 1u, ji, k); // mirror the partner's block, write nothing
+    const bool writer = live;
+    const JobDesc &j = jobs[ji];
+    const uint64_t n_out = res[j.job_index].value_count;
     const uint64_t first = (uint64_t)k * j.vcm;
     const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
     const uint32_t size = kHeaderSize + cnt * j.value_size;
@@ -648,9 +727,10 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint
                   void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     if (total_dblocks) {
-        const uint32_t wpb = waves_per_block(total_dblocks);
-        hipLaunchKernelGGL(k_data_blocks, dim3((total_dblocks + wpb - 1) / wpb), dim3(64 * wpb), 0, s, d_jobs,
-                           njobs, (const JobResultDev *)d_results);
+        const uint32_t waves = (total_dblocks + 1) / 2;
+        const uint32_t wpb = waves_per_block(waves);
+        hipLaunchKernelGGL(k_data_blocks, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, s, d_jobs, njobs,
+                           total_dblocks, (const JobResultDev *)d_results);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "data_blocks");

@@ -256,7 +256,7 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
     uint64_t *hp = (uint64_t *)h;
     uint64_t *hl = hp + count;
     for (uint32_t i = 0; i < count; i++) {
-        hp[i] = (uint64_t)(uintptr_t)messages[i];
+        hp[i] = lengths[i] ? (uint64_t)(uintptr_t)messages[i] : (uint64_t)(uintptr_t)d; // empty: any readable pointer
         hl[i] = lengths[i];
     }
     tbc_status st = TBC_OK;
@@ -367,7 +367,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         d.address_count = c.address_count;
         d.out_blocks = (uint8_t *)c.output_blocks;
         d.tile_count = (uint32_t)((n + kMergeTile - 1) / kMergeTile);
-        d.dblock_max = db_max ? (uint32_t)((db_max - 1 + 1) / 2 + 1) : 0;
+        d.dblock_max = (uint32_t)db_max;
         d.table_max = (uint32_t)tables_max;
         d.job_index = i;
         seg_words += 2ull * (c.segment_count_a + c.segment_count_b) + 2;

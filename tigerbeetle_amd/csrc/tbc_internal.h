@@ -57,7 +57,7 @@ struct JobDesc {
     // Batch bases (global grid indices).
     uint32_t tile_base, tile_count;      // merge tiles
     uint32_t split_base;                 // tile_count + 1 splits
-    uint32_t dblock_base, dblock_max;    // data-block checksum groups (upper bound)
+    uint32_t dblock_base, dblock_max;    // data blocks (upper bound), batch-wide numbering
     uint32_t table_base, table_max;      // index-block groups (upper bound)
     uint32_t info_base;                  // first TableInfo slot in the batch's info buffer
     uint32_t job_index;
