@@ -142,6 +142,30 @@ def cpu_baseline(budget_s: float = 12.0, bs: int = 1 << 20) -> dict:
                       f"(single thread, AES-NI={bool(olib().tbo_has_aesni())}) on {cpu}"}
 
 
+# bench kernel label -> rocprofv3 kernel symbol (tools/traffic.py short names)
+KERNEL_SYMBOL = {"merge_partition": "k_partition", "merge": "k_merge_tile", "data_blocks": "k_data_blocks",
+                 "index_blocks": "k_index_blocks"}
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the PMC passes committed under
+    profiles/*/traffic.json (tools/profile.sh + tools/traffic.py), used only
+    when that profile was taken with this very libtbc.so (md5 match)."""
+    import glob
+    import hashlib
+    from tigerbeetle_amd import abi
+    try:
+        md5 = hashlib.md5(open(abi.LIB_PATH, "rb").read()).hexdigest()
+    except OSError:
+        return None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+        d = json.load(open(f))
+        k = d.get("kernels", {}).get(KERNEL_SYMBOL.get(kernel, kernel))
+        if d.get("lib_md5") == md5 and k:
+            return k["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +251,7 @@ def main() -> None:
     kt_us = per_step[dominant]
     achieved = alg_bytes.get(dominant, R) / (kt_us * 1e-6) / 1e9
     job_bytes = R + W_data + W_index
+    traffic, traffic_src = pmc_traffic(dominant)
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -245,7 +270,8 @@ def main() -> None:
                    "input_bytes_per_gpu": wl.input_bytes, "block_size": bs, "parallelism": f"shard-by-job x{world}"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "alg_bytes_per_launch": alg_bytes.get(dominant, R)},
         "job_roofline": {"bytes": job_bytes, "achieved": round(job_bytes / step_s / 1e9, 1), "unit": "GB/s",
                          "frac": round(job_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},

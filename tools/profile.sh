@@ -1,0 +1,21 @@
+#!/bin/bash
+# One round's measurement on the GPU box (run through gpurun):
+#   1. bench.py default line (with the CPU baseline)        -> bench.json
+#   2. rocprofv3 --kernel-trace --stats over the same bench  -> trace/
+#   3. one --pmc pass per TCC counter (FETCH_SIZE, WRITE_SIZE), each its own
+#      run (MI355X_MICROARCH.md: they do not fit one pass)   -> fetch/, write/
+# Every GPU step has its own time limit and the steps are chained with &&.
+# Summarise afterwards on the CPU with tools/traffic.py.
+set -e -o pipefail
+export TMPDIR=/tmp
+TAG=${1:?usage: profile.sh TAG}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+ARGS="--steps 10 --warmup 3"
+timeout -k 10 240 python -u bench.py $ARGS > $OUT/bench.log 2>&1
+tail -1 $OUT/bench.log > $OUT/bench.json
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 -u bench.py $ARGS --no-cpu-baseline > $OUT/trace.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/write.log 2>&1
+md5sum tigerbeetle_amd/libtbc.so > $OUT/lib.md5
+echo PROFILE_OK

@@ -1,0 +1,67 @@
+"""Summarise a tools/profile.sh run into profiles/<tag>/.
+
+    python tools/traffic.py gpurun_out/prof_<tag> profiles/<tag>
+
+Writes kernel_stats.csv (rocprofv3 --stats), bench.json, and traffic.json:
+per kernel, the average launch duration from the kernel trace and the HBM
+bytes per launch from the PMC passes, corrected as MI355X_MICROARCH.md
+§HBM prescribes (FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
+tallies 128-byte requests at 64 bytes, so it is doubled). bench.py reports
+`roofline.traffic` from traffic.json only when its lib_md5 matches the
+libtbc.so being benchmarked.
+"""
+from __future__ import annotations
+
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def short(name: str) -> str:
+    n = name.split("(")[0].replace("void ", "")
+    return n.split("::")[-1].split("<")[0]
+
+
+def find(root: str, pattern: str) -> str:
+    hits = glob.glob(os.path.join(root, "**", pattern), recursive=True)
+    if not hits:
+        raise SystemExit(f"no {pattern} under {root}")
+    return hits[0]
+
+
+def counters(root: str, counter: str) -> dict:
+    per = collections.defaultdict(list)
+    for row in csv.DictReader(open(find(root, "*counter_collection.csv"))):
+        if row["Counter_Name"] == counter:
+            per[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}
+
+
+def main() -> None:
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    stats = find(os.path.join(src, "trace"), "*kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+    avg_ns = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
+    fetch = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
+    write = counters(os.path.join(src, "write"), "WRITE_SIZE")
+    md5 = open(os.path.join(src, "lib.md5")).read().split()[0]
+    out = {"lib_md5": md5, "note": "bytes per launch; fetch = 2 x FETCH_SIZE KiB (gfx950 correction), "
+                                   "write = WRITE_SIZE KiB", "kernels": {}}
+    for k in sorted(avg_ns):
+        f = fetch.get(k, 0.0) * 1024 * 2
+        w = write.get(k, 0.0) * 1024
+        out["kernels"][k] = {"avg_ns": avg_ns[k], "fetch_bytes": round(f), "write_bytes": round(w),
+                             "traffic_bytes": round(f + w),
+                             "traffic_gbs": round((f + w) / avg_ns[k], 1) if avg_ns[k] else None}
+    json.dump(out, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
