@@ -244,8 +244,8 @@ def main() -> None:
     W_index = tables * index_size
     alg_bytes = {
         "merge_partition": (args.jobs * 2400) * 2 * 21 * 32,
-        "merge": R + out_values * spec.value_size,  # read every input value once, write every survivor
-        "data_blocks": W_data + data_blocks * 256,  # read bodies, write headers
+        "merge": R,  # read every input value once (keys decide; 2 mask bits per position written)
+        "data_blocks": out_values * spec.value_size + W_data,  # read every survivor once, write the blocks
         "index_blocks": W_index + data_blocks * 64,
     }
     kt_us = per_step[dominant]

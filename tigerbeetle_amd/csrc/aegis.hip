@@ -17,10 +17,11 @@
 //   * message words are prefetched a 1 KiB group (32 updates) ahead.
 //
 // Block finishing (Table.Builder.data_block_finish / index_block_finish,
-// src/lsm/table.zig:306-457) is fused here: body assembly (the values are
-// gathered through the merge's route and stored as they are absorbed, so the
-// copy costs no pass of its own), body checksum, header fields, header
-// checksum, index-block body, TableInfo.
+// src/lsm/table.zig:306-457) is fused here: body assembly (producer waves
+// copy the surviving values into the output block from the merge's masks
+// while the chain waves of the same workgroup checksum what is already in
+// place), body checksum, header fields, header checksum, index-block body,
+// TableInfo.
 #include <hip/hip_runtime.h>
 
 #include "tbc_internal.h"
@@ -224,6 +225,7 @@ struct GlobalMsg {
         return v;
     }
     __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
+    __device__ __forceinline__ void ready(uint32_t) const {}
 };
 
 struct LdsMsg {
@@ -243,32 +245,41 @@ struct LdsMsg {
         return v;
     }
     __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
+    __device__ __forceinline__ void ready(uint32_t) const {}
 };
 
-// A data block body that does not exist yet: value i of the block is wherever
-// route[i] points (an input value chosen by the merge), and every absorbed
-// dword is also stored into the output block — the copy rides on the
-// checksum chain, whose LDS latency leaves the wave's memory pipe idle.
-// len is a whole number of values (16 B or more each), so no dword is partial.
-struct RoutedMsg {
+// A data block body that the producer waves of the same workgroup are still
+// assembling in the output block: before the chain loads the words of a
+// group it waits until the producer's LDS progress word covers them. The
+// producer publishes progress in whole 256-byte units (or the full length),
+// after its stores have completed, so every cache line the chain pulls into
+// L1 is already final.
+struct BodyMsg {
     using Addr = const uint8_t *;
-    const uint64_t *route;
-    uint8_t *dst;
+    const uint8_t *base;
     uint32_t len;
     uint32_t max_off;
-    uint32_t vs_shift, vs_mask;
-    bool store;
-    __device__ __forceinline__ RoutedMsg(const uint64_t *r, uint8_t *d, uint32_t l, uint32_t vs, bool st)
-        : route(r), dst(d), len(l), max_off(l >= 4 ? l - 4 : 0), vs_shift(__builtin_ctz(vs)), vs_mask(vs - 1),
-          store(st) {}
-    __device__ __forceinline__ Addr addr(uint32_t off) const {
-        off = off < max_off ? off : max_off;
-        return (const uint8_t *)gld<uint64_t>(route + (off >> vs_shift)) + (off & vs_mask);
-    }
+    const uint32_t *prog; // LDS
+    uint32_t *err;        // JobResultDev.invariant: set if the producer never delivers
+    __device__ __forceinline__ BodyMsg(const uint8_t *b, uint32_t l, const uint32_t *p, uint32_t *e)
+        : base(b), len(l), max_off(l >= 4 ? l - 4 : 0), prog(p), err(e) {}
+    __device__ __forceinline__ Addr addr(uint32_t off) const { return base + (off < max_off ? off : max_off); }
     __device__ __forceinline__ uint32_t word(Addr a) const { return gld<uint32_t>(a); }
-    __device__ __forceinline__ uint32_t exact(uint32_t off) const { return off < len ? word(addr(off)) : 0u; }
-    __device__ __forceinline__ void sink(uint32_t off, uint32_t w) const {
-        if (store && off < len) gst<uint32_t>(dst + off, w);
+    __device__ __forceinline__ uint32_t exact(uint32_t off) const { return off < len ? gld<uint32_t>(base + off) : 0u; }
+    __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
+    __device__ __forceinline__ void ready(uint32_t upto) const {
+        const uint32_t need = upto < len ? upto : len;
+        for (uint32_t spins = 0;; spins++) {
+            const uint32_t have = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const bool late = have < need;
+            if (!__any(late)) break;
+            if (spins > (1u << 22)) { // bounded: report instead of hanging
+                if (late) gst<uint32_t>(err, 0xdeadu);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 };
 
@@ -352,8 +363,7 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     // messages, in groups of kGroup windows (64 updates, 2 KiB per message). At
     // the top of each group the words of the next group are loaded (a full
     // group ahead of use, so the compiler's loop back-edge vmcnt(0) finds
-    // them landed) and the addresses of the group after resolved (for a
-    // routed message that is a load too).
+    // them landed) and the addresses of the group after resolved.
     constexpr uint32_t kGroup = 8; // windows per group: 64 updates (~3.8 us) hide two dependent gathers
     auto fast = [&](uint32_t w0, uint32_t w1) {
         if (w0 >= w1) return;
@@ -367,6 +377,7 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
             }
         };
         uint32_t cur[2 * kGroup];
+        msg.ready(256 * (w0 + kGroup));
         resolve(256 * w0);
 #pragma unroll
         for (int i = 0; i < 2 * kGroup; i++) cur[i] = msg.word(ad[i]);
@@ -374,6 +385,7 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
         for (uint32_t grp = 0; grp < groups; grp++) {
             const uint32_t wg = w0 + kGroup * grp;
             uint32_t nxt[2 * kGroup];
+            msg.ready(256 * (wg + 2 * kGroup));
 #pragma unroll
             for (int i = 0; i < 2 * kGroup; i++) nxt[i] = msg.word(ad[i]);
             resolve(256 * (wg + 2 * kGroup));
@@ -412,6 +424,7 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     auto slow = [&](uint32_t w0, uint32_t w1) {
         for (uint32_t w = w0; w < w1; w++) {
             const uint32_t o_lo = 256 * w + off_lo, o_hi = 256 * w + off_hi;
+            msg.ready(256 * (w + 1));
             const uint32_t wl = msg.exact(o_lo), wh = msg.exact(o_hi);
             if (o_lo < len) msg.sink(o_lo, wl);
             if (o_hi < len) msg.sink(o_hi, wh);
@@ -536,48 +549,176 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
     return tag;
 }
 
-// Data blocks: data_block_finish (table.zig:306-384) for every output data
-// block. Blocks are numbered batch-wide by their upper bound (job base + k);
-// wave w takes blocks 2w and 2w+1, one per 32-lane group, whatever their
-// lengths (aegis_mac32 takes two lengths), so a batch needs only
-// ceil(blocks / 2) waves -- one per SIMD for config 2's 2,044 blocks. A group
-// whose block does not exist (dedup left fewer blocks than the bound)
-// mirrors its partner's block without writing, so all its loads stay valid.
-__global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
-                                                      const JobResultDev *res) {
-    __shared__ uint32_t sT[kTableDwords];
-    __shared__ uint32_t sHdr[16][2][64];
-    load_tables(sT);
-    __syncthreads();
-    const uint32_t wave_in_block = threadIdx.x >> 6;
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wave_in_block;
+// Producer: assemble the body of data block k of job j (output values
+// [k*vcm, k*vcm + cnt)) from the merge's masks, 64 merged positions per step.
+// Lane l owns merged position 64w + l of tile t: its side (from-A bit), its
+// input index (cursor + side bits below it), and, if it survives, its output
+// position (cursor + survivor bits below it); survivors of this block copy
+// their value into place with 16-byte loads and stores. Progress (body bytes
+// final and visible) goes to *prog in 256-byte units, after the stores have
+// completed, for the chain waves of the workgroup (BodyMsg::ready).
+struct SegCursor {
+    const uint64_t *ptrs;
+    const uint32_t *pre;
+    uint32_t nseg, seg, lo, hi;
+    uint64_t base;
+    __device__ __forceinline__ void load() {
+        lo = gld<uint32_t>(pre + seg);
+        hi = gld<uint32_t>(pre + seg + 1);
+        base = gld<uint64_t>(ptrs + seg);
+    }
+    __device__ __forceinline__ void init(const Stream &s, uint32_t seg0) {
+        ptrs = s.seg_ptr;
+        pre = s.seg_pre;
+        nseg = s.nseg;
+        seg = nseg ? (seg0 < nseg ? seg0 : nseg - 1) : 0;
+        if (nseg) load();
+        else lo = hi = 0, base = 0;
+    }
+    // Move forward to the segment holding element `idx` (wave-uniform).
+    __device__ __forceinline__ void advance(uint32_t idx) {
+        while (seg + 1 < nseg && idx >= hi) {
+            seg++;
+            load();
+        }
+    }
+    // Address of element idx >= lo (per lane; usually inside the cursor's segment).
+    __device__ __forceinline__ const uint8_t *elem(uint32_t idx, uint32_t vs) const {
+        uint32_t s = seg, l = lo, h = hi;
+        uint64_t b = base;
+        while (idx >= h && s + 1 < nseg) {
+            s++;
+            l = h;
+            h = gld<uint32_t>(pre + s + 1);
+            b = gld<uint64_t>(ptrs + s);
+        }
+        return (const uint8_t *)(uintptr_t)b + (size_t)(idx - l) * vs;
+    }
+};
+
+__device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint32_t cnt, const uint64_t *status,
+                                             const uint64_t *masks, const uint32_t *block_tile,
+                                             const SplitDesc *splits, uint8_t *body, uint32_t *prog,
+                                             uint32_t *err) {
     const uint32_t lane = threadIdx.x & 63;
-    const bool upper = lane >= 32;
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t vs = j.value_size;
+    const uint32_t n = j.a.n + j.b.n;
+    const uint64_t out_begin = (uint64_t)k * j.vcm, out_end = out_begin + cnt;
+    const uint32_t len = cnt * vs;
+    uint32_t t = __builtin_amdgcn_readfirstlane(gld<uint32_t>(block_tile + j.dblock_base + k));
+    const SplitDesc sp = splits[j.split_base + t];
+    uint64_t out_cur = gld<uint64_t>(status + j.tile_base + t) >> 32;
+    uint32_t a_cur = sp.i, b_cur = t * kMergeTile - sp.i;
+    SegCursor ca, cb;
+    ca.init(j.a, sp.seg_a);
+    cb.init(j.b, sp.seg_b);
+    uint32_t w = 0, since = 0;
+    while (out_cur < out_end) {
+        const uint64_t *m = masks + (size_t)(j.tile_base + t) * (2 * (kMergeTile / 64));
+        const uint64_t sm = gld<uint64_t>(m + w), am = gld<uint64_t>(m + kMergeTile / 64 + w);
+        const uint32_t pos0 = t * kMergeTile + 64 * w;
+        const uint64_t valid = n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1);
+        const uint32_t ns = __builtin_popcountll(sm);
+        if (out_cur + ns > out_begin) {
+            ca.advance(a_cur);
+            cb.advance(b_cur);
+            const bool from_a = (am >> lane) & 1;
+            const uint64_t o = out_cur + __builtin_popcountll(sm & lt);
+            if (((sm >> lane) & 1) && o >= out_begin && o < out_end) {
+                const uint8_t *src = from_a ? ca.elem(a_cur + __builtin_popcountll(am & lt), vs)
+                                            : cb.elem(b_cur + __builtin_popcountll(valid & ~am & lt), vs);
+                uint8_t *dst = body + (size_t)(o - out_begin) * vs;
+                for (uint32_t q = 0; q < vs; q += 16) gst<u32x4>(dst + q, gld<u32x4>(src + q));
+            }
+        }
+        a_cur += __builtin_popcountll(am);
+        b_cur += __builtin_popcountll(valid & ~am);
+        out_cur += ns;
+        if (++w == kMergeTile / 64) {
+            w = 0;
+            if (++t >= j.tile_count && out_cur < out_end) { // masks disagree with the scan: report, release
+                if (lane == 0) gst<uint32_t>(err, 0xbad0u);
+                out_cur = out_end;
+            }
+        }
+        // Publish every 4 steps (and at the end): stores complete, then progress.
+        if (++since == 4 || out_cur >= out_end) {
+            since = 0;
+            const uint64_t done = (out_cur < out_end ? out_cur : out_end);
+            const uint32_t bytes = done > out_begin ? (uint32_t)(done - out_begin) * vs : 0u;
+            const uint32_t pub = bytes >= len ? len : (bytes & ~255u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(prog, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// Data blocks: data_block_finish (table.zig:306-384) for every output data
+// block. Blocks are numbered batch-wide by their upper bound (job base + k).
+// A workgroup holds C chain waves and 2C producer waves: chain wave c takes
+// blocks 2w and 2w+1 (w = blockIdx * C + c), one per 32-lane group, whatever
+// their lengths (aegis_mac32 takes two lengths), and producer 2c + h
+// assembles block 2w + h in the output block while the chain absorbs it.
+// Config 2's 2,016 blocks need 1,008 chain waves: one per SIMD. A group
+// whose block does not exist (dedup left fewer blocks than the bound) mirrors
+// its partner's block without writing, so all its loads stay valid.
+constexpr uint32_t kMaxChainWaves = 5;
+
+__global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
+                                                      const JobResultDev *res, const uint64_t *status,
+                                                      const uint64_t *masks, const uint32_t *block_tile,
+                                                      const SplitDesc *splits, uint32_t chain_waves) {
+    __shared__ uint32_t sT[kTableDwords];
+    __shared__ uint32_t sHdr[kMaxChainWaves][2][64];
+    __shared__ uint32_t sProg[2 * kMaxChainWaves];
+    load_tables(sT);
+    if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t C = chain_waves;
+    const uint32_t wave_in_block = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
     auto locate = [&](uint32_t m, int &ji_, uint32_t &k_) {
         ji_ = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
         k_ = m - jobs[ji_].dblock_base;
         return m < total && k_ < res[jobs[ji_].job_index].data_block_count;
     };
-    const uint32_t mine = 2 * wave + (upper ? 1u : 0u);
+    auto block_count = [&](const JobDesc &j, uint32_t k_) {
+        const uint64_t n_out = res[j.job_index].value_count;
+        const uint64_t first = (uint64_t)k_ * j.vcm;
+        return (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
+    };
     int ji;
     uint32_t k;
+    if (wave_in_block >= C) { // producer
+        const uint32_t p = wave_in_block - C;
+        const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
+        if (!locate(mine, ji, k)) return;
+        const JobDesc &j = jobs[ji];
+        uint8_t *blk = j.out_blocks + (size_t)data_block_slot(k, j.dbcm) * j.block_size;
+        produce_body(j, k, block_count(j, k), status, masks, block_tile, splits, blk + kHeaderSize, &sProg[p],
+                     const_cast<uint32_t *>(&res[j.job_index].invariant));
+        return;
+    }
+    const uint32_t wave = blockIdx.x * C + wave_in_block;
+    const bool upper = lane >= 32;
+    const uint32_t mine = 2 * wave + (upper ? 1u : 0u);
     const bool live = locate(mine, ji, k);
     const bool live_lo = __builtin_amdgcn_readlane((int)live, 0) != 0;
     const bool live_hi = __builtin_amdgcn_readlane((int)live, 32) != 0;
     if (!live_lo && !live_hi) return;
     if (!live) locate(mine ^ 1u, ji, k); // mirror the partner's block, write nothing
     const bool writer = live;
+    const uint32_t src_half = (upper ? 1u : 0u) ^ (live ? 0u : 1u);
     const JobDesc &j = jobs[ji];
-    const uint64_t n_out = res[j.job_index].value_count;
-    const uint64_t first = (uint64_t)k * j.vcm;
-    const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
+    const uint32_t cnt = block_count(j, k);
     const uint32_t size = kHeaderSize + cnt * j.value_size;
     const uint32_t slot = data_block_slot(k, j.dbcm);
     uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
 
-    // The body is assembled here: values gathered through the merge's route
-    // and stored into the block as they are absorbed.
-    RoutedMsg body(j.route + first, blk + kHeaderSize, cnt * j.value_size, j.value_size, writer);
+    BodyMsg body(blk + kHeaderSize, cnt * j.value_size, &sProg[2 * wave_in_block + src_half],
+                 const_cast<uint32_t *>(&res[j.job_index].invariant));
     const uint32_t body_tag = aegis_mac32(sT, body);
 
     HeaderFields h;
@@ -724,14 +865,17 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
 }
 
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
-                  JobResultDev *d_results, uint8_t *d_infos, void *stream, void (*mark)(void *, const char *),
-                  void *mark_ctx) {
+                  JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
+                  const uint32_t *d_block_tile, const SplitDesc *d_splits, void *stream,
+                  void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     if (total_dblocks) {
-        const uint32_t waves = (total_dblocks + 1) / 2;
-        const uint32_t wpb = waves_per_block(waves);
-        hipLaunchKernelGGL(k_data_blocks, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, s, d_jobs, njobs,
-                           total_dblocks, (const JobResultDev *)d_results);
+        const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
+        uint32_t c = waves_per_block(waves);
+        c = c > kMaxChainWaves ? kMaxChainWaves : c;
+        hipLaunchKernelGGL(k_data_blocks, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
+                           total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
+                           c);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "data_blocks");

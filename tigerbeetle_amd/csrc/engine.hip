@@ -84,25 +84,25 @@ struct tbc_engine {
     hipStream_t stream = nullptr;
     Arena dev, host;
     std::vector<hipEvent_t> event_pool;
-    // Route buffer (8 bytes per input value of a batch). Batches run in stream
-    // order, so one buffer serves them all; it only grows (after a stream
-    // drain), which a steady-state caller sees once.
-    uint64_t *route = nullptr;
-    uint64_t route_words = 0;
+    // Merge mask buffer (2 bits per merged position of a batch: 512 bytes
+    // per tile). Batches run in stream order, so one buffer serves them all;
+    // it only grows (after a stream drain), which a steady-state caller sees once.
+    uint64_t *masks = nullptr;
+    uint64_t mask_words = 0;
 };
 
-static bool ensure_route(tbc_engine *e, uint64_t words) {
-    if (words <= e->route_words) return true;
+static bool ensure_masks(tbc_engine *e, uint64_t words) {
+    if (words <= e->mask_words) return true;
     if (hipStreamSynchronize(e->stream) != hipSuccess) return false;
-    if (e->route) hipFree(e->route);
-    e->route = nullptr;
-    e->route_words = 0;
-    const uint64_t want = align_up(words, 1ull << 20);
-    if (hipMalloc((void **)&e->route, want * 8) != hipSuccess) {
-        e->route = nullptr;
+    if (e->masks) hipFree(e->masks);
+    e->masks = nullptr;
+    e->mask_words = 0;
+    const uint64_t want = align_up(words, 1ull << 16);
+    if (hipMalloc((void **)&e->masks, want * 8) != hipSuccess) {
+        e->masks = nullptr;
         return false;
     }
-    e->route_words = want;
+    e->mask_words = want;
     return true;
 }
 
@@ -176,7 +176,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
     hipHostFree(e->host.base);
     hipFree(e->dev.base);
-    if (e->route) hipFree(e->route);
+    if (e->masks) hipFree(e->masks);
     hipStreamDestroy(e->stream);
     delete e;
 }
@@ -377,20 +377,17 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     // Group jobs by key kind (one kernel instantiation per kind) and assign
     // batch-wide bases in that order.
     std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hj[x].key_kind < hj[y].key_kind; });
-    uint64_t route_words = 0;
-    for (uint32_t i = 0; i < count; i++) route_words += (uint64_t)hj[i].a.n + hj[i].b.n;
-    if (!ensure_route(e, route_words)) {
+    uint64_t all_tiles = 0;
+    for (uint32_t i = 0; i < count; i++) all_tiles += hj[i].tile_count;
+    if (!ensure_masks(e, all_tiles * (2 * kMergeTile / 64))) {
         delete b;
         return TBC_ERR_OUT_OF_MEMORY;
     }
     std::vector<JobDesc> sj(count);
     uint32_t tiles = 0, splits = 0, dblocks = 0, tables = 0, infos = 0;
-    uint64_t route_at = 0;
     for (uint32_t k = 0; k < count; k++) {
         sj[k] = hj[order[k]];
         JobDesc &d = sj[k];
-        d.route = e->route + route_at;
-        route_at += (uint64_t)d.a.n + d.b.n;
         d.tile_base = tiles;
         d.split_base = splits;
         d.dblock_base = dblocks;
@@ -411,7 +408,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     const uint64_t sz_order = align_up(sizeof(TileRef) * (uint64_t)tiles, 256);
     const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order;
     const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
-    const uint64_t sz_tiles = align_up(8ull * tiles + 4ull * count + 8, 256); // status granules + tile counters
+    const uint64_t sz_tiles = align_up(8ull * tiles + 4ull * dblocks + 8, 256); // tile status + block_tile
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
     b->dev_top = e->dev.top;
@@ -429,7 +426,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     uint8_t *d_in = dbase;
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
     uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
-    uint32_t *d_counters = (uint32_t *)(d_status + tiles);
+    uint32_t *d_block_tile = (uint32_t *)(d_status + tiles);
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
     b->h_results = (JobResultDev *)(hbase + sz_in);
@@ -507,14 +504,15 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
 
     hipStream_t s = e->stream;
     bool ok = hipMemcpyAsync(d_in, h_in, sz_in, hipMemcpyHostToDevice, s) == hipSuccess;
-    // Status granules, tile counters and results must start zeroed (contiguous).
+    // Tile status, block tiles and results start zeroed (contiguous).
     ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");
     if (ok && count)
-        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, d_counters, d_order,
-                          d_res, s, mark_cb, b) == 0;
+        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile,
+                          d_order, d_res, s, mark_cb, b) == 0;
     if (ok && count)
-        ok = launch_blocks((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, s, mark_cb, b) == 0;
+        ok = launch_blocks((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status, e->masks,
+                           d_block_tile, d_splits, s, mark_cb, b) == 0;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     if (!ok) {

@@ -16,17 +16,17 @@
 //   B[j] is written       iff A has no dedup survivor with the same key
 //                          (B tombstones are never dropped, :775-779).
 //
-// Kernels: merge-path split per tile boundary -> per tile: survivor flags,
-// block scan, decoupled look-back for the job-global output offset (the last
-// tile also yields the data-block / table counts) -> the route (one source
-// pointer per output value, in output order). k_data_blocks then gathers the
-// values through the route into the output blocks as it checksums them.
+// Kernels: merge-path split per tile boundary -> per tile: survivor and side
+// bit masks plus the survivor count (tiles independent) -> per job: scan of
+// the counts into tile output offsets and the output shape. k_data_blocks
+// then assembles each output block from the masks (producer waves) while its
+// AEGIS chain checksums it (aegis.hip).
 #include <hip/hip_runtime.h>
 
 #include "tbc_internal.h"
 
 #ifndef TBC_ABLATE
-#define TBC_ABLATE 0 // timing experiments only: 2 = no look-back wait, 4 = no key loads
+#define TBC_ABLATE 0 // timing experiments only: 4 = no key loads
 #endif
 
 namespace tbc {
@@ -137,46 +137,32 @@ __global__ __launch_bounds__(256) void k_partition(const JobDesc *jobs, int njob
 }
 
 // --------------------------------------------------------------------------
-// One pass per tile (merged positions [d0, d1)): load keys, decide
-// survivors, exclusive-scan them, learn the tile's global output offset by
-// decoupled look-back over its job's earlier tiles, and copy the survivors
-// straight into their output data-block slots.
-//
-// Tiles take ids from an atomic counter in start order, so a tile only ever
-// waits on tiles that are already running (no deadlock). Each tile publishes
-// one 8-byte status granule {flag:2, count:62}: 1 = own count, 2 = inclusive
-// prefix (single aligned 8-byte agent-scope store: untorn, no payload behind
-// it; MI355X guide §Workgroup dispatch, hand-off granules).
+// One pass per tile (merged positions [d0, d1)): load keys, decide each
+// position's side (A or B) and whether it survives, and publish them as two
+// bit masks per 64 positions plus the tile's survivor count. Tiles are
+// independent (no look-back, any order); k_tile_scan turns the counts into
+// output offsets, and the producer waves of k_data_blocks walk the masks to
+// assemble each output block's body.
 // --------------------------------------------------------------------------
 constexpr uint32_t kSegWindow = 16;
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kCountMask = (1ull << 62) - 1;
+constexpr uint32_t kMaskWords = kMergeTile / 64; // per mask kind per tile
 
 template <int KL> struct TileShared {
     uint64_t key[KL][kMergeTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
-    const uint8_t *ptr[kMergeTile + 3];
     uint8_t tomb[kMergeTile + 4];
-    uint32_t out[kMergeTile];  // output order -> entry
     uint32_t seg_pre[2][kSegWindow + 1];
     uint64_t seg_ptr[2][kSegWindow];
     uint32_t wave_sums[kMergeThreads / 64];
-    uint32_t tile, count;
-    uint64_t offset;
 };
 
 template <int KIND>
 __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
-                                                              uint32_t order_offset, uint32_t *tile_counter,
-                                                              const SplitDesc *splits, uint64_t *status,
-                                                              JobResultDev *res) {
+                                                              uint32_t order_offset, const SplitDesc *splits,
+                                                              uint64_t *status, uint64_t *masks) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    // Tiles start in counter order, so a tile waits only on running tiles.
-    // The order table interleaves the batch's jobs, which keeps each job's
-    // look-back chain short however many tiles are in flight.
-    if (tid == 0) sh.tile = order_offset + atomicAdd(tile_counter, 1u);
-    __syncthreads();
-    const TileRef ref = order[sh.tile];
+    const TileRef ref = order[order_offset + blockIdx.x];
     const JobDesc &j = jobs[ref.job];
     const uint32_t t = ref.tile;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
@@ -245,7 +231,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         }
 #pragma unroll
         for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
-        sh.ptr[e] = ptrs[r];
         if (e < ea) sh.tomb[e] = (uint8_t)tb;
     }
     __syncthreads();
@@ -280,6 +265,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     // merge-path search in LDS for its start, then a sequential merge (A
     // first on equal keys) applying the survivor rules to each element.
     constexpr uint32_t kPer = kMergeTile / kMergeThreads;
+    static_assert(64 % kPer == 0 && kPer <= 32, "a mask word covers whole threads");
     const uint32_t total_pos = na + nb;
     const uint32_t d = kPer * tid < total_pos ? kPer * tid : total_pos;
     uint32_t a, b;
@@ -293,12 +279,9 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         a = lo;
         b = d - lo;
     }
-    uint32_t f[kPer], ent[kPer];
-    uint32_t sum = 0;
+    uint32_t sbits = 0, abits = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; k++) {
-        f[k] = 0;
-        ent[k] = 0;
         if (d + k >= total_pos) continue;
         const bool take_a = a < na && (b >= nb || key_le(entry_key(1 + a), entry_key(ea + b)));
         bool surv;
@@ -315,7 +298,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
             const bool b_valid = b < nb || j1 < nb_all;
             const bool eq_b = b_valid && key_eq(entry_key(ea + b), ka);
             surv = dedup && !(drop && sh.tomb[e]) && !(secondary && eq_b);
-            ent[k] = e;
+            abits |= 1u << k;
             a++;
         } else {
             // B element jb = j0 + b at entry ea + b; the previous A (global
@@ -325,114 +308,92 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
             bool a_exists = (i0 + a) >= 1 && key_eq(entry_key(a), kb);
             if (a_exists && immutable && secondary) a_exists = (run_len(i0 + a - 1) & 1) != 0;
             surv = !a_exists;
-            ent[k] = e;
             b++;
         }
-        f[k] = surv ? 1u : 0u;
-        sum += f[k];
+        sbits |= (surv ? 1u : 0u) << k;
     }
-    // Block exclusive scan of the survivor counts (threads in merged order).
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
+    // Mask word q (positions 64q..64q+63) is the OR of the bit groups of
+    // threads q*64/kPer .. (q+1)*64/kPer - 1, all in one wave.
+    constexpr uint32_t kThreadsPerWord = 64 / kPer;
+    const uint32_t sh_bits = kPer * (tid % kThreadsPerWord);
+    uint64_t sw = (uint64_t)sbits << sh_bits, aw = (uint64_t)abits << sh_bits;
+    for (uint32_t o = 1; o < kThreadsPerWord; o <<= 1) {
+        sw |= __shfl_xor(sw, o, 64);
+        aw |= __shfl_xor(aw, o, 64);
     }
-    if (lane == 63) sh.wave_sums[tid >> 6] = incl;
+    uint64_t *m = masks + (size_t)(j.tile_base + t) * (2 * kMaskWords);
+    if (tid % kThreadsPerWord == 0) {
+        gst<uint64_t>(m + tid / kThreadsPerWord, sw);
+        gst<uint64_t>(m + kMaskWords + tid / kThreadsPerWord, aw);
+    }
+    uint32_t sum = __builtin_popcount(sbits);
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) sh.wave_sums[tid >> 6] = sum;
     __syncthreads();
-    uint32_t wave_off = 0;
-    for (uint32_t w = 0; w < (tid >> 6); w++) wave_off += sh.wave_sums[w];
-    {
-        uint32_t o = wave_off + incl - sum;
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; k++)
-            if (f[k]) sh.out[o++] = ent[k];
+    if (tid == 0) {
+        uint32_t cnt = 0;
+        for (uint32_t w = 0; w < kMergeThreads / 64; w++) cnt += sh.wave_sums[w];
+        gst<uint64_t>(status + j.tile_base + t, (uint64_t)cnt);
     }
-    if (tid == kMergeThreads - 1) sh.count = wave_off + incl;
+}
+
+// Per job (one workgroup): exclusive scan of the tile survivor counts into
+// status[t] = count | offset << 32, the output shape (write_blocks,
+// compaction.zig:806-850: full data blocks except the last, full tables
+// except the last), and for every data block k the tile holding its first
+// value (block_tile[dblock_base + k]).
+constexpr uint32_t kScanThreads = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void k_tile_scan(const JobDesc *jobs, uint64_t *status,
+                                                           uint32_t *block_tile, JobResultDev *res) {
+    __shared__ uint32_t wsum[kScanThreads / 64];
+    __shared__ uint64_t carry;
+    const JobDesc &j = jobs[blockIdx.x];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    uint64_t *st = status + j.tile_base;
+    if (tid == 0) carry = 0;
     __syncthreads();
-
-    // Source pointers of this tile's survivors, in output order; read from
-    // LDS before the look-back so only the stores wait for the tile's offset.
-    const uint32_t cnt = sh.count;
-    constexpr uint32_t kRoutePer = kMergeTile / kMergeThreads;
-    uint64_t src[kRoutePer];
-#pragma unroll
-    for (uint32_t u = 0; u < kRoutePer; u++) {
-        const uint32_t o = tid + u * kMergeThreads;
-        src[u] = o < cnt ? (uint64_t)(uintptr_t)sh.ptr[sh.out[o]] : 0;
-    }
-
-    if (tid >= kMergeThreads - 64) {
-        // Decoupled look-back by the last wave: each probe reads the status
-        // granules of 64 predecessors at once (closest first), sums their
-        // counts up to the closest inclusive prefix, and moves 64 further
-        // back only if all 64 were aggregates.
-        uint64_t *st = status + j.tile_base;
-        uint64_t prefix = 0;
-        if (t == 0 || (TBC_ABLATE & 2)) {
-            if (lane == 0) __hip_atomic_store(st + t, kFlagIncl | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(st + t, kFlagAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t base = (int64_t)t - 1;
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t k = base - (int64_t)lane;
-                const uint64_t s = k >= 0 ? __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                          : kFlagIncl;
-                const uint64_t flag = s & ~kCountMask;
-                const uint64_t incl_mask = __ballot(flag == kFlagIncl);
-                const uint64_t wait_mask = __ballot(flag == 0);
-                const uint32_t first = incl_mask ? (uint32_t)__builtin_ctzll(incl_mask) : 64u;
-                const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-                if (wait_mask & need) {
-                    if (++spins > (1u << 24)) { // bounded: report instead of hanging
-                        if (lane == 0) res[j.job_index].invariant = 0xdead;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                uint64_t c = lane <= first ? (s & kCountMask) : 0;
-                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                prefix += c;
-                if (first < 64) break;
-                base -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(st + t, kFlagIncl | (prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t base = 0; base < j.tile_count; base += kScanThreads) {
+        const uint32_t t = base + tid;
+        const uint32_t c = t < j.tile_count ? (uint32_t)gld<uint64_t>(st + t) : 0u;
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
         }
-        if (lane == 0) {
-            sh.offset = prefix;
-            if (t + 1 == j.tile_count) {
-                // Output shape (write_blocks, compaction.zig:806-850): full data
-                // blocks except the last, full tables except the last.
-                const uint64_t total = prefix + cnt;
-                const uint32_t db = (uint32_t)((total + j.vcm - 1) / j.vcm);
-                const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
-                JobResultDev &r = res[j.job_index];
-                r.value_count = total;
-                r.data_block_count = db;
-                r.table_count = tables;
-                r.block_count = db + tables;
+        if (lane == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (uint32_t w = 0; w < (tid >> 6); w++) woff += wsum[w];
+        const uint64_t off = carry + woff + incl - c;
+        if (t < j.tile_count) {
+            gst<uint64_t>(st + t, (uint64_t)c | (off << 32));
+            // Data blocks whose first value lies in this tile.
+            if (c) {
+                uint64_t k = (off + j.vcm - 1) / j.vcm;
+                for (; k * j.vcm < off + c; k++) gst<uint32_t>(block_tile + j.dblock_base + k, t);
             }
         }
+        __syncthreads();
+        if (tid == kScanThreads - 1) carry = off + c;
+        __syncthreads();
     }
-    __syncthreads();
-
-    // Route: output position g of the job -> pointer to the surviving value.
-    // The value bytes are moved by k_data_blocks, which gathers them through
-    // the route while its (latency-bound) AEGIS chain runs (aegis.hip, RoutedMsg).
-    uint64_t *route = j.route + sh.offset;
-#pragma unroll
-    for (uint32_t u = 0; u < kRoutePer; u++) {
-        const uint32_t o = tid + u * kMergeThreads;
-        if (o < cnt) gst<uint64_t>(route + o, src[u]);
+    if (tid == 0) {
+        const uint64_t total = carry;
+        const uint32_t db = (uint32_t)((total + j.vcm - 1) / j.vcm);
+        const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
+        JobResultDev &r = res[j.job_index];
+        r.value_count = total;
+        r.data_block_count = db;
+        r.table_count = tables;
+        r.block_count = db + tables;
     }
 }
 
 template <int KIND>
 static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
-                       SplitDesc *d_splits, uint64_t *d_status, uint32_t *d_counters, const TileRef *d_order,
-                       JobResultDev *d_res, hipStream_t s) {
+                       SplitDesc *d_splits, uint64_t *d_status, uint64_t *d_masks, const TileRef *d_order,
+                       hipStream_t s) {
     const JobDesc &f = h_jobs[first];
     const JobDesc &l = h_jobs[first + count - 1];
     const uint32_t split_off = f.split_base;
@@ -444,15 +405,16 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
                            split_off, nsplits, d_splits);
     else if (ntiles)
         hipLaunchKernelGGL(k_merge_tile<KIND>, dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,
-                           d_counters + first, (const SplitDesc *)d_splits, d_status, d_res);
+                           (const SplitDesc *)d_splits, d_status, d_masks);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // Jobs must be grouped by key kind (contiguous runs) by the caller. d_status
-// (one u64 per tile) and d_counters (one u32 per job) must be zero.
+// holds one u64 per tile, d_masks 2 * kMergeTile / 64 u64 per tile,
+// d_block_tile one u32 per data block (upper bound); results start zeroed.
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
-                 uint64_t *d_status, uint32_t *d_counters, const TileRef *d_order, JobResultDev *d_results,
-                 void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
+                 uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
+                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     auto for_each_kind = [&](auto fn) {
         int first = 0;
@@ -467,16 +429,19 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     auto phase = [&](int ph) {
         return for_each_kind([&](uint32_t kind, int first, int count) {
             switch (kind) {
-            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
-            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
-            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
-            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_counters, d_order, d_results, s);
+            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
+            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
+            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
+            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
             }
         });
     };
     if (phase(0)) return -1;
     if (mark) mark(mark_ctx, "merge_partition");
     if (phase(1)) return -1;
+    hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
+                       d_results);
+    if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge");
     return 0;
 }

@@ -6,11 +6,12 @@
 //   u32 seg_pre[...]        per-stream segment prefix counts (nseg + 1 each)
 //   u64 addresses[...]      acquire-order block addresses per job
 //   SplitDesc splits[...]   merge-path A-splits at every tile boundary (tiles + 1 per job)
-//   u64 status[...]         per-tile look-back granules; u32 tile counters per job
+//   u64 status[...]         per tile: survivor count | output offset << 32
+//   u32 block_tile[...]     per data block (upper bound): tile of its first value
 //   JobResultDev[count]     device results (copied to pinned host memory at the end)
 //   u8  table_infos[...]    128-byte ManifestNode.TableInfo per output table
-// plus the engine's route buffer (grown on demand, outside the arena):
-//   u64 route[...]          per job, output position -> source value pointer
+// plus the engine's mask buffer (grown on demand, outside the arena):
+//   u64 masks[tiles][2][kMergeTile / 64]   survivor bits, then from-A bits
 #pragma once
 
 #include <stdint.h>
@@ -53,7 +54,6 @@ struct JobDesc {
     uint32_t address_count;
     uint32_t pad1;
     uint8_t *out_blocks;
-    uint64_t *route; // output position -> source value pointer (a.n + b.n entries)
     // Batch bases (global grid indices).
     uint32_t tile_base, tile_count;      // merge tiles
     uint32_t split_base;                 // tile_count + 1 splits
@@ -123,10 +123,11 @@ __device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F bas
 struct hipStream_t_;
 namespace tbc {
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
-                 uint64_t *d_status, uint32_t *d_counters, const TileRef *d_order, JobResultDev *d_results,
-                 void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+                 uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
+                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
-                  JobResultDev *d_results, uint8_t *d_infos, void *stream,
+                  JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
+                  const uint32_t *d_block_tile, const SplitDesc *d_splits, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
