@@ -70,24 +70,25 @@ class Job:
     addresses: np.ndarray  # uint64, acquire order
     output: DeviceBuffer
     _keep: list = field(default_factory=list)
+    _ctype: object = field(default=None, repr=False)
 
     def ctype(self) -> abi.Compaction:
+        """The tbc_compaction descriptor, built once per Job (segment tables
+        filled with numpy, not per-element ctypes stores) and reused by every
+        submit: the descriptor is host plumbing, not part of the device step."""
+        if self._ctype is not None:
+            return self._ctype
         c = abi.Compaction()
         c.tree = self.tree.ctype()
         c.a_immutable = int(self.a_immutable)
         c.drop_tombstones = int(self.drop_tombstones)
         c.level_b = self.level_b
-        sa = (abi.Segment * max(1, len(self.segments_a)))()
-        for i, (p, n) in enumerate(self.segments_a):
-            sa[i].values, sa[i].count = p, n
-        sb = (abi.Segment * max(1, len(self.segments_b)))()
-        for i, (p, n) in enumerate(self.segments_b):
-            sb[i].values, sb[i].count = p, n
+        sa, sb = _segment_table(self.segments_a), _segment_table(self.segments_b)
         addrs = np.ascontiguousarray(self.addresses, dtype=np.uint64)
         self._keep = [sa, sb, addrs]
-        c.segments_a = ctypes.cast(sa, ctypes.POINTER(abi.Segment))
+        c.segments_a = ctypes.cast(sa.ctypes.data, ctypes.POINTER(abi.Segment))
         c.segment_count_a = len(self.segments_a)
-        c.segments_b = ctypes.cast(sb, ctypes.POINTER(abi.Segment))
+        c.segments_b = ctypes.cast(sb.ctypes.data, ctypes.POINTER(abi.Segment))
         c.segment_count_b = len(self.segments_b)
         c.cluster[0] = self.cluster & ((1 << 64) - 1)
         c.cluster[1] = self.cluster >> 64
@@ -95,7 +96,16 @@ class Job:
         c.addresses = addrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         c.address_count = len(addrs)
         c.output_blocks = self.output.ptr
+        self._ctype = c
         return c
+
+
+def _segment_table(segments: list) -> np.ndarray:
+    """tbc_segment[] as a (n, 2) uint64 array: {values, count | reserved << 32}."""
+    t = np.zeros((max(1, len(segments)), 2), dtype=np.uint64)
+    if segments:
+        t[: len(segments)] = np.asarray(segments, dtype=np.uint64).reshape(-1, 2)
+    return t
 
 
 class Batch:
@@ -148,6 +158,7 @@ class Engine:
         check(lib().tbc_engine_init(ctypes.byref(cfg), ctypes.byref(h)), "tbc_engine_init")
         self.handle = h.value
         self.block_size = block_size
+        self._prepared = None
 
     def close(self) -> None:
         if self.handle:
@@ -208,10 +219,19 @@ class Engine:
         f = lib().tbc_sort_values if sync else lib().tbc_sort_values_async
         check(f(self.handle, ctypes.byref(t), buf.ptr, count), "tbc_sort_values")
 
-    def submit(self, jobs: list) -> Batch:
+    def prepare(self, jobs: list):
+        """The tbc_compaction[] array of a job list (cached for a repeated list)."""
+        key = tuple(id(j) for j in jobs)
+        if self._prepared is not None and self._prepared[0] == key:
+            return self._prepared[1]
         arr = (abi.Compaction * max(1, len(jobs)))()
         for i, j in enumerate(jobs):
             arr[i] = j.ctype()
+        self._prepared = (key, arr, list(jobs))
+        return arr
+
+    def submit(self, jobs: list) -> Batch:
+        arr = self.prepare(jobs)
         h = ctypes.c_void_p()
         check(lib().tbc_compaction_submit(self.handle, arr, len(jobs), ctypes.byref(h)), "tbc_compaction_submit")
         return Batch(self, h.value, jobs)
