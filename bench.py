@@ -1,16 +1,19 @@
 """Benchmark: GPU LSM compaction throughput (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): transfers id-tree
-L0->L1 compaction, 28 independent jobs per GPU. Each job draws 2,358,720
-unique uniform-random u128 ids (seed 0x7B0002 + job); 262,080 of them form
-table A (one level-0 disk table), the rest are sorted and cut into 8 full
-level-B tables. IdTreeValue{id, timestamp, padding = 0}, no tombstones,
-drop_tombstones = false, usage general. 66,044,160 values x 32 B = 2.11 GB of
-input per GPU, resident in HBM (as 1 MiB grid blocks) before timing.
+Default workload (BASELINE.json configs[1]):
+transfers id-tree L0->L1 compaction, 28 independent jobs per GPU. Each job
+draws 2,358,720 unique uniform-random u128 ids (seed 0x7B0002 + job);
+262,080 of them form table A (one level-0 disk table), the rest are sorted
+and cut into 8 full level-B tables. IdTreeValue{id, timestamp, padding = 0},
+no tombstones, drop_tombstones = false, usage general. 66,044,160 values x
+32 B = 2.11 GB of input per GPU, resident in HBM (as 1 MiB grid blocks)
+before timing. `--config 3` / `--config 5` run BASELINE configs[2] / [4]
+(tigerbeetle_amd/configs.py); config 3's step includes landing each unsorted
+memtable (a D2D copy) and sorting all of them (tbc_sort_values_batch).
 
-A step = one batch of all 28 compactions (merge, data blocks with AEGIS-128L
-checksums, index blocks, TableInfos) through the C ABI. Multi-GPU: every
-rank compacts its own 28 jobs (jobs shard with no data-path collective:
+A step = one batch of all the GPU's compactions (merge, data blocks with
+AEGIS-128L checksums, index blocks, TableInfos) through the C ABI. Multi-GPU:
+every rank compacts its own jobs (jobs shard with no data-path collective:
 weak scaling); value = total input bytes of all ranks / max-over-ranks time.
 
 Prints ONE JSON line (rank 0).
@@ -28,37 +31,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from tigerbeetle_amd import Engine, Job, trees  # noqa: E402
+from tigerbeetle_amd import Engine, Job, configs  # noqa: E402
 from tigerbeetle_amd.shard import plan_shards, reduce_step  # noqa: E402
 
 METRIC = "compacted input MB/s per GPU and per node (1/2/4/8) + % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-TABLE = 262_080
-JOBS = 28
-SEED = 0x7B0002
-
-
-def gen_job(job: int, n_b_tables: int = 8):
-    """Values of one L0->L1 id-tree compaction: A (1 table) and B (8 tables)."""
-    rng = np.random.default_rng(SEED + job)
-    n = TABLE * (n_b_tables + 1)
-    hi = rng.integers(0, 1 << 63, size=n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, size=n, dtype=np.uint64)
-    lo = rng.integers(0, 1 << 63, size=n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, size=n, dtype=np.uint64)
-    order = np.lexsort((lo, hi))
-    hi, lo = hi[order], lo[order]
-    dup = (hi[1:] == hi[:-1]) & (lo[1:] == lo[:-1])
-    assert not dup.any(), "duplicate u128 id drawn"
-    vals = np.zeros((n, 32), dtype=np.uint8)
-    w = vals.view(np.uint64)
-    w[:, 0] = lo
-    w[:, 1] = hi
-    w[:, 2] = rng.permutation(n).astype(np.uint64) + np.uint64(1)  # timestamps, insertion order
-    a_idx = np.sort(rng.choice(n, size=TABLE, replace=False))
-    mask = np.zeros(n, dtype=bool)
-    mask[a_idx] = True
-    a = vals[mask]
-    b = vals[~mask]
-    return a, [b[i * TABLE:(i + 1) * TABLE] for i in range(n_b_tables)]
 
 
 def blocks_of(table: np.ndarray, vcm: int) -> list:
@@ -66,66 +43,110 @@ def blocks_of(table: np.ndarray, vcm: int) -> list:
 
 
 class Workload:
-    """All jobs of one GPU staged in HBM as 1 MiB grid blocks."""
+    """All jobs of one GPU staged in HBM: disk tables as 1 MiB grid blocks,
+    memtables as one contiguous array (plus the unsorted copy they are
+    re-landed from each step when the config sorts them)."""
 
-    def __init__(self, eng: Engine, job_ids: list, bs: int):
-        self.spec = trees.BY_NAME["transfers.id"]
+    def __init__(self, eng: Engine, config: int, job_ids: list, bs: int):
+        self.config = config
         self.bs = bs
-        lay = self.spec.layout(bs)
-        self.vcm = lay["block_value_count_max"]
-        self.block_count_max = lay["block_count_max"]
-        self.jobs, self.bufs = [], []
+        self.jobs, self.bufs, self.specs = [], [], []
+        self.sorts, self.landings = [], []
         self.input_values = 0
-        for j, gid in enumerate(job_ids):
-            a, b_tables = gen_job(gid)
-            tables = [blocks_of(a, self.vcm)] + [blocks_of(t, self.vcm) for t in b_tables]
+        self.input_bytes = 0
+        self.sort_bytes = 0
+        base_addr = 1
+        for gid in job_ids:
+            js = configs.GENERATORS[config](gid)
+            spec = js.tree
+            lay = spec.layout(bs)
+            vcm = lay["block_value_count_max"]
+            reservation = (len(js.b_tables) + 1) * lay["block_count_max"]  # compaction.zig:316-318
+            if js.a_immutable:
+                abuf = eng.upload(js.a) if len(js.a) else None
+                segs_a = [(abuf.ptr, len(js.a))] if abuf else []
+                if abuf:
+                    self.bufs.append(abuf)
+                if js.a_unsorted:
+                    pristine = eng.upload(js.a)
+                    self.bufs.append(pristine)
+                    self.landings.append((abuf.ptr, pristine.ptr, js.a.nbytes))
+                    self.sorts.append((spec, abuf.ptr, len(js.a)))
+                    self.sort_bytes += 2 * js.a.nbytes
+                tables = []
+            else:
+                tables = [blocks_of(js.a, vcm)]
+                segs_a = None
+            tables += [blocks_of(t, vcm) for t in js.b_tables]
             nblk = sum(len(t) for t in tables)
-            host = np.zeros((nblk, bs), dtype=np.uint8)
-            segs, k = [], 0
-            for t in tables:
-                for v in t:
-                    host[k, 256:256 + v.nbytes] = v.reshape(-1)
-                    segs.append((k, len(v)))
-                    k += 1
-            ibuf = eng.upload(host)
-            del host
-            seg_ptrs = [(ibuf.ptr + i * bs + 256, c) for i, c in segs]
-            na = len(blocks_of(a, self.vcm))
-            reservation = (len(b_tables) + 1) * self.block_count_max  # compaction.zig:316-318
+            segs = []
+            if nblk:
+                host = np.zeros((nblk, bs), dtype=np.uint8)
+                k = 0
+                for t in tables:
+                    for v in t:
+                        host[k, 256:256 + v.nbytes] = v.reshape(-1)
+                        segs.append((k, len(v)))
+                        k += 1
+                ibuf = eng.upload(host)
+                del host
+                self.bufs.append(ibuf)
+                seg_ptrs = [(ibuf.ptr + i * bs + 256, c) for i, c in segs]
+            else:
+                seg_ptrs = []
+            if segs_a is None:
+                na = len(tables[0])
+                segs_a, segs_b = seg_ptrs[:na], seg_ptrs[na:]
+            else:
+                segs_b = seg_ptrs
             out = eng.alloc(reservation * bs)
-            addrs = np.arange(1 + j * reservation, 1 + (j + 1) * reservation, dtype=np.uint64)
-            self.jobs.append(Job(self.spec, seg_ptrs[:na], seg_ptrs[na:], False, False, 1, 0xA5A5, 48,
+            addrs = np.arange(base_addr, base_addr + reservation, dtype=np.uint64)
+            base_addr += reservation
+            self.jobs.append(Job(spec, segs_a, segs_b, js.a_immutable, js.drop_tombstones, js.level_b, 0xA5A5, 48,
                                  addrs, out))
-            self.bufs += [ibuf, out]
-            self.input_values += len(a) + sum(len(t) for t in b_tables)
+            self.specs.append(js)
+            self.bufs.append(out)
+            self.input_values += js.input_values
+            self.input_bytes += js.input_bytes
+            del js
 
-    @property
-    def input_bytes(self) -> int:
-        return self.input_values * self.spec.value_size
+    def step(self, eng: Engine):
+        """One step: land + sort the bar's memtables (config 3), then the
+        compaction batch; returns the completed batch."""
+        for dst, src, n in self.landings:
+            eng.copy_device_async(dst, src, n)
+        if self.sorts:
+            eng.sort_values_batch(self.sorts)
+        b = eng.submit(self.jobs)
+        b.wait()
+        return b
 
 
-def cpu_baseline(budget_s: float = 12.0, bs: int = 1 << 20) -> dict:
+def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 << 20) -> dict:
     """The oracle (single-threaded C restatement, AES-NI AEGIS) on a bounded
-    sample of the same workload: whole jobs until the time budget is used."""
+    sample of the same workload: whole jobs (memtable sort included for
+    config 3) until the time budget is used."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle
     oracle.build()
-    spec = trees.BY_NAME["transfers.id"]
-    t = oracle.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
-                    spec.value_count_max, bs)
-    vcm = t.block_value_count_max
     total_bytes, total_t, jobs = 0, 0.0, 0
-    while total_t < budget_s and jobs < JOBS:
-        a, b_tables = gen_job(jobs)
-        segs_a = blocks_of(a, vcm)
-        segs_b = [blk for tb in b_tables for blk in blocks_of(tb, vcm)]
-        reservation = (len(b_tables) + 1) * (t.data_block_count_max + 1)
+    while total_t < budget_s and jobs < njobs:
+        js = configs.GENERATORS[config](jobs)
+        spec = js.tree
+        t = oracle.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                        spec.value_count_max, bs)
+        vcm = t.block_value_count_max
+        segs_b = [blk for tb in js.b_tables for blk in blocks_of(tb, vcm)]
+        reservation = (len(js.b_tables) + 1) * (t.data_block_count_max + 1)
         t0 = time.perf_counter()
-        r = oracle.compact(t, segs_a, segs_b, a_immutable=False, drop_tombstones=False, level_b=1, cluster=0xA5A5,
-                           snapshot_min=48, addresses=np.arange(1, 1 + reservation, dtype=np.uint64))
+        a = oracle.sort_values(t, js.a) if js.a_unsorted else js.a
+        segs_a = ([a] if len(a) else []) if js.a_immutable else blocks_of(a, vcm)
+        r = oracle.compact(t, segs_a, segs_b, a_immutable=js.a_immutable, drop_tombstones=js.drop_tombstones,
+                           level_b=js.level_b, cluster=0xA5A5, snapshot_min=48,
+                           addresses=np.arange(1, 1 + reservation, dtype=np.uint64))
         total_t += time.perf_counter() - t0
         assert r.status == 0
-        total_bytes += (len(a) + sum(len(x) for x in b_tables)) * spec.value_size
+        total_bytes += js.input_bytes
         jobs += 1
     import platform
     cpu = platform.processor() or "unknown"
@@ -138,8 +159,8 @@ def cpu_baseline(budget_s: float = 12.0, bs: int = 1 << 20) -> dict:
         pass
     from oracle.oracle import lib as olib
     return {"value": round(total_bytes / total_t / 1e6, 1), "unit": "MB/s", "cores": 1, "kind": "port",
-            "sample": f"{jobs} of {JOBS} jobs ({total_bytes/1e6:.0f} MB of input) through oracle/tbc_oracle.c "
-                      f"(single thread, AES-NI={bool(olib().tbo_has_aesni())}) on {cpu}"}
+            "sample": f"{jobs} of {njobs} jobs ({total_bytes/1e6:.0f} MB of input) of config {config} through "
+                      f"oracle/tbc_oracle.c (single thread, AES-NI={bool(olib().tbo_has_aesni())}) on {cpu}"}
 
 
 # bench kernel label -> rocprofv3 kernel symbol (tools/traffic.py short names)
@@ -169,11 +190,13 @@ def pmc_traffic(kernel: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--jobs", type=int, default=JOBS)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(configs.GENERATORS))
+    ap.add_argument("--jobs", type=int, default=None, help="jobs per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    njobs = args.jobs or configs.DEFAULT_JOBS[args.config]
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,20 +210,16 @@ def main() -> None:
         dist = td
 
     bs = 1 << 20
-    eng = Engine(device=local, block_size=bs, profile=True)
-    # Weak scaling: args.jobs jobs per GPU; the global job set is sharded by
-    # bytes (all jobs are the same size here), no data-path collective.
-    plan = plan_shards([1] * (args.jobs * world), world)
-    wl = Workload(eng, plan[rank], bs)
+    eng = Engine(device=local, block_size=bs, profile=True, arena_bytes=2 << 30)
+    # Weak scaling: njobs jobs per GPU; the global job set is sharded by
+    # bytes (all jobs of a config are about the same size), no data-path
+    # collective.
+    plan = plan_shards([1] * (njobs * world), world)
+    wl = Workload(eng, args.config, plan[rank], bs)
     eng.synchronize()
 
-    def step():
-        b = eng.submit(wl.jobs)
-        b.wait()
-        return b
-
     for _ in range(args.warmup):
-        step().release()
+        wl.step(eng).release()
 
     def barrier():
         eng.synchronize()
@@ -210,21 +229,36 @@ def main() -> None:
             dist.barrier()
 
     barrier()
+    import gc
+    gc.collect()
+    gc.disable()  # no collector pause inside the timed region
     t0 = time.perf_counter()
     ktimes: dict = {}
+    marks = []
     for _ in range(args.steps):
-        b = step()
+        b = wl.step(eng)
+        marks.append(time.perf_counter())
         for k, v in b.kernel_times().items():
             ktimes[k] = ktimes.get(k, 0.0) + v
         b.release()
     barrier()
+    gc.enable()
+    if os.environ.get("TBC_BENCH_TRACE"):
+        print("step ms:", " ".join(f"{(b - a) * 1e3:.2f}" for a, b in zip([t0] + marks, marks)), file=sys.stderr)
     dt = time.perf_counter() - t0
-    # Verify the last step's shape (every job: all values out, 72 data blocks, 9 tables).
-    b = step()
-    res0, _ = b.result(0)
+    # Check the last step's results: every job OK, and output shape for the bytes.
+    b = wl.step(eng)
+    out_values = data_blocks = tables = index_bytes = 0
+    for i, js in enumerate(wl.specs):
+        r, _ = b.result(i)
+        assert r.status == 0, (i, r.status)
+        out_values += r.value_count * js.tree.value_size
+        data_blocks += r.data_block_count
+        tables += r.table_count
+        index_bytes += r.table_count * js.tree.layout(bs)["index_size"]
+        if args.config == 2 and not os.environ.get("TBC_LIB"):  # ablation builds (timing only) skip this
+            assert r.value_count == 9 * configs.TABLE_T and r.table_count == 9, (r.value_count, r.table_count)
     b.release()
-    if not os.environ.get("TBC_LIB"):  # ablation builds (timing only) skip the shape check
-        assert res0.value_count == 9 * TABLE and res0.table_count == 9, (res0.value_count, res0.table_count)
 
     total_bytes, t_max = reduce_step(dist, wl.input_bytes, dt, device=f"cuda:{local}" if dist else None)
     step_s = t_max / args.steps
@@ -233,24 +267,18 @@ def main() -> None:
     # Per-kernel device times (hipEvents on the engine's stream), per step.
     per_step = {k: v / args.steps for k, v in ktimes.items()}
     dominant = max(per_step, key=per_step.get)
-    spec = wl.spec
-    n_in = wl.input_values
-    out_values = n_in  # no dedup / tombstones in this workload
-    data_blocks = args.jobs * 72
-    tables = args.jobs * 9
-    index_size = spec.layout(bs)["index_size"]
-    R = n_in * spec.value_size
-    W_data = out_values * spec.value_size + data_blocks * 256
-    W_index = tables * index_size
+    R = wl.input_bytes
+    W_data = out_values + data_blocks * 256  # out_values is in bytes here
+    W_index = index_bytes
     alg_bytes = {
-        "merge_partition": (args.jobs * 2400) * 2 * 21 * 32,
+        "merge_partition": len(wl.jobs) * 2400 * 2 * 21 * 32,
         "merge": R,  # read every input value once (keys decide; 2 mask bits per position written)
-        "data_blocks": out_values * spec.value_size + W_data,  # read every survivor once, write the blocks
+        "data_blocks": out_values + W_data,  # read every survivor once, write the blocks
         "index_blocks": W_index + data_blocks * 64,
     }
     kt_us = per_step[dominant]
     achieved = alg_bytes.get(dominant, R) / (kt_us * 1e-6) / 1e9
-    job_bytes = R + W_data + W_index
+    job_bytes = R + W_data + W_index + wl.sort_bytes  # R + W (+ S)
     traffic, traffic_src = pmc_traffic(dominant)
     line = {
         "metric": METRIC,
@@ -264,10 +292,10 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded IdTreeValue tables, config 2)",
-        "config": {"workload": "transfers.id L0->L1 compaction, 28 jobs x (1 A + 8 B tables) per GPU, "
-                               "64M u128 keys, 1 MiB blocks", "jobs_per_gpu": args.jobs,
-                   "input_bytes_per_gpu": wl.input_bytes, "block_size": bs, "parallelism": f"shard-by-job x{world}"},
+        "data": f"synthetic (seeded tables, BASELINE config {args.config}: tigerbeetle_amd/configs.py)",
+        "config": {"workload": configs.DESCRIPTION[args.config], "baseline_config": args.config,
+                   "jobs_per_gpu": njobs, "input_bytes_per_gpu": wl.input_bytes, "block_size": bs,
+                   "parallelism": f"shard-by-job x{world}"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
@@ -277,7 +305,7 @@ def main() -> None:
         "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline()
+        line["cpu_baseline"] = cpu_baseline(args.config, njobs)
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()

@@ -139,6 +139,9 @@ tbc_status tbc_device_alloc(tbc_engine *engine, uint64_t bytes, void **out_ptr);
 tbc_status tbc_device_free(tbc_engine *engine, void *ptr);
 tbc_status tbc_copy_to_device(tbc_engine *engine, void *dst, const void *src, uint64_t bytes);
 tbc_status tbc_copy_to_host(tbc_engine *engine, void *dst, const void *src, uint64_t bytes);
+/* Device-to-device copy enqueued on the engine stream (no host wait): e.g.
+ * landing a bar's mutable table next to the sort that consumes it. */
+tbc_status tbc_copy_device_async(tbc_engine *engine, void *dst, const void *src, uint64_t bytes);
 tbc_status tbc_memset_device(tbc_engine *engine, void *dst, int value, uint64_t bytes);
 tbc_status tbc_synchronize(tbc_engine *engine);
 
@@ -155,6 +158,20 @@ tbc_status tbc_checksum_batch(tbc_engine *engine, const void *const *messages, c
 tbc_status tbc_sort_values(tbc_engine *engine, const tbc_tree *tree, void *values, uint32_t count);
 /* Asynchronous variant: enqueued on the engine stream ahead of later batches. */
 tbc_status tbc_sort_values_async(tbc_engine *engine, const tbc_tree *tree, void *values, uint32_t count);
+
+/* Bar end of a whole forest: every tree's mutable table sorted by ONE
+ * segmented launch sequence (tree.zig:979-999 calls TableMemory.sort once per
+ * tree; the batch is the same work without a launch train per tree). Same
+ * semantics per table as tbc_sort_values; tables that are already sorted are
+ * left untouched. Enqueued on the engine stream; blocks once on a small
+ * device->host read of the key probe (the radix digit plan). */
+typedef struct tbc_sort_job {
+    tbc_tree tree;
+    void *values;   /* device pointer, 16-byte aligned */
+    uint32_t count;
+    uint32_t reserved;
+} tbc_sort_job;
+tbc_status tbc_sort_values_batch(tbc_engine *engine, const tbc_sort_job *jobs, uint32_t count);
 
 /* ---- compaction ------------------------------------------------------------- */
 /* Enqueue `count` independent compactions (one half-bar's jobs) as one batch.

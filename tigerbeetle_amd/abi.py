@@ -75,6 +75,11 @@ class Segment(ctypes.Structure):
     _fields_ = [("values", ctypes.c_void_p), ("count", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+class SortJob(ctypes.Structure):
+    _fields_ = [("tree", Tree), ("values", ctypes.c_void_p), ("count", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
 class Compaction(ctypes.Structure):
     _fields_ = [
         ("tree", Tree),
@@ -121,8 +126,10 @@ _SIGNATURES = {
     "tbc_synchronize": (ctypes.c_int, [_P]),
     "tbc_checksum_batch": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_uint32, _P]),
+    "tbc_copy_device_async": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64]),
     "tbc_sort_values": (ctypes.c_int, [_P, ctypes.POINTER(Tree), _P, ctypes.c_uint32]),
     "tbc_sort_values_async": (ctypes.c_int, [_P, ctypes.POINTER(Tree), _P, ctypes.c_uint32]),
+    "tbc_sort_values_batch": (ctypes.c_int, [_P, ctypes.POINTER(SortJob), ctypes.c_uint32]),
     "tbc_compaction_submit": (ctypes.c_int, [_P, ctypes.POINTER(Compaction), ctypes.c_uint32,
                                              ctypes.POINTER(_P)]),
     "tbc_batch_poll": (ctypes.c_int, [_P]),

@@ -1,0 +1,177 @@
+"""BASELINE.json workloads as seeded synthetic compaction jobs.
+
+Every generator is deterministic in (config, job id), so any rank can build
+any job without communication, and jobs are produced lazily (one job's host
+arrays at a time) to keep host memory bounded at the 1B-value scale.
+
+  config 2  transfers.id L0->L1: 1 disk A table + 8 full B tables of unique
+            uniform-random u128 ids (IdTreeValue, 32 B), no dups/tombstones.
+  config 3  secondary indexes transfers.debit_account_id / credit_account_id
+            (CompositeKey(u128), 32 B): the bar's mutable table (262,080
+            values, account id Zipf(1.1) over 10,000 accounts, timestamps
+            monotone) arrives UNSORTED and is sorted on the device
+            (TableMemory.sort) before its immutable->L0 compaction against 8
+            L0 tables; 1% of the bar's puts are removed again (half inside the
+            bar -> put/remove pairs cancel in fill_immutable_values, half
+            removing an older put that lives in B -> both dropped by the
+            secondary-index merge rule). Every 7th job is the sequential
+            transfers.timestamp object tree (Transfer, 128 B): already sorted,
+            no B, a pure flush.
+  config 5  accounts.timestamp object tree (Account, 128 B), last level:
+            disk A = 1 table (524,160 newer versions of uniformly chosen
+            existing keys, 1% tombstones) into 8 last-level B tables;
+            drop_tombstones = true, level_b = 6.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import trees, workloads
+from .workloads import TOMB
+
+CONFIG2_SEED = 0x7B0002
+CONFIG3_SEED = 0x7B0003
+CONFIG5_SEED = 0x7B0005
+TABLE_T = trees.BY_NAME["transfers.id"].value_count_max               # 262,080
+TABLE_A_TS = trees.BY_NAME["accounts.timestamp"].value_count_max      # 524,160
+ACCOUNTS = 10_000
+
+
+@dataclass
+class JobSpec:
+    tree: trees.TreeSpec
+    a: np.ndarray             # (n, vs) uint8; immutable: insertion order if a_unsorted
+    a_immutable: bool
+    a_unsorted: bool          # the memtable must be sorted (TableMemory.sort) first
+    b_tables: list            # [(n_i, vs) uint8], ascending, disjoint
+    drop_tombstones: bool
+    level_b: int
+
+    @property
+    def input_values(self) -> int:
+        return len(self.a) + sum(len(t) for t in self.b_tables)
+
+    @property
+    def input_bytes(self) -> int:
+        return self.input_values * self.tree.value_size
+
+
+def config2_job(job: int, n_b_tables: int = 8) -> JobSpec:
+    """One transfers.id L0->L1 compaction (BASELINE configs[1])."""
+    rng = np.random.default_rng(CONFIG2_SEED + job)
+    n = TABLE_T * (n_b_tables + 1)
+    hi = rng.integers(0, 1 << 63, size=n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, size=n, dtype=np.uint64)
+    lo = rng.integers(0, 1 << 63, size=n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, size=n, dtype=np.uint64)
+    order = np.lexsort((lo, hi))
+    hi, lo = hi[order], lo[order]
+    dup = (hi[1:] == hi[:-1]) & (lo[1:] == lo[:-1])
+    assert not dup.any(), "duplicate u128 id drawn"
+    vals = np.zeros((n, 32), dtype=np.uint8)
+    w = vals.view(np.uint64)
+    w[:, 0] = lo
+    w[:, 1] = hi
+    w[:, 2] = rng.permutation(n).astype(np.uint64) + np.uint64(1)  # timestamps, insertion order
+    a_idx = np.sort(rng.choice(n, size=TABLE_T, replace=False))
+    mask = np.zeros(n, dtype=bool)
+    mask[a_idx] = True
+    a = vals[mask]
+    b = vals[~mask]
+    return JobSpec(trees.BY_NAME["transfers.id"], a, False, False,
+                   [b[i * TABLE_T:(i + 1) * TABLE_T] for i in range(n_b_tables)], False, 1)
+
+
+def _zipf_accounts(rng, n: int, s: float = 1.1) -> np.ndarray:
+    ranks = np.arange(1, ACCOUNTS + 1, dtype=np.float64)
+    p = ranks ** -s
+    p /= p.sum()
+    ids = rng.choice(ACCOUNTS, size=n, p=p).astype(np.uint64) + np.uint64(1)
+    return ids
+
+
+def _composite128(field: np.ndarray, ts: np.ndarray, tomb: np.ndarray) -> np.ndarray:
+    """CompositeKey(u128){field, timestamp (| tombstone bit), padding 0}
+    (composite_key.zig:17-46); field < 2^64 here (account ids)."""
+    v = np.zeros((len(field), 32), dtype=np.uint8)
+    w = v.view(np.uint64)
+    w[:, 0] = field
+    w[:, 2] = ts | np.where(tomb, TOMB, np.uint64(0))
+    return v
+
+
+def _sorted_composite(v: np.ndarray) -> np.ndarray:
+    w = v.view(np.uint64)
+    return v[np.lexsort((w[:, 2] & workloads.MASK63, w[:, 0], w[:, 1]))]  # field hi, field lo, ts (stable)
+
+
+def config3_job(job: int, n_b_tables: int = 8) -> JobSpec:
+    """One bar-end job of config 3 (BASELINE configs[2])."""
+    rng = np.random.default_rng(CONFIG3_SEED + job)
+    bar_ts0 = np.uint64(1 + (job + n_b_tables) * 4 * TABLE_T)  # later jobs are later bars
+    if job % 7 == 6:
+        # Sequential: transfers.timestamp, already-sorted memtable, empty L0.
+        spec = trees.BY_NAME["transfers.timestamp"]
+        ts = bar_ts0 + np.arange(TABLE_T, dtype=np.uint64)
+        a = workloads.values_from_keys(spec, [ts], np.zeros(TABLE_T, dtype=bool), rng)
+        return JobSpec(spec, a, True, False, [], False, 0)
+    spec = trees.BY_NAME["transfers.debit_account_id" if job % 2 == 0 else "transfers.credit_account_id"]
+    # B: 8 L0 tables of older puts (timestamps before this bar), sorted, cut.
+    nb = n_b_tables * TABLE_T
+    b_ts = np.uint64(1) + rng.choice(int(bar_ts0) - 1, size=nb, replace=False).astype(np.uint64)
+    b_all = _sorted_composite(_composite128(_zipf_accounts(rng, nb), b_ts, np.zeros(nb, dtype=bool)))
+    b_tables = [b_all[i * TABLE_T:(i + 1) * TABLE_T] for i in range(n_b_tables)]
+    # The bar: 262,080 index updates in timestamp order (insertion order).
+    n_rm = TABLE_T // 100
+    n_put = TABLE_T - n_rm
+    put_ts = bar_ts0 + np.arange(n_put, dtype=np.uint64)
+    put_field = _zipf_accounts(rng, n_put)
+    ins = [_composite128(put_field, put_ts, np.zeros(n_put, dtype=bool))]
+    # removes of puts inside this bar (appended after their put: insertion order)
+    k_in = n_rm // 2
+    victims = rng.choice(n_put, size=k_in, replace=False)
+    ins.append(_composite128(put_field[victims], put_ts[victims], np.ones(k_in, dtype=bool)))
+    # removes of older puts that live in B
+    k_b = n_rm - k_in
+    bw = b_all.view(np.uint64)
+    old = rng.choice(nb, size=k_b, replace=False)
+    ins.append(_composite128(bw[old, 0].copy(), bw[old, 2].copy(), np.ones(k_b, dtype=bool)))
+    a = np.concatenate(ins)
+    # Interleave removes after their puts: a random insertion order that keeps
+    # each (field, ts) run in put-then-remove order (last put wins).
+    a = workloads.shuffle_for_memtable(_sorted_composite(a), rng, spec)
+    return JobSpec(spec, a, True, True, b_tables, False, 0)
+
+
+def config5_job(job: int, n_b_tables: int = 8) -> JobSpec:
+    """One last-level accounts.timestamp compaction (BASELINE configs[4])."""
+    rng = np.random.default_rng(CONFIG5_SEED + job)
+    spec = trees.BY_NAME["accounts.timestamp"]
+    nb = n_b_tables * TABLE_A_TS
+    # disjoint key range per job; strictly increasing timestamps with gaps
+    base = np.uint64(1 + job * nb * 4)
+    keys = base + np.cumsum(rng.integers(1, 4, size=nb, dtype=np.uint64))
+    b_all = np.empty((nb, 128), dtype=np.uint8)
+    bw = b_all.view(np.uint64)
+    bw[:] = rng.integers(0, 1 << 63, size=(nb, 16), dtype=np.uint64)
+    bw[:, 15] = keys  # timestamp at byte 120 (tigerbeetle.zig:7-40)
+    a_idx = np.sort(rng.choice(nb, size=TABLE_A_TS, replace=False))
+    tomb = rng.random(TABLE_A_TS) < 0.01
+    a = np.empty((TABLE_A_TS, 128), dtype=np.uint8)
+    aw = a.view(np.uint64)
+    aw[:] = rng.integers(0, 1 << 63, size=(TABLE_A_TS, 16), dtype=np.uint64)
+    aw[tomb] = 0  # tombstone = zeroed Value with ts | bit63 (groove.zig:38-44)
+    aw[:, 15] = keys[a_idx] | np.where(tomb, TOMB, np.uint64(0))
+    return JobSpec(spec, a, False, False, [b_all[i * TABLE_A_TS:(i + 1) * TABLE_A_TS] for i in range(n_b_tables)],
+                   True, 6)
+
+
+GENERATORS = {2: config2_job, 3: config3_job, 5: config5_job}
+DEFAULT_JOBS = {2: 28, 3: 28, 5: 27}
+DESCRIPTION = {
+    2: "transfers.id L0->L1 compaction, 28 jobs x (1 A + 8 B tables) per GPU, 64M u128 keys, 1 MiB blocks",
+    3: "bar end of transfers.debit/credit_account_id (Zipf 1.1 over 10k accounts, unsorted memtable sorted on "
+       "device, 1% put/remove pairs) + sequential transfers.timestamp flushes, 28 jobs per GPU",
+    5: "accounts.timestamp last-level compaction (Account 128 B, 1% tombstones dropped), 27 jobs x 4.7M values "
+       "per GPU (1B values over 8 GPUs)",
+}

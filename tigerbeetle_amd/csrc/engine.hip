@@ -224,6 +224,13 @@ tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t 
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
+tbc_status tbc_copy_device_async(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    if (!e || (bytes && (!dst || !src))) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, e->stream) == hipSuccess ? TBC_OK
+                                                                                          : TBC_ERR_DEVICE;
+}
+
 tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
@@ -273,22 +280,39 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
     return st;
 }
 
-tbc_status tbc_sort_values_async(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
-    if (!e || !tree || (count && !values)) return TBC_ERR_INVALID_ARGUMENT;
-    Layout L;
-    if (!compute_layout(tree, e->block_size, &L)) return TBC_ERR_INVALID_ARGUMENT;
-    if (count < 2) return TBC_OK;
+static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count) {
+    if (!e || (count && !jobs)) return TBC_ERR_INVALID_ARGUMENT;
+    std::vector<SortItem> items(count);
+    for (uint32_t k = 0; k < count; k++) {
+        const tbc_sort_job &j = jobs[k];
+        Layout L;
+        if (!compute_layout(&j.tree, e->block_size, &L) || (j.count && !j.values) || ((uintptr_t)j.values & 15))
+            return TBC_ERR_INVALID_ARGUMENT;
+        items[k] = SortItem{j.values, j.count, j.tree.value_size, j.tree.timestamp_offset, j.tree.key_kind};
+    }
     hipSetDevice(e->device);
-    const uint64_t need = sort_scratch_bytes(tree->value_size, count);
+    const uint64_t need = sort_scratch_bytes(items.data(), count);
     const uint64_t dt = e->dev.top;
     uint8_t *scratch = e->dev.alloc(need);
     if (!scratch) return TBC_ERR_OUT_OF_MEMORY;
-    int rc = launch_sort(tree->key_kind, tree->value_size, tree->timestamp_offset, values, count, scratch, need,
-                         e->stream);
+    int rc = launch_sort_batch(items.data(), count, scratch, need, e->stream);
     // Stream order protects the scratch: the next user of this arena range is
     // enqueued on the same stream after the sort.
     e->dev.top = dt;
     return rc == 0 ? TBC_OK : TBC_ERR_DEVICE;
+}
+
+tbc_status tbc_sort_values_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count) {
+    return sort_batch(e, jobs, count);
+}
+
+tbc_status tbc_sort_values_async(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
+    if (!e || !tree) return TBC_ERR_INVALID_ARGUMENT;
+    tbc_sort_job j{};
+    j.tree = *tree;
+    j.values = values;
+    j.count = count;
+    return sort_batch(e, &j, 1);
 }
 
 tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
@@ -553,7 +577,12 @@ tbc_status tbc_batch_wait(tbc_batch *b) {
     if (!b) return TBC_ERR_INVALID_ARGUMENT;
     if (b->complete) return b->result;
     hipSetDevice(b->engine->device);
-    if (hipEventSynchronize(b->done) != hipSuccess) {
+    // Poll like the adapter's event loop would (tbc_batch_poll), instead of a
+    // blocking hipEventSynchronize whose OS wake-up adds milliseconds of jitter.
+    hipError_t q;
+    while ((q = hipEventQuery(b->done)) == hipErrorNotReady) {
+    }
+    if (q != hipSuccess) {
         b->complete = true;
         b->result = TBC_ERR_DEVICE;
         return b->result;

@@ -5,6 +5,8 @@
 // (table_memory.zig:83-87). Stability is load-bearing: fill_immutable_values
 // keeps the LAST of a run of equal keys (compaction.zig:519-522).
 //
+// A batch of memtables (every tree's at the bar end) is sorted by ONE
+// launch sequence (segmented: tiles never straddle memtables).
 // Here: a stable LSD radix sort of (key limbs, original index) items with
 // 4-bit digits, skipping every digit that is constant across the table (one
 // probe pass computes OR/AND of all keys and the sortedness flag), then one
@@ -17,6 +19,8 @@
 //             (tile offset of digit) + (rank among earlier same-digit items):
 //             stable by construction.
 #include <hip/hip_runtime.h>
+
+#include <vector>
 
 #include "tbc_internal.h"
 
@@ -31,8 +35,19 @@ constexpr uint32_t kBins = 1u << kDigitBits;
 struct SortProbe {
     uint64_t or_[4];
     uint64_t and_[4];
-    uint32_t unsorted;
-    uint32_t pad[7];
+};
+
+// One memtable of the batch. Items of all segments live in one global item
+// space (segment s at [item_base, item_base + n)); tiles never straddle a
+// segment, so every tile knows its segment and the digit-major histograms of
+// a segment are contiguous: ONE exclusive scan over [segment][digit][tile]
+// yields global, segment-grouped destinations (a segmented stable sort with
+// no segment digit).
+struct SortSeg {
+    uint8_t *values;
+    uint8_t *scratch; // n * vs bytes: gather target, copied back
+    uint32_t n, vs, ts_off, kind;
+    uint32_t item_base, tile_base, tiles, unsorted;
 };
 
 __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t ts_off, uint64_t k[3]) {
@@ -45,28 +60,34 @@ __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t
     }
 }
 
-// Extract keys (limb-major) and indices; OR/AND of all keys; sortedness.
-__global__ __launch_bounds__(256) void k_sort_extract(uint32_t kind, uint32_t kl, const uint8_t *values, uint32_t n,
-                                                      uint32_t vs, uint32_t ts_off, uint64_t *keys, uint32_t *idx,
-                                                      SortProbe *probe) {
+// One workgroup per tile: extract keys (limb-major, global item positions)
+// and item indices; OR/AND of all keys; per-segment sortedness
+// (table_memory.zig:83-87 tracks it on put; here it is recomputed).
+__global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint32_t *tile_seg, uint32_t kl,
+                                                      uint32_t N, uint64_t *keys, uint32_t *idx, SortProbe *probe) {
     __shared__ uint64_t s_or[3][4], s_and[3][4];
     __shared__ uint32_t s_uns;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t sg = tile_seg[blockIdx.x];
+    const SortSeg S = segs[sg];
+    const uint32_t lt = blockIdx.x - S.tile_base;
     if (tid == 0) s_uns = 0;
     uint64_t o[3] = {0, 0, 0}, a[3] = {~0ull, ~0ull, ~0ull};
     uint32_t uns = 0;
-    for (uint32_t i = blockIdx.x * 256 + tid; i < n; i += gridDim.x * 256) {
+    for (uint32_t r = 0; r < kSortPer; r++) {
+        const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
+        if (li >= S.n) break;
+        const uint32_t i = S.item_base + li;
         uint64_t k[3], kn[3];
-        key_of(kind, values + (size_t)i * vs, ts_off, k);
+        key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
         for (uint32_t l = 0; l < kl; l++) {
-            keys[(size_t)l * n + i] = k[l];
+            keys[(size_t)l * N + i] = k[l];
             o[l] |= k[l];
             a[l] &= k[l];
         }
         idx[i] = i;
-        if (i + 1 < n) {
-            key_of(kind, values + (size_t)(i + 1) * vs, ts_off, kn);
-            // unsorted iff key[i] > key[i+1]
+        if (li + 1 < S.n) {
+            key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
             bool gt = false, decided = false;
             for (int l = (int)kl - 1; l >= 0 && !decided; l--) {
                 if (k[l] != kn[l]) {
@@ -100,28 +121,32 @@ __global__ __launch_bounds__(256) void k_sort_extract(uint32_t kind, uint32_t kl
             atomicOr((unsigned long long *)&probe->or_[l], (unsigned long long)oo);
             atomicAnd((unsigned long long *)&probe->and_[l], (unsigned long long)aa);
         }
-        if (s_uns) atomicOr(&probe->unsorted, 1u);
+        if (s_uns) atomicOr(&segs[sg].unsorted, 1u);
     }
 }
 
-__device__ __forceinline__ uint32_t digit_of(const uint64_t *keys, uint32_t n, uint32_t limb, uint32_t shift,
-                                             uint32_t i) {
-    return (uint32_t)(gld<uint64_t>(keys + (size_t)limb * n + i) >> shift) & (kBins - 1);
+__device__ __forceinline__ uint32_t hist_slot(const SortSeg &S, uint32_t d, uint32_t lt) {
+    return S.tile_base * kBins + d * S.tiles + lt;
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort_hist(const uint64_t *keys, uint32_t n, uint32_t limb,
-                                                            uint32_t shift, uint32_t *hist, uint32_t ntiles) {
+__global__ __launch_bounds__(kSortThreads) void k_sort_hist(const SortSeg *segs, const uint32_t *tile_seg,
+                                                            const uint64_t *keys, uint32_t N, uint32_t limb,
+                                                            uint32_t shift, uint32_t *hist) {
     __shared__ uint32_t cnt[kBins];
     const uint32_t tid = threadIdx.x;
+    const SortSeg S = segs[tile_seg[blockIdx.x]];
+    const uint32_t lt = blockIdx.x - S.tile_base;
     if (tid < kBins) cnt[tid] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * kSortTile;
     for (uint32_t r = 0; r < kSortPer; r++) {
-        const uint32_t i = base + r * kSortThreads + tid;
-        if (i < n) atomicAdd(&cnt[digit_of(keys, n, limb, shift, i)], 1u);
+        const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
+        if (li < S.n) {
+            const uint32_t i = S.item_base + li;
+            atomicAdd(&cnt[(uint32_t)(gld<uint64_t>(keys + (size_t)limb * N + i) >> shift) & (kBins - 1)], 1u);
+        }
     }
     __syncthreads();
-    if (tid < kBins) hist[tid * ntiles + blockIdx.x] = cnt[tid];
+    if (tid < kBins) hist[hist_slot(S, tid, lt)] = cnt[tid];
 }
 
 // Exclusive scan of m entries in place (one workgroup).
@@ -152,23 +177,24 @@ __global__ __launch_bounds__(1024) void k_sort_scan(uint32_t *hist, uint32_t m) 
 }
 
 template <int KL>
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const uint64_t *keys_in, const uint32_t *idx_in,
-                                                               uint64_t *keys_out, uint32_t *idx_out, uint32_t n,
-                                                               uint32_t limb, uint32_t shift, const uint32_t *hist,
-                                                               uint32_t ntiles) {
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *segs, const uint32_t *tile_seg,
+                                                               const uint64_t *keys_in, const uint32_t *idx_in,
+                                                               uint64_t *keys_out, uint32_t *idx_out, uint32_t N,
+                                                               uint32_t limb, uint32_t shift, const uint32_t *hist) {
     __shared__ uint64_t s_key[KL][kSortTile];
     __shared__ uint32_t s_idx[kSortTile];
     __shared__ uint32_t s_cnt[kBins][kSortThreads + 1]; // digit-major per-thread counts
-    __shared__ uint32_t s_tot[kBins];
     const uint32_t tid = threadIdx.x;
-    const uint32_t base = blockIdx.x * kSortTile;
-    const uint32_t m = (n - base) < kSortTile ? (n - base) : kSortTile;
+    const SortSeg S = segs[tile_seg[blockIdx.x]];
+    const uint32_t lt = blockIdx.x - S.tile_base;
+    const uint32_t base = S.item_base + lt * kSortTile;
+    const uint32_t m = (S.n - lt * kSortTile) < kSortTile ? (S.n - lt * kSortTile) : kSortTile;
     // Coalesced load into LDS.
     for (uint32_t r = 0; r < kSortPer; r++) {
         const uint32_t e = r * kSortThreads + tid;
         if (e < m) {
 #pragma unroll
-            for (int l = 0; l < KL; l++) s_key[l][e] = gld<uint64_t>(keys_in + (size_t)l * n + base + e);
+            for (int l = 0; l < KL; l++) s_key[l][e] = gld<uint64_t>(keys_in + (size_t)l * N + base + e);
             s_idx[e] = gld<uint32_t>(idx_in + base + e);
         }
     }
@@ -203,13 +229,12 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const uint64_t *k
                 s_cnt[d][b0 + lane] = carry + incl - v;
                 carry += __shfl(incl, 63, 64);
             }
-            if (lane == 0) s_tot[d] = carry;
         }
     }
     __syncthreads();
     uint32_t run[kBins];
 #pragma unroll
-    for (uint32_t d = 0; d < kBins; d++) run[d] = hist[d * ntiles + blockIdx.x] + s_cnt[d][tid];
+    for (uint32_t d = 0; d < kBins; d++) run[d] = hist[hist_slot(S, d, lt)] + s_cnt[d][tid];
 #pragma unroll
     for (uint32_t k = 0; k < kSortPer; k++) {
         const uint32_t e = tid * kSortPer + k;
@@ -219,99 +244,160 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const uint64_t *k
             for (uint32_t d = 0; d < kBins; d++)
                 if (dig[k] == d) dst = run[d]++;
 #pragma unroll
-            for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)l * n + dst, s_key[l][e]);
+            for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)l * N + dst, s_key[l][e]);
             gst<uint32_t>(idx_out + dst, s_idx[e]);
         }
     }
 }
 
-// values_out[i] = values_in[idx[i]], 16 bytes per lane.
-__global__ __launch_bounds__(256) void k_sort_gather(const uint8_t *values_in, uint8_t *values_out,
-                                                     const uint32_t *idx, uint32_t n, uint32_t vs) {
-    const uint32_t cpv = vs >> 4;
-    const uint64_t chunks = (uint64_t)n * cpv;
-    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < chunks; c += (uint64_t)gridDim.x * 256) {
-        const uint32_t i = (uint32_t)(c / cpv), part = (uint32_t)(c % cpv);
-        const uint32_t src = gld<uint32_t>(idx + i);
-        gst<u32x4>(values_out + (size_t)i * vs + 16 * part, gld<u32x4>(values_in + (size_t)src * vs + 16 * part));
+// scratch[i] = values[idx[i]] (segment-local), 16 bytes per lane; sorted
+// segments are left alone.
+__global__ __launch_bounds__(256) void k_sort_gather(const SortSeg *segs, const uint32_t *tile_seg,
+                                                     const uint32_t *idx) {
+    const SortSeg S = segs[tile_seg[blockIdx.x]];
+    if (!S.unsorted) return;
+    const uint32_t lt = blockIdx.x - S.tile_base;
+    const uint32_t first = lt * kSortTile;
+    const uint32_t m = (S.n - first) < kSortTile ? (S.n - first) : kSortTile;
+    const uint32_t cpv = S.vs >> 4;
+    for (uint32_t c = threadIdx.x; c < m * cpv; c += 256) {
+        const uint32_t e = c / cpv, part = c % cpv;
+        const uint32_t src = gld<uint32_t>(idx + S.item_base + first + e) - S.item_base;
+        gst<u32x4>(S.scratch + (size_t)(first + e) * S.vs + 16 * part,
+                   gld<u32x4>(S.values + (size_t)src * S.vs + 16 * part));
     }
+}
+
+__global__ __launch_bounds__(256) void k_sort_copyback(const SortSeg *segs, const uint32_t *tile_seg) {
+    const SortSeg S = segs[tile_seg[blockIdx.x]];
+    if (!S.unsorted) return;
+    const uint32_t lt = blockIdx.x - S.tile_base;
+    const uint32_t first = lt * kSortTile;
+    const uint32_t m = (S.n - first) < kSortTile ? (S.n - first) : kSortTile;
+    const uint32_t chunks = m * (S.vs >> 4);
+    const size_t off = (size_t)first * S.vs;
+    for (uint32_t c = threadIdx.x; c < chunks; c += 256)
+        gst<u32x4>(S.values + off + 16 * (size_t)c, gld<u32x4>(S.scratch + off + 16 * (size_t)c));
 }
 
 static uint32_t key_limbs(uint32_t kind) {
     return kind == kKeyTimestamp ? 1 : kind == kKeyCompositeU128 ? 3 : 2;
 }
 
-uint64_t sort_scratch_bytes(uint32_t value_size, uint32_t n) {
-    const uint64_t ntiles = (n + kSortTile - 1) / kSortTile;
-    return 256                                       // probe
-           + 2 * ((uint64_t)n * (3 * 8 + 4) + 256)   // two item buffers
-           + 4 * kBins * ntiles + 256                // histogram
-           + (uint64_t)n * value_size + 256;         // gathered values
+static uint64_t tiles_of(uint32_t n) { return (n + kSortTile - 1) / kSortTile; }
+
+uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count) {
+    uint64_t N = 0, tiles = 0, vals = 0;
+    for (uint32_t j = 0; j < count; j++) {
+        if (items[j].n < 2) continue;
+        N += items[j].n;
+        tiles += tiles_of(items[j].n);
+        vals += ((uint64_t)items[j].n * items[j].value_size + 255) / 256 * 256;
+    }
+    return 256                                          // probe
+           + ((uint64_t)sizeof(SortSeg) * count + 255) / 256 * 256
+           + (4 * tiles + 255) / 256 * 256              // tile -> segment
+           + 2 * ((N * 3 * 8) + (N * 4 + 255) / 256 * 256) // two item buffers
+           + (4 * kBins * tiles + 255) / 256 * 256      // histogram
+           + vals;                                      // gathered values
 }
 
-int launch_sort(uint32_t kind, uint32_t vs, uint32_t ts_off, void *values, uint32_t n, void *scratch,
-                uint64_t scratch_bytes, void *stream) {
-    if (n < 2) return 0;
-    if (scratch_bytes < sort_scratch_bytes(vs, n)) return -1;
+int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *stream) {
+    if (scratch_bytes < sort_scratch_bytes(items, count)) return -1;
     hipStream_t s = (hipStream_t)stream;
-    const uint32_t kl = key_limbs(kind);
-    const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+    // Host plan: segments (n >= 2), tile bases, widest key.
+    std::vector<SortSeg> segs;
+    std::vector<uint32_t> tile_seg;
+    uint32_t N = 0, kl = 1;
+    for (uint32_t j = 0; j < count; j++) {
+        const SortItem &it = items[j];
+        if (it.n < 2) continue;
+        SortSeg g{};
+        g.values = (uint8_t *)it.values;
+        g.n = it.n;
+        g.vs = it.value_size;
+        g.ts_off = it.timestamp_offset;
+        g.kind = it.key_kind;
+        g.item_base = N;
+        g.tile_base = (uint32_t)tile_seg.size();
+        g.tiles = (uint32_t)tiles_of(it.n);
+        for (uint32_t t = 0; t < g.tiles; t++) tile_seg.push_back((uint32_t)segs.size());
+        N += it.n;
+        kl = kl > key_limbs(it.key_kind) ? kl : key_limbs(it.key_kind);
+        segs.push_back(g);
+    }
+    if (segs.empty()) return 0;
+    const uint32_t nseg = (uint32_t)segs.size(), ntiles = (uint32_t)tile_seg.size();
     uint8_t *p = (uint8_t *)scratch;
     SortProbe *probe = (SortProbe *)p;
     p += 256;
+    SortSeg *d_segs = (SortSeg *)p;
+    p += ((uint64_t)sizeof(SortSeg) * count + 255) / 256 * 256;
+    uint32_t *d_tile_seg = (uint32_t *)p;
+    p += (4ull * ntiles + 255) / 256 * 256;
     uint64_t *keys[2];
     uint32_t *idx[2];
     for (int b = 0; b < 2; b++) {
         keys[b] = (uint64_t *)p;
-        p += (uint64_t)n * 3 * 8;
+        p += (uint64_t)N * 3 * 8;
         idx[b] = (uint32_t *)p;
-        p += ((uint64_t)n * 4 + 255) / 256 * 256;
+        p += ((uint64_t)N * 4 + 255) / 256 * 256;
     }
     uint32_t *hist = (uint32_t *)p;
     p += ((uint64_t)4 * kBins * ntiles + 255) / 256 * 256;
-    uint8_t *gathered = p;
+    for (SortSeg &g : segs) {
+        g.scratch = p;
+        p += ((uint64_t)g.n * g.vs + 255) / 256 * 256;
+    }
 
+    // The plan is staged through static host memory owned by the caller's
+    // stream order: copy it synchronously with the probe read below.
     SortProbe init{};
     for (int l = 0; l < 4; l++) init.and_[l] = ~0ull;
-    if (hipMemcpyAsync(probe, &init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
-    const uint32_t eblocks = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
-    hipLaunchKernelGGL(k_sort_extract, dim3(eblocks), dim3(256), 0, s, kind, kl, (const uint8_t *)values, n, vs,
-                       ts_off, keys[0], idx[0], probe);
-    // The digit plan needs the probe on the host (one small synchronous read).
+    if (hipMemcpyAsync(probe, &init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_segs, segs.data(), sizeof(SortSeg) * nseg, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_tile_seg, tile_seg.data(), 4ull * ntiles, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg, kl, N, keys[0], idx[0],
+                       probe);
+    // The digit plan needs the probe on the host (one small synchronous read
+    // per batch, not per memtable).
     SortProbe host{};
-    if (hipMemcpyAsync(&host, probe, sizeof host, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-    if (hipStreamSynchronize(s) != hipSuccess) return -1;
-    if (!host.unsorted) return 0; // table_memory.zig:141: already sorted, no-op
+    std::vector<SortSeg> hsegs(nseg);
+    if (hipMemcpyAsync(&host, probe, sizeof host, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(hsegs.data(), d_segs, sizeof(SortSeg) * nseg, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    bool any = false;
+    for (const SortSeg &g : hsegs) any |= g.unsorted != 0;
+    if (!any) return 0; // table_memory.zig:141: already sorted, no-op
     int cur = 0;
     for (uint32_t limb = 0; limb < kl; limb++) {
         const uint64_t varies = host.or_[limb] ^ host.and_[limb];
         for (uint32_t shift = 0; shift < 64; shift += kDigitBits) {
             if (((varies >> shift) & (kBins - 1)) == 0) continue; // constant digit: order unchanged
-            hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(kSortThreads), 0, s, keys[cur], n, limb, shift, hist,
-                               ntiles);
+            hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg, keys[cur],
+                               N, limb, shift, hist);
             hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, kBins * ntiles);
             switch (kl) {
             case 1:
-                hipLaunchKernelGGL(k_sort_scatter<1>, dim3(ntiles), dim3(kSortThreads), 0, s, keys[cur], idx[cur],
-                                   keys[cur ^ 1], idx[cur ^ 1], n, limb, shift, hist, ntiles);
+                hipLaunchKernelGGL(k_sort_scatter<1>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
+                                   keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
                 break;
             case 2:
-                hipLaunchKernelGGL(k_sort_scatter<2>, dim3(ntiles), dim3(kSortThreads), 0, s, keys[cur], idx[cur],
-                                   keys[cur ^ 1], idx[cur ^ 1], n, limb, shift, hist, ntiles);
+                hipLaunchKernelGGL(k_sort_scatter<2>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
+                                   keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
                 break;
             default:
-                hipLaunchKernelGGL(k_sort_scatter<3>, dim3(ntiles), dim3(kSortThreads), 0, s, keys[cur], idx[cur],
-                                   keys[cur ^ 1], idx[cur ^ 1], n, limb, shift, hist, ntiles);
+                hipLaunchKernelGGL(k_sort_scatter<3>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
+                                   keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
                 break;
             }
             cur ^= 1;
         }
     }
-    const uint64_t chunks = (uint64_t)n * (vs >> 4);
-    const uint32_t gblocks = (uint32_t)((chunks + 255) / 256 < 4096 ? (chunks + 255) / 256 : 4096);
-    hipLaunchKernelGGL(k_sort_gather, dim3(gblocks), dim3(256), 0, s, (const uint8_t *)values, gathered, idx[cur], n,
-                       vs);
-    if (hipMemcpyAsync(values, gathered, (size_t)n * vs, hipMemcpyDeviceToDevice, s) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_sort_gather, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg, idx[cur]);
+    hipLaunchKernelGGL(k_sort_copyback, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

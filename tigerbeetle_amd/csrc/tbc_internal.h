@@ -131,7 +131,10 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint
                   void (*mark)(void *, const char *), void *mark_ctx);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
-int launch_sort(uint32_t key_kind, uint32_t value_size, uint32_t timestamp_offset, void *values, uint32_t n,
-                void *scratch, uint64_t scratch_bytes, void *stream);
-uint64_t sort_scratch_bytes(uint32_t value_size, uint32_t n);
+struct SortItem {
+    void *values;
+    uint32_t n, value_size, timestamp_offset, key_kind;
+};
+int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *stream);
+uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count);
 } // namespace tbc

@@ -219,6 +219,20 @@ class Engine:
         f = lib().tbc_sort_values if sync else lib().tbc_sort_values_async
         check(f(self.handle, ctypes.byref(t), buf.ptr, count), "tbc_sort_values")
 
+    def copy_device_async(self, dst: int, src: int, nbytes: int) -> None:
+        check(lib().tbc_copy_device_async(self.handle, dst, src, nbytes), "tbc_copy_device_async")
+
+    def sort_values_batch(self, tables: list) -> None:
+        """Bar end: [(TreeSpec, DeviceBuffer | device ptr, count)] sorted by one
+        segmented launch sequence (tbc_sort_values_batch), enqueued on the
+        engine stream."""
+        arr = (abi.SortJob * max(1, len(tables)))()
+        for i, (tree, buf, n) in enumerate(tables):
+            arr[i].tree = tree.ctype()
+            arr[i].values = buf if isinstance(buf, int) else buf.ptr
+            arr[i].count = n
+        check(lib().tbc_sort_values_batch(self.handle, arr, len(tables)), "tbc_sort_values_batch")
+
     def prepare(self, jobs: list):
         """The tbc_compaction[] array of a job list (cached for a repeated list)."""
         key = tuple(id(j) for j in jobs)
