@@ -165,6 +165,7 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
 
 # bench kernel label -> rocprofv3 kernel symbol (tools/traffic.py short names)
 KERNEL_SYMBOL = {"merge_partition": "k_partition", "merge": "k_merge_tile", "data_blocks": "k_data_blocks",
+                 "assemble": "k_assemble",
                  "index_blocks": "k_index_blocks"}
 
 
@@ -274,8 +275,11 @@ def main() -> None:
         "merge_partition": len(wl.jobs) * 2400 * 2 * 21 * 32,
         "merge": R,  # read every input value once (keys decide; 2 mask bits per position written)
         "data_blocks": out_values + W_data,  # read every survivor once, write the blocks
+        "assemble": 2 * out_values,  # two-pass regime: gather survivors into the bodies
         "index_blocks": W_index + data_blocks * 64,
     }
+    if "assemble" in per_step:  # two-pass regime: the chains read the assembled bodies and write headers
+        alg_bytes["data_blocks"] = out_values + data_blocks * 256
     kt_us = per_step[dominant]
     achieved = alg_bytes.get(dominant, R) / (kt_us * 1e-6) / 1e9
     job_bytes = R + W_data + W_index + wl.sort_bytes  # R + W (+ S)

@@ -221,3 +221,23 @@ def test_sort_values_batch_of_memtables(engine, oracle_lib):
     for (spec, buf, n), want in zip(tables, wants):
         got = buf.download(n * spec.value_size).reshape(n, spec.value_size)
         assert np.array_equal(got, want), spec.name
+
+
+def test_compaction_parity_throughput_regime(engine_small, oracle_lib):
+    """More than 4,096 output data blocks in one batch switch the engine to
+    its two-pass path (k_assemble, then chain-only k_data_blocks at 4 chains
+    per SIMD); 4 KiB blocks reach that with small inputs."""
+    bs = 4096
+    T = trees.BY_NAME
+    cases = []
+    for i, name in enumerate(["transfers.id", "accounts.timestamp", "transfers.debit_account_id", "accounts.ledger",
+                              "posted.timestamp", "transfers.id", "account_history.timestamp", "transfers.amount"]):
+        base = T[name]
+        spec = trees.with_table_size(base, 6 * (bs - 256) // base.value_size + 1)
+        n = 125 * (bs - 256) // base.value_size  # 125 blocks of A, 4.5x that in all
+        cases.append((spec, dict(n_a=n, b_table_sizes=[n // 2] * 7, a_immutable=i % 2 == 1, dup_frac=0.1 * (i % 2),
+                                 tomb_frac=0.05 * (i % 3 != 2), drop_tombstones=i % 4 == 3, overlap=0.2)))
+    # the batch must exceed the fused limit (2,048 chain waves = 4,096 blocks)
+    total_blocks = sum(workloads.worst_case_blocks(s, kw["n_a"] * 9 // 2, bs) for s, kw in cases)
+    assert total_blocks > 4096, total_blocks
+    _compare(oracle_lib, engine_small, cases, bs)

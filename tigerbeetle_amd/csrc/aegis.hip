@@ -664,14 +664,26 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
 // Config 2's 2,016 blocks need 1,008 chain waves: one per SIMD. A group
 // whose block does not exist (dedup left fewer blocks than the bound) mirrors
 // its partner's block without writing, so all its loads stay valid.
+//
+// Throughput regime (many more blocks than SIMDs, e.g. config 5's 13,824
+// blocks): `Fused = false`. The bodies are first assembled by k_assemble (one
+// wave per block, every CU, no LDS tables: HBM-bound), then this kernel runs
+// chain waves only, up to 16 per workgroup (4 per SIMD), so the AES rounds of
+// four waves hide each other's LDS latency instead of one chain per SIMD
+// waiting on it.
 constexpr uint32_t kMaxChainWaves = 5;
+constexpr uint32_t kMaxChainOnlyWaves = 16;
+// Above this many chain waves (2 per SIMD) the two-pass path wins.
+constexpr uint32_t kFusedMaxChainWaves = 2048;
 
+template <bool Fused>
 __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
                                                       const JobResultDev *res, const uint64_t *status,
                                                       const uint64_t *masks, const uint32_t *block_tile,
                                                       const SplitDesc *splits, uint32_t chain_waves) {
+    constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
     __shared__ uint32_t sT[kTableDwords];
-    __shared__ uint32_t sHdr[kMaxChainWaves][2][64];
+    __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
     load_tables(sT);
     if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = 0;
@@ -691,7 +703,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
     };
     int ji;
     uint32_t k;
-    if (wave_in_block >= C) { // producer
+    if (Fused && wave_in_block >= C) { // producer
         const uint32_t p = wave_in_block - C;
         const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
         if (!locate(mine, ji, k)) return;
@@ -717,9 +729,19 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
     const uint32_t slot = data_block_slot(k, j.dbcm);
     uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
 
-    BodyMsg body(blk + kHeaderSize, cnt * j.value_size, &sProg[2 * wave_in_block + src_half],
-                 const_cast<uint32_t *>(&res[j.job_index].invariant));
-    const uint32_t body_tag = aegis_mac32(sT, body);
+    uint32_t body_tag;
+    if constexpr (Fused) {
+        BodyMsg body(blk + kHeaderSize, cnt * j.value_size, &sProg[2 * wave_in_block + src_half],
+                     const_cast<uint32_t *>(&res[j.job_index].invariant));
+        body_tag = aegis_mac32(sT, body);
+    } else {
+        (void)src_half;
+        // Four chains per SIMD are VALU-issue-bound, not latency-bound: take
+        // the round key with one ds_bpermute (LDS pipe) instead of the six
+        // VALU lane moves that win when a chain waits alone on LDS latency.
+        GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
+        body_tag = aegis_mac32<GlobalMsg, StepBpermute>(sT, body);
+    }
 
     HeaderFields h;
     h.cluster_lo = j.cluster_lo;
@@ -744,6 +766,90 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
         // Zero [size, sector_ceil(size)) (grid.zig:686).
         const uint32_t end = (uint32_t)sector_ceil(size);
         for (uint32_t o = size + 4 * g; o < end; o += 128) gst<uint32_t>(blk + o, 0u);
+    }
+}
+
+// Throughput regime, pass 1: assemble every data block body from the merge's
+// masks, parallel over merge positions (not sequential per block like the
+// fused path's producers): one workgroup per merge tile; the tile's output
+// offset (k_tile_scan) and A/B cursors (merge-path split) plus per-mask-word
+// prefix counts give every survivor its source value and output slot; each
+// wave then copies its word's survivors cooperatively, 16 bytes per lane, so
+// consecutive lanes read and write consecutive bytes. HBM-bound: every
+// survivor is read once and written once.
+__global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs, uint32_t total_tiles,
+                                                  const uint64_t *status, const uint64_t *masks,
+                                                  const SplitDesc *splits) {
+    constexpr uint32_t W = kMergeTile / 64; // mask words per kind per tile
+    __shared__ uint32_t s_pre[3][W + 1];    // survivors, A taken, B taken before word w
+    __shared__ uint64_t s_src[4][64], s_dst[4][64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1;
+    for (uint32_t g = blockIdx.x; g < total_tiles; g += gridDim.x) {
+        const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.tile_base; });
+        const JobDesc &j = jobs[ji];
+        const uint32_t t = g - j.tile_base;
+        const uint32_t n = j.a.n + j.b.n, vs = j.value_size, vcm = j.vcm;
+        const uint64_t *m = masks + (size_t)g * (2 * W);
+        const SplitDesc sp = splits[j.split_base + t];
+        const uint32_t out0 = (uint32_t)(gld<uint64_t>(status + g) >> 32);
+        const uint32_t a0 = sp.i, b0 = t * kMergeTile - sp.i;
+        auto valid_of = [&](uint32_t w) -> uint64_t {
+            const uint32_t pos0 = t * kMergeTile + 64 * w;
+            return pos0 >= n ? 0ull : (n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1));
+        };
+        __syncthreads(); // the previous tile's readers of s_pre are done
+        if (tid < W) {
+            const uint64_t sm = gld<uint64_t>(m + tid), am = gld<uint64_t>(m + W + tid);
+            s_pre[0][tid + 1] = __builtin_popcountll(sm);
+            s_pre[1][tid + 1] = __builtin_popcountll(am);
+            s_pre[2][tid + 1] = __builtin_popcountll(valid_of(tid) & ~am);
+        }
+        __syncthreads();
+        if (tid < 3) {
+            uint32_t acc = 0;
+            s_pre[tid][0] = 0;
+            for (uint32_t w = 1; w <= W; w++) {
+                acc += s_pre[tid][w];
+                s_pre[tid][w] = acc;
+            }
+        }
+        __syncthreads();
+        SegCursor ca, cb;
+        ca.init(j.a, sp.seg_a);
+        cb.init(j.b, sp.seg_b);
+        const uint32_t cpv_log = __builtin_ctz(vs >> 4);
+        for (uint32_t w = wv; w < W; w += 4) {
+            if (t * kMergeTile + 64 * w >= n) break;
+            const uint64_t sm = gld<uint64_t>(m + w), am = gld<uint64_t>(m + W + w);
+            const uint32_t ns = __builtin_popcountll(sm);
+            if (ns == 0) continue;
+            const uint64_t valid = valid_of(w);
+            const uint32_t ab = a0 + s_pre[1][w], bb = b0 + s_pre[2][w];
+            ca.advance(ab);
+            cb.advance(bb);
+            if ((sm >> lane) & 1) {
+                const uint32_t r = __builtin_popcountll(sm & lt);
+                const uint32_t o = out0 + s_pre[0][w] + r;
+                const uint8_t *src = ((am >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(am & lt), vs)
+                                                        : cb.elem(bb + __builtin_popcountll(valid & ~am & lt), vs);
+                const uint32_t k = o / vcm;
+                uint8_t *dst = j.out_blocks + (size_t)data_block_slot(k, j.dbcm) * j.block_size + kHeaderSize +
+                               (size_t)(o - k * vcm) * vs;
+                s_src[wv][r] = (uint64_t)(uintptr_t)src;
+                s_dst[wv][r] = (uint64_t)(uintptr_t)dst;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (uint32_t c = lane; c < (ns << cpv_log); c += 64) {
+                const uint32_t e = c >> cpv_log, q = c & ((1u << cpv_log) - 1);
+                const uint8_t *src = (const uint8_t *)(uintptr_t)s_src[wv][e];
+                uint8_t *dst = (uint8_t *)(uintptr_t)s_dst[wv][e];
+                gst<u32x4>(dst + 16 * q, gld<u32x4>(src + 16 * q));
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
     }
 }
 
@@ -864,16 +970,32 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
+int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
-    if (total_dblocks) {
-        const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
+    const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
+    if (total_dblocks && waves <= kFusedMaxChainWaves) {
+        // Latency regime: every chain is in flight at once; producers fill
+        // the bodies while the chains absorb them.
         uint32_t c = waves_per_block(waves);
         c = c > kMaxChainWaves ? kMaxChainWaves : c;
-        hipLaunchKernelGGL(k_data_blocks, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
+        hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
+                           total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
+                           c);
+        if (hipGetLastError() != hipSuccess) return -1;
+    } else if (total_dblocks) {
+        // Throughput regime: assemble all bodies, then chains at 4 per SIMD,
+        // spread evenly over the 256 CUs' rounds.
+        const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+        hipLaunchKernelGGL(k_assemble, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status, d_masks,
+                           d_splits);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (mark) mark(mark_ctx, "assemble");
+        const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
+        const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
+        hipLaunchKernelGGL(k_data_blocks<false>, dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs, njobs,
                            total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
                            c);
         if (hipGetLastError() != hipSuccess) return -1;

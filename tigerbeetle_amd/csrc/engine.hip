@@ -535,7 +535,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile,
                           d_order, d_res, s, mark_cb, b) == 0;
     if (ok && count)
-        ok = launch_blocks((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status, e->masks,
+        ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_res, d_infos, d_status, e->masks,
                            d_block_tile, d_splits, s, mark_cb, b) == 0;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipEventRecord(b->done, s) == hipSuccess;
