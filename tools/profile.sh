@@ -19,3 +19,8 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/write.log 2>&1
 md5sum tigerbeetle_amd/libtbc.so > $OUT/lib.md5
 echo PROFILE_OK
+# Kernel traces of the other BASELINE configs (no PMC passes).
+for c in $EXTRA_CONFIGS; do
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_c$c -o run -- python3 -u bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline > $OUT/trace_c$c.log 2>&1
+done
+echo PROFILE_EXTRA_OK
