@@ -12,7 +12,8 @@
 // probe pass computes OR/AND of all keys and the sortedness flag), then one
 // gather of the Values by original index. Per pass:
 //   hist    — per-tile digit counts (16 bins x tiles, digit-major);
-//   scan    — exclusive scan of the digit-major counts (one workgroup);
+//   scan    — exclusive scan of the [table][digit][tile] counts (chunk sums,
+//             their scan, chunk rescans: three short coalesced launches);
 //   scatter — each tile is staged through LDS so every thread owns 8
 //             consecutive items, per-thread digit counts are scanned across
 //             the tile in digit-major order, and items are written to
@@ -36,6 +37,10 @@ struct SortProbe {
     uint64_t or_[4];
     uint64_t and_[4];
 };
+// Workgroups fold their OR/AND into one of kProbeBuckets probes (one hot
+// address per limb serialised thousands of atomics in L2); the host folds
+// the buckets.
+constexpr uint32_t kProbeBuckets = 64;
 
 // One memtable of the batch. Items of all segments live in one global item
 // space (segment s at [item_base, item_base + n)); tiles never straddle a
@@ -45,7 +50,7 @@ struct SortProbe {
 // no segment digit).
 struct SortSeg {
     uint8_t *values;
-    uint8_t *scratch; // n * vs bytes: gather target, copied back
+    uint8_t *scratch; // n * vs bytes: the unsorted table, the gather's source
     uint32_t n, vs, ts_off, kind;
     uint32_t item_base, tile_base, tiles, unsorted;
 };
@@ -76,10 +81,20 @@ __global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint3
     uint32_t uns = 0;
     for (uint32_t r = 0; r < kSortPer; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-        if (li >= S.n) break;
+        if (lt * kSortTile + r * kSortThreads >= S.n) break; // wave-uniform (whole row past the end)
+        const bool in = li < S.n;
         const uint32_t i = S.item_base + li;
-        uint64_t k[3], kn[3];
-        key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
+        uint64_t k[3] = {0, 0, 0}, kn[3];
+        if (in) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
+        // The next item's key comes from the next lane (one value read per
+        // item); lane 63 reads its neighbour itself.
+        for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
+        if (lane == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
+        if (!in) continue;
+        // Stage the value in the table's scratch (the gather reads from there
+        // and writes the table in place: no copy-back pass).
+        for (uint32_t q = 0; q < S.vs; q += 16)
+            gst<u32x4>(S.scratch + (size_t)li * S.vs + q, gld<u32x4>(S.values + (size_t)li * S.vs + q));
         for (uint32_t l = 0; l < kl; l++) {
             keys[(size_t)l * N + i] = k[l];
             o[l] |= k[l];
@@ -87,7 +102,6 @@ __global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint3
         }
         idx[i] = i;
         if (li + 1 < S.n) {
-            key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
             bool gt = false, decided = false;
             for (int l = (int)kl - 1; l >= 0 && !decided; l--) {
                 if (k[l] != kn[l]) {
@@ -118,8 +132,9 @@ __global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint3
                 oo |= s_or[l][w];
                 aa &= s_and[l][w];
             }
-            atomicOr((unsigned long long *)&probe->or_[l], (unsigned long long)oo);
-            atomicAnd((unsigned long long *)&probe->and_[l], (unsigned long long)aa);
+            SortProbe *pb = probe + (blockIdx.x % kProbeBuckets);
+            atomicOr((unsigned long long *)&pb->or_[l], (unsigned long long)oo);
+            atomicAnd((unsigned long long *)&pb->and_[l], (unsigned long long)aa);
         }
         if (s_uns) atomicOr(&segs[sg].unsorted, 1u);
     }
@@ -149,30 +164,71 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_hist(const SortSeg *segs,
     if (tid < kBins) hist[hist_slot(S, tid, lt)] = cnt[tid];
 }
 
-// Exclusive scan of m entries in place (one workgroup).
-__global__ __launch_bounds__(1024) void k_sort_scan(uint32_t *hist, uint32_t m) {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry;
+// Exclusive scan of the m histogram entries in place, in three short
+// launches (all loads coalesced): per-chunk sums, a scan of the chunk sums,
+// then every chunk rescanned with its offset. kScanChunk entries per chunk.
+constexpr uint32_t kScanChunk = 2048;
+
+__device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t *wsum, uint32_t &total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) carry = 0;
+    uint32_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    for (uint32_t base = 0; base < m; base += 1024) {
-        const uint32_t i = base + tid;
-        const uint32_t v = i < m ? hist[i] : 0;
-        uint32_t incl = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= (uint32_t)o) incl += y;
-        }
-        if (lane == 63) wsum[wave] = incl;
-        __syncthreads();
-        uint32_t woff = 0;
-        for (uint32_t w = 0; w < wave; w++) woff += wsum[w];
-        const uint32_t c0 = carry;
-        if (i < m) hist[i] = c0 + woff + incl - v;
-        __syncthreads();
-        if (tid == 1023) carry = c0 + woff + incl;
-        __syncthreads();
+    uint32_t off = 0;
+    total = 0;
+    for (uint32_t w = 0; w < 4; w++) {
+        off += w < wave ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    __syncthreads();
+    return off + incl - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *hist, uint32_t m, uint32_t *chunk_sums) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t base = blockIdx.x * kScanChunk;
+    uint32_t sum = 0;
+    for (uint32_t k = threadIdx.x; k < kScanChunk; k += 256)
+        sum += base + k < m ? hist[base + k] : 0u;
+    uint32_t total;
+    block_excl_scan_256(sum, wsum, total);
+    if (threadIdx.x == 0) chunk_sums[blockIdx.x] = total;
+}
+
+// One workgroup: exclusive scan of the chunk sums in place.
+__global__ __launch_bounds__(256) void k_scan_top(uint32_t *chunk_sums, uint32_t chunks) {
+    __shared__ uint32_t wsum[4];
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < chunks; b += 256) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = i < chunks ? chunk_sums[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan_256(v, wsum, total);
+        if (i < chunks) chunk_sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+// Each thread owns 8 consecutive entries of the chunk (loaded as 2 x 16 B).
+__global__ __launch_bounds__(256) void k_scan_apply(uint32_t *hist, uint32_t m, const uint32_t *chunk_sums) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * 8;
+    uint32_t v[8], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        v[k] = base + k < m ? hist[base + k] : 0u;
+        sum += v[k];
+    }
+    uint32_t total;
+    uint32_t run = chunk_sums[blockIdx.x] + block_excl_scan_256(sum, wsum, total);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        if (base + k < m) hist[base + k] = run;
+        run += v[k];
     }
 }
 
@@ -184,6 +240,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *se
     __shared__ uint64_t s_key[KL][kSortTile];
     __shared__ uint32_t s_idx[kSortTile];
     __shared__ uint32_t s_cnt[kBins][kSortThreads + 1]; // digit-major per-thread counts
+    __shared__ uint32_t s_tot[kBins], s_dstart[kBins], s_gbase[kBins];
+    __shared__ uint16_t s_perm[kSortTile]; // tile position in digit order -> item
     const uint32_t tid = threadIdx.x;
     const SortSeg S = segs[tile_seg[blockIdx.x]];
     const uint32_t lt = blockIdx.x - S.tile_base;
@@ -229,29 +287,49 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *se
                 s_cnt[d][b0 + lane] = carry + incl - v;
                 carry += __shfl(incl, 63, 64);
             }
+            if (lane == 0) s_tot[d] = carry;
         }
     }
     __syncthreads();
+    if (tid < kBins) s_gbase[tid] = hist[hist_slot(S, tid, lt)];
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t d = 0; d < kBins; d++) {
+            s_dstart[d] = acc;
+            acc += s_tot[d];
+        }
+    }
+    __syncthreads();
+    // Rank every item inside the tile in digit order (stable: thread order,
+    // then item order within the thread) ...
     uint32_t run[kBins];
 #pragma unroll
-    for (uint32_t d = 0; d < kBins; d++) run[d] = hist[hist_slot(S, d, lt)] + s_cnt[d][tid];
+    for (uint32_t d = 0; d < kBins; d++) run[d] = s_dstart[d] + s_cnt[d][tid];
 #pragma unroll
     for (uint32_t k = 0; k < kSortPer; k++) {
-        const uint32_t e = tid * kSortPer + k;
         if (dig[k] < kBins) {
-            uint32_t dst = 0;
+            uint32_t loc = 0;
 #pragma unroll
             for (uint32_t d = 0; d < kBins; d++)
-                if (dig[k] == d) dst = run[d]++;
-#pragma unroll
-            for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)l * N + dst, s_key[l][e]);
-            gst<uint32_t>(idx_out + dst, s_idx[e]);
+                if (dig[k] == d) loc = run[d]++;
+            s_perm[loc] = (uint16_t)(tid * kSortPer + k);
         }
+    }
+    __syncthreads();
+    // ... then write the tile out in that order: consecutive threads write
+    // consecutive destinations inside each digit's run (coalesced).
+    for (uint32_t i = tid; i < m; i += kSortThreads) {
+        const uint32_t e = s_perm[i];
+        const uint32_t d = (uint32_t)(s_key[limb][e] >> shift) & (kBins - 1);
+        const uint32_t dst = s_gbase[d] + (i - s_dstart[d]);
+#pragma unroll
+        for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)l * N + dst, s_key[l][e]);
+        gst<uint32_t>(idx_out + dst, s_idx[e]);
     }
 }
 
-// scratch[i] = values[idx[i]] (segment-local), 16 bytes per lane; sorted
-// segments are left alone.
+// values[i] = scratch[idx[i]] (segment-local; scratch holds the unsorted
+// table), 16 bytes per lane; sorted tables are left alone.
 __global__ __launch_bounds__(256) void k_sort_gather(const SortSeg *segs, const uint32_t *tile_seg,
                                                      const uint32_t *idx) {
     const SortSeg S = segs[tile_seg[blockIdx.x]];
@@ -263,21 +341,9 @@ __global__ __launch_bounds__(256) void k_sort_gather(const SortSeg *segs, const 
     for (uint32_t c = threadIdx.x; c < m * cpv; c += 256) {
         const uint32_t e = c / cpv, part = c % cpv;
         const uint32_t src = gld<uint32_t>(idx + S.item_base + first + e) - S.item_base;
-        gst<u32x4>(S.scratch + (size_t)(first + e) * S.vs + 16 * part,
-                   gld<u32x4>(S.values + (size_t)src * S.vs + 16 * part));
+        gst<u32x4>(S.values + (size_t)(first + e) * S.vs + 16 * part,
+                   gld<u32x4>(S.scratch + (size_t)src * S.vs + 16 * part));
     }
-}
-
-__global__ __launch_bounds__(256) void k_sort_copyback(const SortSeg *segs, const uint32_t *tile_seg) {
-    const SortSeg S = segs[tile_seg[blockIdx.x]];
-    if (!S.unsorted) return;
-    const uint32_t lt = blockIdx.x - S.tile_base;
-    const uint32_t first = lt * kSortTile;
-    const uint32_t m = (S.n - first) < kSortTile ? (S.n - first) : kSortTile;
-    const uint32_t chunks = m * (S.vs >> 4);
-    const size_t off = (size_t)first * S.vs;
-    for (uint32_t c = threadIdx.x; c < chunks; c += 256)
-        gst<u32x4>(S.values + off + 16 * (size_t)c, gld<u32x4>(S.scratch + off + 16 * (size_t)c));
 }
 
 static uint32_t key_limbs(uint32_t kind) {
@@ -294,11 +360,12 @@ uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count) {
         tiles += tiles_of(items[j].n);
         vals += ((uint64_t)items[j].n * items[j].value_size + 255) / 256 * 256;
     }
-    return 256                                          // probe
+    return sizeof(SortProbe) * kProbeBuckets           // probes
            + ((uint64_t)sizeof(SortSeg) * count + 255) / 256 * 256
            + (4 * tiles + 255) / 256 * 256              // tile -> segment
            + 2 * ((N * 3 * 8) + (N * 4 + 255) / 256 * 256) // two item buffers
            + (4 * kBins * tiles + 255) / 256 * 256      // histogram
+           + (4 * (kBins * tiles / kScanChunk + 1) + 255) / 256 * 256 // scan chunk sums
            + vals;                                      // gathered values
 }
 
@@ -330,7 +397,7 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     const uint32_t nseg = (uint32_t)segs.size(), ntiles = (uint32_t)tile_seg.size();
     uint8_t *p = (uint8_t *)scratch;
     SortProbe *probe = (SortProbe *)p;
-    p += 256;
+    p += sizeof(SortProbe) * kProbeBuckets;
     SortSeg *d_segs = (SortSeg *)p;
     p += ((uint64_t)sizeof(SortSeg) * count + 255) / 256 * 256;
     uint32_t *d_tile_seg = (uint32_t *)p;
@@ -345,6 +412,8 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     }
     uint32_t *hist = (uint32_t *)p;
     p += ((uint64_t)4 * kBins * ntiles + 255) / 256 * 256;
+    uint32_t *chunk_sums = (uint32_t *)p;
+    p += ((uint64_t)4 * (kBins * ntiles / kScanChunk + 1) + 255) / 256 * 256;
     for (SortSeg &g : segs) {
         g.scratch = p;
         p += ((uint64_t)g.n * g.vs + 255) / 256 * 256;
@@ -352,9 +421,11 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
 
     // The plan is staged through static host memory owned by the caller's
     // stream order: copy it synchronously with the probe read below.
-    SortProbe init{};
-    for (int l = 0; l < 4; l++) init.and_[l] = ~0ull;
-    if (hipMemcpyAsync(probe, &init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess ||
+    std::vector<SortProbe> init(kProbeBuckets);
+    for (SortProbe &pr : init)
+        for (int l = 0; l < 4; l++) pr.or_[l] = 0, pr.and_[l] = ~0ull;
+    if (hipMemcpyAsync(probe, init.data(), sizeof(SortProbe) * kProbeBuckets, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
         hipMemcpyAsync(d_segs, segs.data(), sizeof(SortSeg) * nseg, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d_tile_seg, tile_seg.data(), 4ull * ntiles, hipMemcpyHostToDevice, s) != hipSuccess)
         return -1;
@@ -362,12 +433,16 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
                        probe);
     // The digit plan needs the probe on the host (one small synchronous read
     // per batch, not per memtable).
-    SortProbe host{};
+    std::vector<SortProbe> buckets(kProbeBuckets);
     std::vector<SortSeg> hsegs(nseg);
-    if (hipMemcpyAsync(&host, probe, sizeof host, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(buckets.data(), probe, sizeof(SortProbe) * kProbeBuckets, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
         hipMemcpyAsync(hsegs.data(), d_segs, sizeof(SortSeg) * nseg, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -1;
+    SortProbe host = buckets[0];
+    for (const SortProbe &pr : buckets)
+        for (int l = 0; l < 4; l++) host.or_[l] |= pr.or_[l], host.and_[l] &= pr.and_[l];
     bool any = false;
     for (const SortSeg &g : hsegs) any |= g.unsorted != 0;
     if (!any) return 0; // table_memory.zig:141: already sorted, no-op
@@ -378,7 +453,10 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
             if (((varies >> shift) & (kBins - 1)) == 0) continue; // constant digit: order unchanged
             hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg, keys[cur],
                                N, limb, shift, hist);
-            hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, kBins * ntiles);
+            const uint32_t m = kBins * ntiles, chunks = (m + kScanChunk - 1) / kScanChunk;
+            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(256), 0, s, hist, m, chunk_sums);
+            hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, chunk_sums, chunks);
+            hipLaunchKernelGGL(k_scan_apply, dim3(chunks), dim3(256), 0, s, hist, m, chunk_sums);
             switch (kl) {
             case 1:
                 hipLaunchKernelGGL(k_sort_scatter<1>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
@@ -397,7 +475,6 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         }
     }
     hipLaunchKernelGGL(k_sort_gather, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg, idx[cur]);
-    hipLaunchKernelGGL(k_sort_copyback, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
