@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *se
         const uint32_t e = r * kSortThreads + tid;
         if (e < m) {
 #pragma unroll
-            for (int l = 0; l < KL; l++) s_key[l][e] = gld<uint64_t>(keys_in + (size_t)l * N + base + e);
+            for (int l = 0; l < KL; l++) s_key[l][e] = gld<uint64_t>(keys_in + (size_t)(limb + l) * N + base + e);
             s_idx[e] = gld<uint32_t>(idx_in + base + e);
         }
     }
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *se
 #pragma unroll
     for (uint32_t k = 0; k < kSortPer; k++) {
         const uint32_t e = tid * kSortPer + k;
-        dig[k] = e < m ? (uint32_t)(s_key[limb][e] >> shift) & (kBins - 1) : kBins; // kBins = none
+        dig[k] = e < m ? (uint32_t)(s_key[0][e] >> shift) & (kBins - 1) : kBins; // kBins = none
 #pragma unroll
         for (uint32_t d = 0; d < kBins; d++) c[d] += dig[k] == d ? 1u : 0u;
     }
@@ -320,10 +320,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *se
     // consecutive destinations inside each digit's run (coalesced).
     for (uint32_t i = tid; i < m; i += kSortThreads) {
         const uint32_t e = s_perm[i];
-        const uint32_t d = (uint32_t)(s_key[limb][e] >> shift) & (kBins - 1);
+        const uint32_t d = (uint32_t)(s_key[0][e] >> shift) & (kBins - 1);
         const uint32_t dst = s_gbase[d] + (i - s_dstart[d]);
 #pragma unroll
-        for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)l * N + dst, s_key[l][e]);
+        for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)(limb + l) * N + dst, s_key[l][e]);
         gst<uint32_t>(idx_out + dst, s_idx[e]);
     }
 }
@@ -447,8 +447,14 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     for (const SortSeg &g : hsegs) any |= g.unsorted != 0;
     if (!any) return 0; // table_memory.zig:141: already sorted, no-op
     int cur = 0;
-    for (uint32_t limb = 0; limb < kl; limb++) {
+    // LSD passes carry only the limbs still to be sorted on: limbs below the
+    // current one are final, limbs above the highest varying one are constant.
+    uint32_t hi = 0;
+    for (uint32_t limb = 0; limb < kl; limb++)
+        if (host.or_[limb] ^ host.and_[limb]) hi = limb + 1;
+    for (uint32_t limb = 0; limb < hi; limb++) {
         const uint64_t varies = host.or_[limb] ^ host.and_[limb];
+        const uint32_t live = hi - limb; // limbs [limb, hi) move with the items
         for (uint32_t shift = 0; shift < 64; shift += kDigitBits) {
             if (((varies >> shift) & (kBins - 1)) == 0) continue; // constant digit: order unchanged
             hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg, keys[cur],
@@ -457,7 +463,7 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
             hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(256), 0, s, hist, m, chunk_sums);
             hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, chunk_sums, chunks);
             hipLaunchKernelGGL(k_scan_apply, dim3(chunks), dim3(256), 0, s, hist, m, chunk_sums);
-            switch (kl) {
+            switch (live) {
             case 1:
                 hipLaunchKernelGGL(k_sort_scatter<1>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
                                    keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
