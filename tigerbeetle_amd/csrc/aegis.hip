@@ -12,9 +12,10 @@
 //     the quad with DPP quad_perm (MixColumns/ShiftRows), no VGPR tables;
 //   * AEGIS' block rotation S'[i] = AESRound(S[i-1]) ^ S[i] is turned into a
 //     label rotation: quad p keeps its register and becomes block label+1,
-//     so the only cross-quad move is the round key S[label+1], fetched with
-//     ds_bpermute at the start of the step — off the dependency chain;
-//   * message words are prefetched a 1 KiB group (32 updates) ahead.
+//     so the only cross-quad move is the round key S[label+1], fetched off
+//     the dependency chain (DPP row_ror + permlane16_swap when a chain runs
+//     alone per SIMD, one ds_bpermute when four chains share a SIMD);
+//   * message words are prefetched a whole group (64 updates) ahead.
 //
 // Block finishing (Table.Builder.data_block_finish / index_block_finish,
 // src/lsm/table.zig:306-457) is fused here: body assembly (producer waves
@@ -680,7 +681,8 @@ template <bool Fused>
 __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
                                                       const JobResultDev *res, const uint64_t *status,
                                                       const uint64_t *masks, const uint32_t *block_tile,
-                                                      const SplitDesc *splits, uint32_t chain_waves) {
+                                                      const SplitDesc *splits, uint32_t chain_waves,
+                                                      const uint32_t *ready) {
     constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
@@ -739,6 +741,10 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
         // Four chains per SIMD are VALU-issue-bound, not latency-bound: take
         // the round key with one ds_bpermute (LDS pipe) instead of the six
         // VALU lane moves that win when a chain waits alone on LDS latency.
+        // k_assemble ran before this kernel (stream order): every survivor of
+        // the block must have landed.
+        if (__hip_atomic_load(ready + j.dblock_base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
+            gst<uint32_t>(const_cast<uint32_t *>(&res[j.job_index].invariant), 0xdeafu);
         GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
         body_tag = aegis_mac32<GlobalMsg, StepBpermute>(sT, body);
     }
@@ -779,7 +785,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
 // survivor is read once and written once.
 __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs, uint32_t total_tiles,
                                                   const uint64_t *status, const uint64_t *masks,
-                                                  const SplitDesc *splits) {
+                                                  const SplitDesc *splits, uint32_t *ready) {
     constexpr uint32_t W = kMergeTile / 64; // mask words per kind per tile
     __shared__ uint32_t s_pre[3][W + 1];    // survivors, A taken, B taken before word w
     __shared__ uint64_t s_src[4][64], s_dst[4][64];
@@ -849,6 +855,22 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        // Count the survivors landed in every data block (checked by the
+        // chain kernel before it checksums the block).
+        // (No release fence: the reader is the next kernel in stream order, and
+        // an agent-scope release writes back the XCD's L2 — per tile, that
+        // quadrupled this kernel's time.)
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t cnt = s_pre[0][W];
+            uint32_t o = out0;
+            while (o < out0 + cnt) {
+                const uint32_t k = o / vcm;
+                const uint32_t e = (k + 1) * vcm < out0 + cnt ? (k + 1) * vcm : out0 + cnt;
+                __hip_atomic_fetch_add(ready + j.dblock_base + k, e - o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                o = e;
+            }
         }
     }
 }
@@ -971,6 +993,7 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
 }
 
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
+                  uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx) {
@@ -983,21 +1006,25 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         c = c > kMaxChainWaves ? kMaxChainWaves : c;
         hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
                            total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
-                           c);
+                           c, (const uint32_t *)d_ready);
         if (hipGetLastError() != hipSuccess) return -1;
     } else if (total_dblocks) {
-        // Throughput regime: assemble all bodies, then chains at 4 per SIMD,
-        // spread evenly over the 256 CUs' rounds.
+        // Throughput regime: assemble every body, then the chains, 4 per SIMD.
+        // (Running k_assemble concurrently on a second stream, chains waiting
+        // on the per-block counts, measured 2.2x SLOWER for config 5: the
+        // chain workgroups leave the assemble waves too little of each CU.)
+        // The counts stay as a check: a chain whose block is short of values
+        // reports an invariant error instead of checksumming a partial body.
         const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
         hipLaunchKernelGGL(k_assemble, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status, d_masks,
-                           d_splits);
+                           d_splits, d_ready);
         if (hipGetLastError() != hipSuccess) return -1;
         if (mark) mark(mark_ctx, "assemble");
         const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
         const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
         hipLaunchKernelGGL(k_data_blocks<false>, dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs, njobs,
                            total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
-                           c);
+                           c, (const uint32_t *)d_ready);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "data_blocks");

@@ -432,7 +432,8 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     const uint64_t sz_order = align_up(sizeof(TileRef) * (uint64_t)tiles, 256);
     const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order;
     const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
-    const uint64_t sz_tiles = align_up(8ull * tiles + 4ull * dblocks + 8, 256); // tile status + block_tile
+    // tile status + block_tile + per-block assembled-value counts (throughput regime)
+    const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8, 256);
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
     b->dev_top = e->dev.top;
@@ -451,6 +452,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
     uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
     uint32_t *d_block_tile = (uint32_t *)(d_status + tiles);
+    uint32_t *d_ready = d_block_tile + dblocks;
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
     b->h_results = (JobResultDev *)(hbase + sz_in);
@@ -535,7 +537,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile,
                           d_order, d_res, s, mark_cb, b) == 0;
     if (ok && count)
-        ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_res, d_infos, d_status, e->masks,
+        ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
                            d_block_tile, d_splits, s, mark_cb, b) == 0;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipEventRecord(b->done, s) == hipSuccess;
