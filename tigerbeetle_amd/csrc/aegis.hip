@@ -875,17 +875,28 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
     }
 }
 
+// LDS ordering among the lanes of one wave (the only wave left running).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Index blocks: index_block_finish (table.zig:403-457) + the TableInfo
 // manifest entry (manifest.zig:121-149, schema.zig:489-509). One table per
 // wave (both groups compute it; the lower group writes).
 constexpr uint32_t kIndexLdsBytes = 16384;
 
-__global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
+__global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
                                                      uint8_t *infos) {
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sIdx[kIndexLdsBytes / 4];
     __shared__ uint64_t sKeys[2][4];
+    // Sixteen waves load the 128 KiB of replicated tables (one wave alone spent
+    // ~50 us on it); wave 0 then builds the table's index block.
     load_tables(sT);
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
     const uint32_t wave = blockIdx.x;
     const int ji = find_job(jobs, njobs, wave, [](const JobDesc &d) { return d.table_base; });
     const JobDesc &j = jobs[ji];
@@ -901,7 +912,7 @@ __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int nj
     const uint32_t ks = j.key_size;
     uint8_t *idx = (uint8_t *)sIdx;
     for (uint32_t i = lane; i < j.index_size / 4; i += 64) sIdx[i] = 0;
-    __syncthreads();
+    wave_sync();
     for (uint32_t s = lane; s < nblk; s += 64) {
         const uint32_t k = k0 + s;
         const uint64_t first = (uint64_t)k * j.vcm;
@@ -924,7 +935,7 @@ __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int nj
         if (s == nblk - 1)
             for (int l = 0; l < 4; l++) sKeys[1][l] = kmax[l];
     }
-    __syncthreads();
+    wave_sync();
     LdsMsg body(sIdx + kHeaderSize / 4, j.index_size - kHeaderSize);
     const uint32_t body_tag = aegis_mac32(sT, body);
     const uint32_t index_slot = index_block_slot(t, k_last);
@@ -939,11 +950,11 @@ __global__ __launch_bounds__(64) void k_index_blocks(const JobDesc *jobs, int nj
     h.meta2 = ks;         // .key_size
     h.meta3 = j.tree_id;  // .tree_id
     h.block_type = 4;     // BlockType.index (schema.zig:64)
-    __syncthreads();
+    wave_sync();
     const uint32_t hdr_tag = finish_header(sT, sIdx, h, body_tag);
-    __syncthreads();
+    wave_sync();
     if (lane < 4) sIdx[lane] = hdr_tag;
-    __syncthreads();
+    wave_sync();
     uint8_t *blk = j.out_blocks + (size_t)index_slot * j.block_size;
     for (uint32_t i = lane; i < j.index_size / 4; i += 64) gst<uint32_t>(blk + 4 * i, sIdx[i]);
     const uint32_t end = (uint32_t)sector_ceil(j.index_size);
@@ -1029,7 +1040,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
     }
     if (mark) mark(mark_ctx, "data_blocks");
     if (total_tables) {
-        hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(64), 0, s, d_jobs, njobs, d_results, d_infos);
+        hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "index_blocks");
