@@ -7,7 +7,7 @@ draws 2,358,720 unique uniform-random u128 ids (seed 0x7B0002 + job);
 and cut into 8 full level-B tables. IdTreeValue{id, timestamp, padding = 0},
 no tombstones, drop_tombstones = false, usage general. 66,044,160 values x
 32 B = 2.11 GB of input per GPU, resident in HBM (as 1 MiB grid blocks)
-before timing. `--config 3` / `--config 5` run BASELINE configs[2] / [4]
+before timing. `--config 3|4|5` run BASELINE configs[2] / [3] / [4]
 (tigerbeetle_amd/configs.py); config 3's step includes landing each unsorted
 memtable (a D2D copy) and sorting all of them (tbc_sort_values_batch).
 
@@ -213,9 +213,8 @@ def main() -> None:
     bs = 1 << 20
     eng = Engine(device=local, block_size=bs, profile=True, arena_bytes=2 << 30)
     # Weak scaling: njobs jobs per GPU; the global job set is sharded by
-    # bytes (all jobs of a config are about the same size), no data-path
-    # collective.
-    plan = plan_shards([1] * (njobs * world), world)
+    # input bytes (LPT, shard.py), no data-path collective.
+    plan = plan_shards([configs.job_bytes(args.config, j) for j in range(njobs * world)], world)
     wl = Workload(eng, args.config, plan[rank], bs)
     eng.synchronize()
 

@@ -1,6 +1,6 @@
 """GPU parity at BASELINE.json's full sizes: whole production-sized jobs of
-configs 2, 3 and 5 (tigerbeetle_amd/configs.py), staged exactly as bench.py
-stages them, compared block-for-block with the oracle; plus size-independent
+configs 2, 3, 4 (a whole forest unit: 21 jobs of 4 key kinds in one batch)
+and 5 (tigerbeetle_amd/configs.py), staged exactly as bench.py stages them, compared block-for-block with the oracle; plus size-independent
 properties of the output (every block's checksums verify, keys strictly
 increase across the whole output, value counts add up).
 """
@@ -25,7 +25,7 @@ def _oracle_job(oracle_lib, js, bs, addrs):
                               level_b=js.level_b, cluster=0xA5A5, snapshot_min=48, addresses=addrs)
 
 
-@pytest.mark.parametrize("config,job_ids", [(2, [0, 1]), (3, [0, 1, 6]), (5, [0])])
+@pytest.mark.parametrize("config,job_ids", [(2, [0, 1]), (3, [0, 1, 6]), (4, list(range(21))), (5, [0])])
 def test_full_size_jobs_bit_exact(oracle_lib, config, job_ids):
     import bench
     from tigerbeetle_amd import Engine

@@ -65,3 +65,15 @@ def test_two_rank_reduction_over_gloo():
         assert total == sum(sizes)            # every job counted exactly once
         assert t == 2.0                       # max over ranks
         assert sorted(i for g in gathered for i in g) == list(range(12))
+
+
+def test_forest_plan_balances_bytes():
+    # Config 4: jobs of 4 key kinds and 3 sizes; every rank's load stays within
+    # one job of the mean (LPT), for every world size the bench runs.
+    from tigerbeetle_amd import configs
+    for world in (1, 2, 4, 8):
+        sizes = [configs.job_bytes(4, j) for j in range(configs.FOREST_JOBS * world)]
+        plan = plan_shards(sizes, world)
+        assert sorted(i for p in plan for i in p) == list(range(len(sizes)))
+        loads = [sum(sizes[i] for i in p) for p in plan]
+        assert max(loads) - min(loads) <= max(sizes)

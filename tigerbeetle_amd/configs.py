@@ -17,6 +17,14 @@ arrays at a time) to keep host memory bounded at the 1B-value scale.
             secondary-index merge rule). Every 7th job is the sequential
             transfers.timestamp object tree (Transfer, 128 B): already sorted,
             no B, a pure flush.
+  config 4  full groove compaction (one forest unit per GPU, 21 jobs): the
+            bar-end immutable->L0 compaction of the 11 trees a create_transfers
+            bar feeds (10 transfer trees — pending_id/timeout are 0 and not
+            indexed, groove.zig:928-934 — plus the accounts object tree, 2
+            updates per transfer over 10,000 accounts), each memtable sorted
+            on the device when it arrives unsorted, and one L1->L2 disk
+            compaction (1 A + 4 B tables) per transfer tree. Jobs differ in
+            tree, key kind and size; ranks get whole jobs by bytes (LPT).
   config 5  accounts.timestamp object tree (Account, 128 B), last level:
             disk A = 1 table (524,160 newer versions of uniformly chosen
             existing keys, 1% tombstones) into 8 last-level B tables;
@@ -166,12 +174,111 @@ def config5_job(job: int, n_b_tables: int = 8) -> JobSpec:
                    True, 6)
 
 
-GENERATORS = {2: config2_job, 3: config3_job, 5: config5_job}
-DEFAULT_JOBS = {2: 28, 3: 28, 5: 27}
+CONFIG4_SEED = 0x7B0004
+# The 11 trees a create_transfers bar feeds.
+FOREST_BAR = ["transfers.id", "transfers.timestamp", "transfers.debit_account_id", "transfers.credit_account_id",
+              "transfers.amount", "transfers.user_data_128", "transfers.user_data_64", "transfers.user_data_32",
+              "transfers.ledger", "transfers.code", "accounts.timestamp"]
+FOREST_DEEP = FOREST_BAR[:10]
+FOREST_JOBS = len(FOREST_BAR) + len(FOREST_DEEP)  # 21 per forest unit
+L0_TABLES = 2
+
+
+def _bar_fields(name: str, rng, n: int) -> np.ndarray:
+    """Indexed field of n transfers (benchmark_load.zig:291-313 shapes)."""
+    if name in ("transfers.debit_account_id", "transfers.credit_account_id"):
+        return rng.integers(1, ACCOUNTS + 1, size=n, dtype=np.uint64)
+    if name == "transfers.amount":
+        return np.maximum(1, rng.exponential(10_000, size=n)).astype(np.uint64)
+    if name == "transfers.ledger":
+        return np.ones(n, dtype=np.uint64)
+    if name == "transfers.code":
+        return rng.integers(1, 100, size=n, dtype=np.uint64)
+    if name == "transfers.user_data_32":
+        return rng.integers(0, 1 << 32, size=n, dtype=np.uint64)
+    return rng.integers(0, 1 << 63, size=n, dtype=np.uint64)
+
+
+def _bar_values(spec: trees.TreeSpec, name: str, rng, ts: np.ndarray, ids: np.ndarray) -> np.ndarray:
+    n = len(ts)
+    if name == "transfers.id":
+        v = np.zeros((n, 32), dtype=np.uint8)
+        w = v.view(np.uint64)
+        w[:, 0] = ids
+        w[:, 2] = ts
+        return v
+    if name == "transfers.timestamp":
+        return workloads.values_from_keys(spec, [ts], np.zeros(n, dtype=bool), rng)
+    field = _bar_fields(name, rng, n)
+    if spec.key_kind == workloads.KEY_COMPOSITE_U64:
+        return workloads.values_from_keys(spec, [ts, field], np.zeros(n, dtype=bool), rng)
+    return workloads.values_from_keys(spec, [ts, field, np.zeros(n, dtype=np.uint64)], np.zeros(n, dtype=bool), rng)
+
+
+def _sorted_by_key(spec: trees.TreeSpec, v: np.ndarray) -> np.ndarray:
+    return v[workloads.sort_keys(workloads.keys_of(v, spec))]
+
+
+def config4_job(job: int) -> JobSpec:
+    """Job `job` of the forest units (BASELINE configs[3]): unit = job // 21."""
+    unit, k = divmod(job, FOREST_JOBS)
+    rng = np.random.default_rng(CONFIG4_SEED + job)
+    n = TABLE_T
+    if k < len(FOREST_BAR):
+        name = FOREST_BAR[k]
+        spec = trees.BY_NAME[name]
+        bar = unit + L0_TABLES + 1  # bars before this one fill L0
+        if name == "accounts.timestamp":
+            # 2 updates per transfer over 10,000 accounts (timestamps 1..10k),
+            # insertion order = update order; L0 holds the previous versions.
+            acc_ts = rng.integers(1, ACCOUNTS + 1, size=2 * n, dtype=np.uint64)
+            a = workloads.values_from_keys(spec, [acc_ts], np.zeros(2 * n, dtype=bool), rng)
+            b = workloads.values_from_keys(spec, [np.arange(1, ACCOUNTS + 1, dtype=np.uint64)],
+                                           np.zeros(ACCOUNTS, dtype=bool), rng)
+            return JobSpec(spec, a, True, True, [b], False, 0)
+        ts0 = np.uint64(ACCOUNTS + 1 + bar * n)
+        ts = ts0 + np.arange(n, dtype=np.uint64)
+        ids = np.uint64(1 + bar * n) + np.arange(n, dtype=np.uint64)
+        a = _bar_values(spec, name, rng, ts, ids)
+        unsorted = bool(len(a) > 1 and workloads.sort_keys(workloads.keys_of(a, spec))[:-1].tolist()
+                        != list(range(len(a) - 1)))
+        # L0: the L0_TABLES previous bars of the same tree, merged and cut.
+        old_ts = np.uint64(ACCOUNTS + 1 + (bar - L0_TABLES) * n) + np.arange(L0_TABLES * n, dtype=np.uint64)
+        old_ids = np.uint64(1 + (bar - L0_TABLES) * n) + np.arange(L0_TABLES * n, dtype=np.uint64)
+        b_all = _sorted_by_key(spec, _bar_values(spec, name, rng, old_ts, old_ids))
+        return JobSpec(spec, a, True, unsorted, [b_all[i * n:(i + 1) * n] for i in range(L0_TABLES)], False, 0)
+    name = FOREST_DEEP[k - len(FOREST_BAR)]
+    spec = trees.BY_NAME[name]
+    ji = workloads.make_job_inputs(spec, rng, n_a=n, b_table_sizes=[n] * 4, a_immutable=False, overlap=0.05,
+                                   tomb_frac=0.01 if spec.usage == 0 else 0.0)
+    return JobSpec(spec, ji.a_values, False, False, ji.b_tables, False, 2)
+
+
+def job_bytes(config: int, job: int) -> int:
+    """Input bytes of a job without generating it (for the byte-balanced shard plan)."""
+    if config == 2:
+        return 9 * TABLE_T * 32
+    if config == 3:
+        return TABLE_T * (128 if job % 7 == 6 else 9 * 32)
+    if config == 5:
+        return 9 * TABLE_A_TS * 128
+    k = job % FOREST_JOBS
+    if k < len(FOREST_BAR):
+        name = FOREST_BAR[k]
+        if name == "accounts.timestamp":
+            return (2 * TABLE_T + ACCOUNTS) * 128
+        return (1 + L0_TABLES) * TABLE_T * trees.BY_NAME[name].value_size
+    return 5 * TABLE_T * trees.BY_NAME[FOREST_DEEP[k - len(FOREST_BAR)]].value_size
+
+
+GENERATORS = {2: config2_job, 3: config3_job, 4: config4_job, 5: config5_job}
+DEFAULT_JOBS = {2: 28, 3: 28, 4: FOREST_JOBS, 5: 27}
 DESCRIPTION = {
     2: "transfers.id L0->L1 compaction, 28 jobs x (1 A + 8 B tables) per GPU, 64M u128 keys, 1 MiB blocks",
     3: "bar end of transfers.debit/credit_account_id (Zipf 1.1 over 10k accounts, unsorted memtable sorted on "
        "device, 1% put/remove pairs) + sequential transfers.timestamp flushes, 28 jobs per GPU",
+    4: "full groove compaction: bar-end immutable->L0 of the 11 trees a create_transfers bar feeds (+ on-device "
+       "memtable sorts) and one L1->L2 job per transfer tree, 21 jobs of 4 key kinds per GPU, sharded by bytes",
     5: "accounts.timestamp last-level compaction (Account 128 B, 1% tombstones dropped), 27 jobs x 4.7M values "
        "per GPU (1B values over 8 GPUs)",
 }

@@ -600,7 +600,7 @@ struct SegCursor {
 __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint32_t cnt, const uint64_t *status,
                                              const uint64_t *masks, const uint32_t *block_tile,
                                              const SplitDesc *splits, uint8_t *body, uint32_t *prog,
-                                             uint32_t *err) {
+                                             uint32_t *err, uint64_t *stage) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1;
     const uint32_t vs = j.value_size;
@@ -614,39 +614,86 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
     SegCursor ca, cb;
     ca.init(j.a, sp.seg_a);
     cb.init(j.b, sp.seg_b);
-    uint32_t w = 0, since = 0;
+    // A tile's 64 mask words (32 survivor, 32 from-A) arrive in ONE load, one
+    // word per lane, and the next tile's are in flight meanwhile: walking a
+    // word is register work, so sparse survivors (heavy dedup, e.g. 2 updates
+    // per transfer over 10k accounts) cost no memory latency per word.
+    constexpr uint32_t W = kMergeTile / 64;
+    auto tile_words = [&](uint32_t tt) -> uint64_t {
+        const uint32_t tc = tt < j.tile_count ? tt : j.tile_count - 1;
+        return gld<uint64_t>(masks + (size_t)(j.tile_base + tc) * (2 * W) + lane);
+    };
+    auto word_of = [](uint64_t v, uint32_t src) -> uint64_t {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)src);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)src);
+        return (uint64_t)hi << 32 | lo;
+    };
+    uint64_t cur = tile_words(t), nxt = tile_words(t + 1);
+    // Survivors are staged as (source, destination) pairs in this wave's LDS
+    // slots and copied 64 at a time: dense words (64 survivors) flush every
+    // word as before, sparse ones (heavy dedup: ~1 survivor per word) share
+    // one memory round trip per 64 survivors instead of one per word.
+    uint64_t *st_src = stage, *st_dst = stage + 64;
+    const uint32_t cpv_log = __builtin_ctz(vs >> 4);
+    uint32_t pend = 0, since = 0;
+    auto flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t c = lane; c < (pend << cpv_log); c += 64) {
+            const uint32_t e = c >> cpv_log, q = c & ((1u << cpv_log) - 1);
+            gst<u32x4>((uint8_t *)(uintptr_t)st_dst[e] + 16 * q, gld<u32x4>((const uint8_t *)(uintptr_t)st_src[e] + 16 * q));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pend = 0;
+        since++;
+    };
+    uint32_t w = 0;
     while (out_cur < out_end) {
-        const uint64_t *m = masks + (size_t)(j.tile_base + t) * (2 * (kMergeTile / 64));
-        const uint64_t sm = gld<uint64_t>(m + w), am = gld<uint64_t>(m + kMergeTile / 64 + w);
+        const uint64_t sm = word_of(cur, w), am = word_of(cur, W + w);
         const uint32_t pos0 = t * kMergeTile + 64 * w;
         const uint64_t valid = n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1);
         const uint32_t ns = __builtin_popcountll(sm);
-        if (out_cur + ns > out_begin) {
+        if (ns && out_cur + ns > out_begin) {
             ca.advance(a_cur);
             cb.advance(b_cur);
-            const bool from_a = (am >> lane) & 1;
             const uint64_t o = out_cur + __builtin_popcountll(sm & lt);
-            if (((sm >> lane) & 1) && o >= out_begin && o < out_end) {
+            const bool mine = ((sm >> lane) & 1) && o >= out_begin && o < out_end;
+            const uint64_t mm = __ballot(mine);
+            const uint32_t m_cnt = __builtin_popcountll(mm);
+            if (pend + m_cnt > 64) flush();
+            if (mine) {
+                const bool from_a = (am >> lane) & 1;
                 const uint8_t *src = from_a ? ca.elem(a_cur + __builtin_popcountll(am & lt), vs)
                                             : cb.elem(b_cur + __builtin_popcountll(valid & ~am & lt), vs);
-                uint8_t *dst = body + (size_t)(o - out_begin) * vs;
-                for (uint32_t q = 0; q < vs; q += 16) gst<u32x4>(dst + q, gld<u32x4>(src + q));
+                const uint32_t slot = pend + __builtin_popcountll(mm & lt);
+                st_src[slot] = (uint64_t)(uintptr_t)src;
+                st_dst[slot] = (uint64_t)(uintptr_t)(body + (size_t)(o - out_begin) * vs);
             }
+            pend += m_cnt;
         }
         a_cur += __builtin_popcountll(am);
         b_cur += __builtin_popcountll(valid & ~am);
         out_cur += ns;
-        if (++w == kMergeTile / 64) {
+        if (++w == W) {
             w = 0;
             if (++t >= j.tile_count && out_cur < out_end) { // masks disagree with the scan: report, release
                 if (lane == 0) gst<uint32_t>(err, 0xbad0u);
                 out_cur = out_end;
             }
+            cur = nxt;
+            nxt = tile_words(t + 1);
         }
-        // Publish every 4 steps (and at the end): stores complete, then progress.
-        if (++since == 4 || out_cur >= out_end) {
+        if (pend == 64) flush();
+        // Publish after every 4 flushes (and at the end): stores complete,
+        // then progress (whole 256-byte units of the flushed prefix).
+        const bool end = out_cur >= out_end;
+        if (end && pend) flush();
+        if (since >= 4 || end) {
             since = 0;
-            const uint64_t done = (out_cur < out_end ? out_cur : out_end);
+            const uint64_t done = (out_cur < out_end ? out_cur : out_end) - pend;
             const uint32_t bytes = done > out_begin ? (uint32_t)(done - out_begin) * vs : 0u;
             const uint32_t pub = bytes >= len ? len : (bytes & ~255u);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -687,6 +734,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
+    __shared__ uint64_t sStage[Fused ? 2 * kMaxChainWaves : 1][128]; // producer copy staging
     load_tables(sT);
     if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = 0;
     __syncthreads();
@@ -712,7 +760,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
         const JobDesc &j = jobs[ji];
         uint8_t *blk = j.out_blocks + (size_t)data_block_slot(k, j.dbcm) * j.block_size;
         produce_body(j, k, block_count(j, k), status, masks, block_tile, splits, blk + kHeaderSize, &sProg[p],
-                     const_cast<uint32_t *>(&res[j.job_index].invariant));
+                     const_cast<uint32_t *>(&res[j.job_index].invariant), sStage[Fused ? p : 0]);
         return;
     }
     const uint32_t wave = blockIdx.x * C + wave_in_block;
