@@ -164,7 +164,7 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
 
 
 # bench kernel label -> rocprofv3 kernel symbol (tools/traffic.py short names)
-KERNEL_SYMBOL = {"merge_partition": "k_partition", "merge": "k_merge_tile", "data_blocks": "k_data_blocks",
+KERNEL_SYMBOL = {"merge_partition": "k_partition_all", "merge": "k_merge_tile", "data_blocks": "k_data_blocks",
                  "assemble": "k_assemble",
                  "index_blocks": "k_index_blocks"}
 

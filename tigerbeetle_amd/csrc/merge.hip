@@ -105,17 +105,11 @@ __device__ __forceinline__ const uint8_t *elem_ptr(const Stream &s, uint32_t seg
 // i of A elements among the first d merged elements, plus the segments that
 // hold A[max(i-1, 0)] and B[min(d-i, nb-1)] (where the tile starts reading).
 // --------------------------------------------------------------------------
+// All key kinds of a batch in ONE launch (the split's job picks the key
+// loader): a batch mixing trees paid one latency-bound launch per kind.
 template <int KIND>
-__global__ __launch_bounds__(256) void k_partition(const JobDesc *jobs, int njobs, uint32_t split_offset,
-                                                   uint32_t nsplits, SplitDesc *splits) {
-    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
-    if (gid >= nsplits) return;
-    const uint32_t gsplit = split_offset + gid;
-    const int ji = find_job(jobs, njobs, gsplit, [](const JobDesc &d) { return d.split_base; });
-    const JobDesc &j = jobs[ji];
-    const uint32_t t = gsplit - j.split_base;
-    const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
-    const uint32_t d = (uint64_t)t * kMergeTile < n ? t * kMergeTile : n;
+__device__ __forceinline__ uint32_t merge_path_split(const JobDesc &j, uint32_t d) {
+    const uint32_t na = j.a.n, nb = j.b.n;
     uint32_t lo = d > nb ? d - nb : 0;
     uint32_t hi = d < na ? d : na;
     const uint32_t vs = j.value_size, ts = j.timestamp_offset;
@@ -126,6 +120,25 @@ __global__ __launch_bounds__(256) void k_partition(const JobDesc *jobs, int njob
         const uint8_t *pb = elem_ptr(j.b, seg_search(j.b, ib), ib, vs);
         if (key_le(load_key<KIND>(pa, ts), load_key<KIND>(pb, ts))) lo = mid + 1;
         else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int njobs, uint32_t nsplits,
+                                                       SplitDesc *splits) {
+    const uint32_t gsplit = blockIdx.x * 256 + threadIdx.x;
+    if (gsplit >= nsplits) return;
+    const int ji = find_job(jobs, njobs, gsplit, [](const JobDesc &d) { return d.split_base; });
+    const JobDesc &j = jobs[ji];
+    const uint32_t t = gsplit - j.split_base;
+    const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
+    const uint32_t d = (uint64_t)t * kMergeTile < n ? t * kMergeTile : n;
+    uint32_t lo;
+    switch (j.key_kind) {
+    case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
+    case kKeyIdU128: lo = merge_path_split<kKeyIdU128>(j, d); break;
+    case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
+    default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
     }
     SplitDesc s;
     s.i = lo;
@@ -400,10 +413,10 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
     const uint32_t nsplits = l.split_base + l.tile_count + 1 - split_off;
     const uint32_t tile_off = f.tile_base;
     const uint32_t ntiles = l.tile_base + l.tile_count - tile_off;
-    if (phase == 0)
-        hipLaunchKernelGGL(k_partition<KIND>, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs + first, count,
-                           split_off, nsplits, d_splits);
-    else if (ntiles)
+    (void)phase;
+    (void)split_off;
+    (void)nsplits;
+    if (ntiles)
         hipLaunchKernelGGL(k_merge_tile<KIND>, dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,
                            (const SplitDesc *)d_splits, d_status, d_masks);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -436,7 +449,13 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
             }
         });
     };
-    if (phase(0)) return -1;
+    {
+        const JobDesc &l = h_jobs[njobs - 1];
+        const uint32_t nsplits = l.split_base + l.tile_count + 1;
+        hipLaunchKernelGGL(k_partition_all, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
+                           d_splits);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
     if (mark) mark(mark_ctx, "merge_partition");
     if (phase(1)) return -1;
     hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
