@@ -202,12 +202,17 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for a 1-GPU box (the driver's N>1 runs use neither):
+    # every rank on device 0, timing reduction over gloo.
+    if os.environ.get("TBC_BENCH_SAME_DEVICE"):
+        local = 0
+    backend = os.environ.get("TBC_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
     dist = None
     if world > 1:
         import torch
         import torch.distributed as td
         torch.cuda.set_device(local)
-        td.init_process_group("nccl")
+        td.init_process_group(backend)
         dist = td
 
     bs = 1 << 20
@@ -260,7 +265,8 @@ def main() -> None:
             assert r.value_count == 9 * configs.TABLE_T and r.table_count == 9, (r.value_count, r.table_count)
     b.release()
 
-    total_bytes, t_max = reduce_step(dist, wl.input_bytes, dt, device=f"cuda:{local}" if dist else None)
+    total_bytes, t_max = reduce_step(dist, wl.input_bytes, dt,
+                                     device=f"cuda:{local}" if dist and backend == "nccl" else None)
     step_s = t_max / args.steps
     value = total_bytes / step_s / 1e6
 
