@@ -313,6 +313,18 @@ def main() -> None:
                          "frac": round(job_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},
     }
+    if "assemble" not in per_step and "data_blocks" in per_step:
+        # Latency regime: every data block's AEGIS-128L chain is in flight at
+        # once, so the data-block kernel is bound by the chain of the longest
+        # block (32,767 sequential updates for a full 1 MiB body), not by HBM.
+        # Floor: 58.3 ns per update for one chain alone on an idle MI355X
+        # (tools/chain_probe.py).
+        updates = (bs - 256 + 31) // 32 + 7
+        floor_us = updates * 58.3e-3
+        line["latency_roofline"] = {"bound": "aegis_chain", "kernel": "data_blocks",
+                                    "updates_per_block": updates, "floor_us": round(floor_us, 1),
+                                    "achieved_us": round(per_step["data_blocks"], 1),
+                                    "frac": round(floor_us / per_step["data_blocks"], 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config, njobs)
     if rank == 0:

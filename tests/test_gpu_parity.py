@@ -241,3 +241,35 @@ def test_compaction_parity_throughput_regime(engine_small, oracle_lib):
     total_blocks = sum(workloads.worst_case_blocks(s, kw["n_a"] * 9 // 2, bs) for s, kw in cases)
     assert total_blocks > 4096, total_blocks
     _compare(oracle_lib, engine_small, cases, bs)
+
+
+def test_submit_rejects_broken_preconditions(engine_small):
+    """The reference asserts (compaction.zig:307-318 reservation, 16-byte
+    aligned values); the C ABI returns a status instead and runs nothing."""
+    from tigerbeetle_amd.abi import TBC_ERR_CAPACITY, TBC_ERR_INVALID_ARGUMENT, TbcError
+    from tigerbeetle_amd.engine import Job
+    bs = 4096
+    spec = trees.with_table_size(trees.BY_NAME["transfers.id"], 500)
+    rng = np.random.default_rng(21)
+    ji = workloads.make_job_inputs(spec, rng, n_a=300, b_table_sizes=[400], a_immutable=True, overlap=0.2)
+    abuf = engine_small.upload(ji.a_values, pad=64)
+    bbuf = engine_small.upload(ji.b_tables[0], pad=64)
+    out = engine_small.alloc(64 * bs)
+    few = np.arange(1, 3, dtype=np.uint64)  # 700 values need 6 data blocks + 2 index blocks
+    with pytest.raises(TbcError) as e:
+        engine_small.submit([Job(spec, [(abuf.ptr, 300)], [(bbuf.ptr, 400)], True, False, 1, 1, 48, few, out)])
+    assert e.value.status == TBC_ERR_CAPACITY
+    addrs = np.arange(1, 64, dtype=np.uint64)
+    with pytest.raises(TbcError) as e:  # values must be 16-byte aligned
+        engine_small.submit([Job(spec, [(abuf.ptr + 8, 300)], [(bbuf.ptr, 400)], True, False, 1, 1, 48, addrs, out)])
+    assert e.value.status == TBC_ERR_INVALID_ARGUMENT
+    with pytest.raises(TbcError) as e:  # an immutable table A is one segment
+        engine_small.submit([Job(spec, [(abuf.ptr, 100), (abuf.ptr + 3200, 200)], [(bbuf.ptr, 400)], True, False, 1,
+                                 1, 48, addrs, out)])
+    assert e.value.status == TBC_ERR_INVALID_ARGUMENT
+    # and the engine still works afterwards
+    ok = engine_small.submit([Job(spec, [(abuf.ptr, 300)], [(bbuf.ptr, 400)], True, False, 1, 1, 48, addrs, out)])
+    ok.wait()
+    r, _ = ok.result(0)
+    assert r.status == 0 and r.value_count > 0
+    ok.release()
