@@ -152,6 +152,23 @@ tbc_status tbc_synchronize(tbc_engine *engine);
 tbc_status tbc_checksum_batch(tbc_engine *engine, const void *const *messages, const uint64_t *lengths,
                               uint32_t count, uint8_t *checksums_out);
 
+/* ---- grid.read_block_validate (src/vsr/grid.zig:1059-1084) ---------------------- */
+/* Result per block, in the reference's check order. */
+typedef enum tbc_block_check {
+    TBC_BLOCK_VALID = 0,
+    TBC_BLOCK_INVALID_CHECKSUM = 1,      /* header checksum (bytes [16, 256)) */
+    TBC_BLOCK_UNEXPECTED_COMMAND = 2,    /* command != block (20) */
+    TBC_BLOCK_INVALID_CHECKSUM_BODY = 3, /* body checksum (bytes [256, size)) */
+    TBC_BLOCK_UNEXPECTED_CHECKSUM = 4,   /* header checksum != the expected (manifest/index) checksum */
+    TBC_BLOCK_UNEXPECTED_ADDRESS = 5,    /* header address != the expected address (reference asserts) */
+    TBC_BLOCK_INVALID_SIZE = 6,          /* size outside [256, block_size] (reference asserts) */
+} tbc_block_check;
+/* Synchronous batched validation of device-resident blocks (16-byte aligned
+ * device pointers, block_size readable). expect_checksums: 2 u64 (u128 LE)
+ * per block; expect_addresses: 1 u64 per block; results_out: count bytes. */
+tbc_status tbc_blocks_validate(tbc_engine *engine, const void *const *blocks, const uint64_t *expect_checksums,
+                               const uint64_t *expect_addresses, uint32_t count, uint8_t *results_out);
+
 /* ---- TableMemory.sort (src/lsm/table_memory.zig:140-154) ---------------------- */
 /* Synchronous stable ascending sort of `count` values (device memory) by key.
  * A no-op when the keys are already non-decreasing (table_memory.zig:83-87). */

@@ -273,3 +273,37 @@ def test_submit_rejects_broken_preconditions(engine_small):
     r, _ = ok.result(0)
     assert r.status == 0 and r.value_count > 0
     ok.release()
+
+
+def test_blocks_validate_matches_grid_read_block_validate(engine_small, oracle_lib):
+    """grid.read_block_validate (grid.zig:1059-1084) on the device: every
+    output block of a compaction validates; each corruption is reported with
+    the reference's result, in the reference's check order."""
+    bs = 4096
+    spec = trees.with_table_size(trees.BY_NAME["transfers.timestamp"], 100)
+    rng = np.random.default_rng(31)
+    ji = workloads.make_job_inputs(spec, rng, n_a=250, b_table_sizes=[80], a_immutable=True, dup_frac=0.1,
+                                   overlap=0.2)
+    addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, 330, bs) + 2, rng, 40)
+    (r, _, blocks), = gpu_run(engine_small, [ji], bs, [addrs])[0]
+    n = r.block_count
+    buf = engine_small.upload(blocks[:n])
+    ptrs = [buf.ptr + i * bs for i in range(n)]
+    cks = [int.from_bytes(b[0:16].tobytes(), "little") for b in blocks[:n]]
+    adr = [int(b[224:232].view(np.uint64)[0]) for b in blocks[:n]]
+    assert list(engine_small.validate_blocks(ptrs, cks, adr)) == [0] * n
+
+    def corrupt(i, off, val, fix_header=False):
+        img = blocks[i].copy()
+        img[off] = val
+        if fix_header:  # keep the header checksum valid (to reach the later checks)
+            img[0:16] = np.frombuffer(oracle_lib.checksum(img[16:256].tobytes()).to_bytes(16, "little"), np.uint8)
+        one = engine_small.upload(img)
+        return int(engine_small.validate_blocks([one.ptr], [cks[i]], [adr[i]])[0])
+
+    assert corrupt(0, 300, blocks[0][300] ^ 1) == 3          # body byte -> invalid_checksum_body
+    assert corrupt(0, 232, blocks[0][232] ^ 1) == 1          # header byte -> invalid_checksum
+    assert corrupt(0, 110, 19, fix_header=True) == 2         # command -> unexpected_command
+    assert corrupt(0, 232, blocks[0][232] ^ 1, fix_header=True) == 4  # valid, but not the expected checksum
+    wrong = engine_small.validate_blocks([ptrs[1]], [cks[1]], [adr[1] + 1])
+    assert int(wrong[0]) == 5                                  # address mismatch

@@ -127,6 +127,7 @@ _SIGNATURES = {
     "tbc_checksum_batch": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_uint32, _P]),
     "tbc_copy_device_async": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64]),
+    "tbc_blocks_validate": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint32, _P]),
     "tbc_sort_values": (ctypes.c_int, [_P, ctypes.POINTER(Tree), _P, ctypes.c_uint32]),
     "tbc_sort_values_async": (ctypes.c_int, [_P, ctypes.POINTER(Tree), _P, ctypes.c_uint32]),
     "tbc_sort_values_batch": (ctypes.c_int, [_P, ctypes.POINTER(SortJob), ctypes.c_uint32]),

@@ -491,6 +491,41 @@ __global__ __launch_bounds__(1024) void k_checksum_batch(const uint64_t *ptrs, c
     if ((lane & 31) < 4 && mine < count) gst<uint32_t>(out + 16 * (size_t)i + 4 * (lane & 3), tag);
 }
 
+// grid.read_block_validate (src/vsr/grid.zig:1059-1084) for a batch of
+// blocks: one wave per block, the lower 32-lane group checksums the header
+// (bytes [16, 256)), the upper group the body ([256, size)); then the checks
+// in the reference's order. Result codes: tbc_block_check (tbc.h).
+__global__ __launch_bounds__(1024) void k_validate_blocks(const uint64_t *ptrs, const uint64_t *expect, uint32_t count,
+                                                          uint32_t block_size, uint8_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= count) return;
+    const uint32_t lane = threadIdx.x & 63, g = lane & 31;
+    const uint8_t *blk = (const uint8_t *)ptrs[wave];
+    const uint32_t size = gld<uint32_t>(blk + 96);
+    const bool size_ok = size >= kHeaderSize && size <= block_size;
+    const bool upper = lane >= 32;
+    GlobalMsg m(upper ? blk + kHeaderSize : blk + 16, upper ? (size_ok ? size - kHeaderSize : 0u) : 240u);
+    const uint32_t tag = aegis_mac32(sT, m);
+    // Lane g < 4 of each group compares its column with the stored checksum.
+    const uint32_t stored = g < 4 ? gld<uint32_t>(blk + (upper ? 32 : 0) + 4 * g) : tag;
+    const uint64_t bad = __ballot(tag != stored);
+    if (lane != 0) return;
+    const bool header_ok = (bad & 0xfull) == 0, body_ok = ((bad >> 32) & 0xfull) == 0;
+    uint8_t r;
+    if (!header_ok) r = 1;                                       // invalid_checksum
+    else if (blk[110] != 20) r = 2;                              // unexpected_command (Command.block)
+    else if (!size_ok) r = 6;                                    // size out of bounds (reference asserts)
+    else if (!body_ok) r = 3;                                    // invalid_checksum_body
+    else if (gld<uint64_t>(blk) != expect[3 * wave] || gld<uint64_t>(blk + 8) != expect[3 * wave + 1])
+        r = 4;                                                   // unexpected_checksum
+    else if (gld<uint64_t>(blk + 224) != expect[3 * wave + 2]) r = 5; // address (reference asserts)
+    else r = 0;
+    out[wave] = r;
+}
+
 __device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return gld<uint64_t>(p); }
 
 // Key (as 4 little-endian limbs) of a value; see composite_key.zig:48-50,
@@ -1040,6 +1075,15 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
 static uint32_t waves_per_block(uint32_t waves) {
     uint32_t w = (waves + 255) / 256;
     return w < 1 ? 1 : (w > 16 ? 16 : w);
+}
+
+int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uint32_t count, uint32_t block_size,
+                          uint8_t *d_out, void *stream) {
+    if (count == 0) return 0;
+    const uint32_t wpb = waves_per_block(count);
+    hipLaunchKernelGGL(k_validate_blocks, dim3((count + wpb - 1) / wpb), dim3(64 * wpb), 0, (hipStream_t)stream,
+                       d_ptrs, d_expect, count, block_size, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,

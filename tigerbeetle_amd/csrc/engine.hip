@@ -280,6 +280,43 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
     return st;
 }
 
+tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const uint64_t *expect_checksums,
+                               const uint64_t *expect_addresses, uint32_t count, uint8_t *results_out) {
+    if (!e || (count && (!blocks || !expect_checksums || !expect_addresses || !results_out)))
+        return TBC_ERR_INVALID_ARGUMENT;
+    if (!count) return TBC_OK;
+    for (uint32_t i = 0; i < count; i++)
+        if (!blocks[i] || ((uintptr_t)blocks[i] & 15)) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    const uint64_t in_bytes = 32ull * count, out_off = align_up(in_bytes, 256);
+    const uint64_t dt = e->dev.top, ht = e->host.top;
+    uint8_t *d = e->dev.alloc(out_off + count);
+    uint8_t *h = e->host.alloc(out_off + count);
+    if (!d || !h) {
+        e->dev.top = dt;
+        e->host.top = ht;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    uint64_t *hp = (uint64_t *)h, *hx = hp + count;
+    for (uint32_t i = 0; i < count; i++) {
+        hp[i] = (uint64_t)(uintptr_t)blocks[i];
+        hx[3 * i] = expect_checksums[2 * i];
+        hx[3 * i + 1] = expect_checksums[2 * i + 1];
+        hx[3 * i + 2] = expect_addresses[i];
+    }
+    tbc_status st = TBC_OK;
+    if (hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        launch_validate_blocks((const uint64_t *)d, (const uint64_t *)d + count, count, e->block_size, d + out_off,
+                               e->stream) != 0 ||
+        hipMemcpyAsync(h + out_off, d + out_off, count, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        st = TBC_ERR_DEVICE;
+    if (st == TBC_OK) memcpy(results_out, h + out_off, count);
+    e->dev.top = dt;
+    e->host.top = ht;
+    return st;
+}
+
 static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count) {
     if (!e || (count && !jobs)) return TBC_ERR_INVALID_ARGUMENT;
     std::vector<SortItem> items(count);

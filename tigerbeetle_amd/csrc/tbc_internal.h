@@ -130,6 +130,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx);
+int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uint32_t count, uint32_t block_size,
+                          uint8_t *d_out, void *stream);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
 struct SortItem {

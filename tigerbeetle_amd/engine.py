@@ -214,6 +214,20 @@ class Engine:
         check(lib().tbc_checksum_batch(self.handle, P, L, n, out.ctypes.data), "tbc_checksum_batch")
         return out[: 16 * n].reshape(n, 16)
 
+    def validate_blocks(self, ptrs: list, expect_checksums: list, expect_addresses: list) -> np.ndarray:
+        """grid.read_block_validate on device-resident blocks (tbc_blocks_validate):
+        one tbc_block_check code per block (0 = valid)."""
+        n = len(ptrs)
+        P = (ctypes.c_void_p * max(1, n))(*ptrs)
+        C = np.zeros(2 * max(1, n), dtype=np.uint64)
+        for i, c in enumerate(expect_checksums):
+            C[2 * i], C[2 * i + 1] = c & ((1 << 64) - 1), c >> 64
+        A = np.asarray(list(expect_addresses) + [0], dtype=np.uint64)
+        out = np.zeros(max(1, n), dtype=np.uint8)
+        check(lib().tbc_blocks_validate(self.handle, P, C.ctypes.data, A.ctypes.data, n, out.ctypes.data),
+              "tbc_blocks_validate")
+        return out[:n]
+
     def sort_values(self, tree: TreeSpec, buf: DeviceBuffer, count: int, sync: bool = True) -> None:
         t = tree.ctype()
         f = lib().tbc_sort_values if sync else lib().tbc_sort_values_async
