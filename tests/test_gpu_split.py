@@ -1,0 +1,126 @@
+"""Key-range split of one compaction on the GPU (tigerbeetle_amd/split.py,
+SURVEY.md §8e.2): every rank runs compact_split through libtbc.so; the tables
+each rank writes must equal, byte for byte, the same tables of the oracle's
+unsplit job. Ranks share the box's one GPU (one process and engine each) and
+exchange counts and heads over gloo; on an 8-GPU node the same code runs with
+the nccl backend (RCCL over xGMI) and device buffers."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # 1 MiB blocks: an immutable transfers.id table into 2 level-B tables (4 output tables)
+    "id_1mib": ("transfers.id", 1 << 20, None, dict(n_a=262_080, b_table_sizes=[262_080, 200_000],
+                                                    a_immutable=True, dup_frac=0.02, overlap=0.3)),
+    # 4 KiB blocks, small tables: many tables, heads crossing empty ranks
+    "debit_4k": ("transfers.debit_account_id", 4096, 3, dict(n_a=3000, b_table_sizes=[900, 800],
+                                                              a_immutable=True, dup_frac=0.2, overlap=0.2)),
+    "acct_last_level_4k": ("accounts.timestamp", 4096, 3, dict(n_a=400, b_table_sizes=[200, 150],
+                                                               a_immutable=False, tomb_frac=0.1,
+                                                               drop_tombstones=True, overlap=0.5)),
+}
+
+
+def _inputs(name):
+    from tigerbeetle_amd import trees, workloads
+    tree, bs, tables, kw = CASES[name]
+    spec = trees.BY_NAME[tree]
+    if tables:
+        spec = trees.with_table_size(spec, tables * (bs - 256) // spec.value_size + 5)
+    rng = np.random.default_rng(sum(map(ord, name)))
+    ji = workloads.make_job_inputs(spec, rng, **kw)
+    n = len(ji.a_values) + sum(len(t) for t in ji.b_tables)
+    addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, n, bs) + 2, rng, 77, 0.05)
+    return spec, bs, ji, addrs
+
+
+def _run_rank(name, rank, world, exchange):
+    """compact_split on this rank; returns (ok, message)."""
+    from helpers import disk_image, run_oracle
+    from oracle import oracle
+    from tigerbeetle_amd import Engine, split, workloads
+    from tigerbeetle_amd.engine import Job, stage_blocks
+    spec, bs, ji, addrs = _inputs(name)
+    with Engine(device=0, block_size=bs) as eng:
+        lay = eng.layout(spec)
+        vcm, dbcm = lay.block_value_count_max, lay.data_block_count_max
+        if ji.a_immutable:
+            abuf = eng.upload(ji.a_values) if len(ji.a_values) else None
+            segs_a = [(abuf.ptr, len(ji.a_values))] if abuf else []
+        else:
+            abuf, segs_a = stage_blocks(eng, [workloads.split_blocks(ji.a_values, vcm)], spec.value_size, bs)
+        bbuf, segs_b = stage_blocks(eng, [workloads.split_blocks(t, vcm) for t in ji.b_tables], spec.value_size, bs)
+        job = Job(spec, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48,
+                  np.asarray(addrs, dtype=np.uint64), None)
+        b_all = np.concatenate(ji.b_tables)
+        cuts = split.split_points(workloads.keys_of(ji.a_values, spec), len(ji.a_values),
+                                  workloads.keys_of(b_all, spec), len(b_all), world)
+        res = split.compact_split(eng, job, cuts, exchange, rank)
+        whole = run_oracle(oracle, ji, bs, addrs)
+        assert whole.status == 0
+        t0, t1 = res.tables
+        if t0 == t1:
+            return True, f"rank {rank}: no tables"
+        lo, hi = split.table_address_range(t0, t1, res.plan.total, vcm, dbcm)
+        if res.plan.total != whole.value_count:
+            return False, f"rank {rank}: total {res.plan.total} != {whole.value_count}"
+        got = res.blocks.download((hi - lo) * bs).reshape(-1, bs)
+        for k in range(hi - lo):
+            if not np.array_equal(disk_image(got[k]), disk_image(whole.blocks[lo + k])):
+                return False, f"rank {rank}: block {lo + k} differs"
+        if not np.array_equal(res.table_infos, whole.table_infos[t0:t1]):
+            return False, f"rank {rank}: TableInfo differs"
+        return True, f"rank {rank}: tables {t0}..{t1} OK"
+
+
+def test_split_single_rank_reblocks_bit_exact():
+    from tigerbeetle_amd import split
+    ok, msg = _run_rank("debit_4k", 0, 1, split.SingleRank())
+    assert ok, msg
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(name, rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tigerbeetle_amd import split
+    try:
+        q.put(_run_rank(name, rank, world, split.TorchExchange(dist)))
+    except Exception as e:  # report, do not hang the other ranks' queue reads
+        q.put((False, f"rank {rank}: {type(e).__name__}: {e}"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,world", [("id_1mib", 2), ("debit_4k", 3), ("acct_last_level_4k", 4)])
+def test_split_ranks_bit_exact(name, world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(name, r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=150) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert all(ok for ok, _ in out), [m for _, m in out]
+    assert all(p.exitcode == 0 for p in procs)
