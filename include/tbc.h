@@ -99,13 +99,19 @@ typedef struct tbc_segment {
     uint32_t reserved;
 } tbc_segment;
 
+/* tbc_compaction.flags. VALUES_ONLY: the survivors only — data-block bodies
+ * (values at +256 of each data-block slot) and the result counts; no headers,
+ * checksums, index blocks or TableInfos. Phase 1 of a job split by key range
+ * across GPUs (tigerbeetle_amd/split.py); every job of a batch must agree. */
+#define TBC_COMPACTION_VALUES_ONLY 1u
+
 /* One `Compaction.start(Context)` (src/lsm/compaction.zig:84-99, 280-404). */
 typedef struct tbc_compaction {
     tbc_tree tree;
     uint8_t a_immutable;     /* 1: table_info_a = .immutable (sorted TableMemory values, one segment) */
     uint8_t drop_tombstones; /* Manifest.compaction_must_drop_tombstones (manifest.zig:547-574) */
     uint8_t level_b;         /* Context.level_b (manifest label of the output tables) */
-    uint8_t reserved0;
+    uint8_t flags;           /* TBC_COMPACTION_* (0 for a reference compaction) */
     uint32_t reserved1;
     const tbc_segment *segments_a; /* host array; A's data blocks in key order (or 1 immutable segment) */
     uint32_t segment_count_a;

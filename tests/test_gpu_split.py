@@ -124,3 +124,45 @@ def test_split_ranks_bit_exact(name, world):
             p.kill()
     assert all(ok for ok, _ in out), [m for _, m in out]
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("bs,name", [(4096, "debit_4k"), (1 << 20, "id_1mib")])
+def test_values_only_bodies_equal_full_compaction(bs, name):
+    """TBC_COMPACTION_VALUES_ONLY (split phase 1): the data-block bodies and
+    result counts of a full compaction; headers, checksums and index blocks
+    are not written."""
+    from helpers import gpu_run
+    from tigerbeetle_amd import Engine, abi, split
+    from tigerbeetle_amd.engine import Job, stage_blocks
+    from tigerbeetle_amd import workloads
+    spec, bs, ji, addrs = _inputs(name)
+    with Engine(device=0, block_size=bs) as eng:
+        (full, _, blocks), = gpu_run(eng, [ji], bs, [addrs])[0]
+        lay = eng.layout(spec)
+        vcm, dbcm = lay.block_value_count_max, lay.data_block_count_max
+        abuf = eng.upload(ji.a_values)
+        bbuf, segs_b = stage_blocks(eng, [workloads.split_blocks(t, vcm) for t in ji.b_tables], spec.value_size, bs)
+        out = eng.alloc(len(addrs) * bs)
+        out.zero()
+        job = Job(spec, [(abuf.ptr, len(ji.a_values))], segs_b, True, ji.drop_tombstones, 1, 0x1234, 48,
+                  np.asarray(addrs, dtype=np.uint64), out, flags=abi.COMPACTION_VALUES_ONLY)
+        b = eng.submit([job])
+        b.wait()
+        r, infos = b.result(0)
+        b.release()
+        assert (r.status, r.value_count, r.data_block_count, r.table_count) == \
+            (0, full.value_count, full.data_block_count, full.table_count)
+        got = out.download(full.block_count * bs).reshape(-1, bs)
+        vs = spec.value_size
+        for k in range(full.data_block_count):
+            slot = k + k // dbcm
+            n = min(vcm, full.value_count - k * vcm)
+            assert np.array_equal(got[slot, 256:256 + n * vs], blocks[slot, 256:256 + n * vs]), k
+            assert not got[slot, :256].any()
+        for t in range(full.table_count):
+            assert not got[min((t + 1) * (dbcm + 1), full.block_count) - 1].any()
+        # mixed flags in one batch are refused
+        job2 = Job(spec, [(abuf.ptr, len(ji.a_values))], segs_b, True, ji.drop_tombstones, 1, 0x1234, 48,
+                   np.asarray(addrs, dtype=np.uint64), out)
+        with pytest.raises(Exception):
+            eng.submit([job, job2])

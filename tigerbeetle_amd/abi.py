@@ -29,6 +29,7 @@ STATUS_NAMES = {
 KEY_TIMESTAMP, KEY_ID_U128, KEY_COMPOSITE_U64, KEY_COMPOSITE_U128 = 0, 1, 2, 3
 USAGE_GENERAL, USAGE_SECONDARY_INDEX = 0, 1
 CONFIG_PROFILE = 1
+COMPACTION_VALUES_ONLY = 1  # tbc_compaction.flags
 
 
 class TbcError(RuntimeError):
@@ -86,7 +87,7 @@ class Compaction(ctypes.Structure):
         ("a_immutable", ctypes.c_uint8),
         ("drop_tombstones", ctypes.c_uint8),
         ("level_b", ctypes.c_uint8),
-        ("reserved0", ctypes.c_uint8),
+        ("flags", ctypes.c_uint8),
         ("reserved1", ctypes.c_uint32),
         ("segments_a", ctypes.POINTER(Segment)),
         ("segment_count_a", ctypes.c_uint32),

@@ -1098,10 +1098,22 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
-                  const uint32_t *d_block_tile, const SplitDesc *d_splits, void *stream,
+                  const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
+    if (values_only) {
+        // Survivors only (TBC_COMPACTION_VALUES_ONLY): the bodies, no chains
+        // and no index blocks.
+        if (total_dblocks) {
+            const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+            hipLaunchKernelGGL(k_assemble, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                               d_masks, d_splits, d_ready);
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
+        if (mark) mark(mark_ctx, "assemble");
+        return 0;
+    }
     if (total_dblocks && waves <= kFusedMaxChainWaves) {
         // Latency regime: every chain is in flight at once; producers fill
         // the bodies while the chains absorb them.

@@ -373,6 +373,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     std::vector<JobDesc> hj(count);
     std::vector<uint32_t> order(count);
     uint64_t seg_words = 0, addr_words = 0;
+    const uint8_t flags0 = count ? jobs_in[0].flags : 0;
     for (uint32_t i = 0; i < count; i++) {
         const tbc_compaction &c = jobs_in[i];
         JobDesc &d = hj[i];
@@ -381,7 +382,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         if (!compute_layout(&c.tree, e->block_size, &L) || L.index_size > kIndexLdsMax ||
             (c.a_immutable && c.segment_count_a > 1) || !c.output_blocks ||
             (c.segment_count_a && !c.segments_a) || (c.segment_count_b && !c.segments_b) ||
-            (c.address_count && !c.addresses)) {
+            (c.address_count && !c.addresses) || (c.flags & ~TBC_COMPACTION_VALUES_ONLY) || c.flags != flags0) {
             delete b;
             return TBC_ERR_INVALID_ARGUMENT;
         }
@@ -575,7 +576,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
                           d_order, d_res, s, mark_cb, b) == 0;
     if (ok && count)
         ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
-                           d_block_tile, d_splits, s, mark_cb, b) == 0;
+                           d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0, s, mark_cb, b) == 0;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     if (!ok) {

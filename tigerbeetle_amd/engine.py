@@ -69,6 +69,7 @@ class Job:
     snapshot_min: int
     addresses: np.ndarray  # uint64, acquire order
     output: DeviceBuffer
+    flags: int = 0  # TBC_COMPACTION_* (abi.COMPACTION_VALUES_ONLY)
     _keep: list = field(default_factory=list)
     _ctype: object = field(default=None, repr=False)
 
@@ -83,6 +84,7 @@ class Job:
         c.a_immutable = int(self.a_immutable)
         c.drop_tombstones = int(self.drop_tombstones)
         c.level_b = self.level_b
+        c.flags = self.flags
         sa, sb = _segment_table(self.segments_a), _segment_table(self.segments_b)
         addrs = np.ascontiguousarray(self.addresses, dtype=np.uint64)
         self._keep = [sa, sb, addrs]

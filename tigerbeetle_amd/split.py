@@ -12,8 +12,8 @@ blocks (compaction.zig:806-886), counted from the job's first survivor. So:
 1. `split_points`: P-1 splitter keys by merge-path co-ranking over A ∪ B
    (A-first on equal keys, like the reference's merge), cuts moved back to the
    start of the splitter's equal-key run. Every rank computes the same cuts.
-2. Phase 1: each rank compacts its key range (any block addresses) and takes
-   its survivor count c_p: the survivors are the data-block bodies.
+2. Phase 1: each rank compacts its key range values-only (bodies in scratch
+   data-block slots, no headers or checksums) and takes its survivor count c_p.
 3. Exchange (the only collective): all-gather of the counts c_p, then of each
    rank's head survivors — the ones the previous table owner still needs to
    complete a table that starts before this rank's range (≤ one table).
@@ -24,15 +24,19 @@ blocks (compaction.zig:806-886), counted from the job's first survivor. So:
    tables. The blocks, index blocks, checksums and TableInfos are therefore
    byte-identical to the unsplit job's (tested against the oracle).
 
-Phase 1's checksums are wasted work (a values-only phase 1 is a later
-optimisation); splitting one job pays off only when a job is larger than a
-GPU's share of the half-bar, which no BASELINE config needs.
+Phase 1 runs with TBC_COMPACTION_VALUES_ONLY (merge + body assembly, no AEGIS
+chains or index blocks), so the split costs one extra HBM pass over the
+survivors, not a second set of checksums. Splitting one job pays off only when
+a job is larger than a GPU's share of the half-bar, which no BASELINE config
+needs.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
 
 import numpy as np
+
+from .abi import COMPACTION_VALUES_ONLY
 
 HEADER_SIZE = 256
 
@@ -260,7 +264,7 @@ def compact_split(engine, job, cuts: list, exchange, rank: int) -> SplitResult:
     nblocks = db + -(-db // dbcm)
     out1 = engine.alloc(max(1, nblocks) * bs)
     p1 = Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
-             job.snapshot_min, np.arange(1, nblocks + 1, dtype=np.uint64), out1)
+             job.snapshot_min, np.arange(1, nblocks + 1, dtype=np.uint64), out1, flags=COMPACTION_VALUES_ONLY)
     b1 = engine.submit([p1])
     b1.wait()
     r1, _ = b1.result(0)
