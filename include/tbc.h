@@ -196,6 +196,19 @@ typedef struct tbc_sort_job {
 } tbc_sort_job;
 tbc_status tbc_sort_values_batch(tbc_engine *engine, const tbc_sort_job *jobs, uint32_t count);
 
+/* ---- scan path: k-way merge ------------------------------------------------
+ * Replaces KWayMergeIteratorType(...).init + pop-until-null
+ * (src/lsm/k_way_merge.zig:8-205) with stream_precedence(a, b) = a > b (the
+ * reference's own tests, :239-244: a higher stream index wins on equal keys;
+ * order streams oldest -> newest). Each stream holds `count` values (device,
+ * 16-byte aligned) sorted by key_from_value in the merge direction, possibly
+ * with repeated keys; the merged values (one per key: the first of the
+ * winning stream's run) are written to `out_values` (device, capacity = the
+ * streams' total) and their number to *out_count. Synchronous. */
+#define TBC_KWAY_STREAMS_MAX 64u
+tbc_status tbc_kway_merge(tbc_engine *engine, const tbc_tree *tree, const tbc_segment *streams, uint32_t stream_count,
+                          uint32_t descending, void *out_values, uint64_t *out_count);
+
 /* ---- compaction ------------------------------------------------------------- */
 /* Enqueue `count` independent compactions (one half-bar's jobs) as one batch.
  * All input/output device memory must stay valid until the batch completes. */

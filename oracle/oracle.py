@@ -192,3 +192,95 @@ def compact(t: Tree, a_segments, b_segments, *, a_immutable: bool, drop_tombston
     return CompactionResult(rc, out_blocks[: job.out_block_count],
                             out_infos[: job.out_table_count], job.out_value_count,
                             job.out_data_block_count)
+
+
+def kway_merge(streams: list, descending: bool = False) -> list:
+    """KWayMergeIteratorType (src/lsm/k_way_merge.zig:8-205), restated line by
+    line as a binary heap over stream heads, with the reference tests'
+    stream_precedence(a, b) = a > b (:239-244). `streams` are lists of
+    (key, payload), each sorted in the merge direction; returns the popped
+    (key, payload) list. Pure Python: small inputs (test checker only)."""
+    streams = [list(s) for s in streams]
+    pos = [0] * len(streams)
+    keys, ids = [None] * len(streams), [0] * len(streams)
+    k = 0
+
+    def peek(s):  # stream_peek: None = error.Empty (no Drained: all data resident)
+        return streams[s][pos[s]][0] if pos[s] < len(streams[s]) else None
+
+    def ordered(a, b):  # :197-203
+        if b is None:
+            return True
+        ka, kb = keys[a], keys[b]
+        if ka == kb:
+            return ids[a] > ids[b]
+        return (ka < kb) != descending
+
+    def swap(a, b):
+        keys[a], keys[b] = keys[b], keys[a]
+        ids[a], ids[b] = ids[b], ids[a]
+
+    def up_heap(i):  # :134-140
+        while i > 0:
+            p = (i - 1) // 2
+            if ordered(p, i):
+                break
+            swap(p, i)
+            i = p
+
+    def down_heap():  # :145-175
+        if k == 0:
+            return
+        i = 0
+        for _ in range(k.bit_length()):
+            left = 2 * i + 1 if 2 * i + 1 < k else None
+            right = 2 * i + 2 if 2 * i + 2 < k else None
+            if ordered(i, left):
+                if ordered(i, right):
+                    break
+                swap(i, right)
+                i = right
+            elif ordered(i, right):
+                swap(i, left)
+                i = left
+            elif ordered(left, right):
+                swap(i, left)
+                i = left
+            else:
+                swap(i, right)
+                i = right
+
+    for s in range(len(streams)):  # init, :71-82
+        key = peek(s)
+        if key is None:
+            continue
+        keys[k], ids[k] = key, s
+        up_heap(k)
+        k += 1
+
+    out, previous = [], None
+    while True:
+        # pop_internal, :109-132: re-key the root from its stream's current
+        # head (the value popped last time came from it), then pop the root.
+        if k == 0:
+            break
+        s0 = ids[0]
+        key = peek(s0)
+        if key is not None:
+            keys[0] = key
+            down_heap()
+        else:
+            swap(0, k - 1)
+            k -= 1
+            down_heap()
+        if k == 0:
+            break
+        root = ids[0]
+        value = streams[root][pos[root]]
+        pos[root] += 1
+        # pop, :91-107
+        if previous is not None and value[0] == previous:
+            continue
+        previous = value[0]
+        out.append(value)
+    return out

@@ -358,6 +358,51 @@ tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, ui
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
+tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams, uint32_t stream_count,
+                          uint32_t descending, void *out_values, uint64_t *out_count) {
+    Layout L;
+    if (!e || !tree || !out_count || (stream_count && !streams) || stream_count > TBC_KWAY_STREAMS_MAX ||
+        !compute_layout(tree, e->block_size, &L) || ((uintptr_t)out_values & 15))
+        return TBC_ERR_INVALID_ARGUMENT;
+    *out_count = 0;
+    uint64_t n = 0;
+    std::vector<uint64_t> tab(2 * (size_t)stream_count + 2, 0); // value pointers, then u32 prefix counts
+    uint32_t *pre = (uint32_t *)(tab.data() + stream_count);
+    for (uint32_t s = 0; s < stream_count; s++) {
+        if (streams[s].count && (!streams[s].values || ((uintptr_t)streams[s].values & 15)))
+            return TBC_ERR_INVALID_ARGUMENT;
+        tab[s] = (uint64_t)(uintptr_t)streams[s].values;
+        pre[s] = (uint32_t)n;
+        n += streams[s].count;
+    }
+    if (n >= 0x7fffffffull) return TBC_ERR_INVALID_ARGUMENT;
+    pre[stream_count] = (uint32_t)n;
+    if (!n) return TBC_OK;
+    if (!out_values) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    const uint64_t tab_bytes = align_up(8ull * tab.size(), 256), flag_bytes = align_up(4 * (n + 1), 256);
+    const size_t cub_bytes = kway_scan_tmp_bytes((uint32_t)n);
+    const uint64_t dt = e->dev.top;
+    uint8_t *d = e->dev.alloc(tab_bytes + 2 * flag_bytes + align_up(cub_bytes, 256) + 256);
+    if (!d) return TBC_ERR_OUT_OF_MEMORY;
+    uint32_t *flags = (uint32_t *)(d + tab_bytes), *scan = (uint32_t *)(d + tab_bytes + flag_bytes);
+    void *cub = d + tab_bytes + 2 * flag_bytes;
+    tbc_status st = TBC_OK;
+    if (hipMemcpyAsync(d, tab.data(), 8 * tab.size(), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        launch_kway(tree->key_kind, descending != 0, (const uint64_t *)d, (const uint32_t *)(d + 8ull * stream_count),
+                    stream_count, (uint32_t)n, tree->value_size, tree->timestamp_offset, flags, scan, cub, cub_bytes,
+                    (uint8_t *)out_values, e->stream) != 0)
+        st = TBC_ERR_DEVICE;
+    uint32_t total = 0;
+    if (st == TBC_OK && (hipMemcpyAsync(&total, scan + n, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+                         hipStreamSynchronize(e->stream) != hipSuccess))
+        st = TBC_ERR_DEVICE;
+    if (st != TBC_OK) hipStreamSynchronize(e->stream);
+    e->dev.top = dt;
+    *out_count = total;
+    return st;
+}
+
 tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;

@@ -249,6 +249,19 @@ class Engine:
             arr[i].count = n
         check(lib().tbc_sort_values_batch(self.handle, arr, len(tables)), "tbc_sort_values_batch")
 
+    def kway_merge(self, tree: TreeSpec, streams: list, out: DeviceBuffer, descending: bool = False) -> int:
+        """Scan-path k-way merge (tbc_kway_merge; k_way_merge.zig:8-205 with a
+        higher stream index winning equal keys): `streams` = [(device ptr,
+        count)] sorted in the merge direction; returns the merged count."""
+        arr = (abi.Segment * max(1, len(streams)))()
+        for i, (p, n) in enumerate(streams):
+            arr[i].values, arr[i].count = p, n
+        t = tree.ctype()
+        n_out = ctypes.c_uint64()
+        check(lib().tbc_kway_merge(self.handle, ctypes.byref(t), arr, len(streams), int(descending),
+                                   out.ptr if out is not None else None, ctypes.byref(n_out)), "tbc_kway_merge")
+        return n_out.value
+
     def prepare(self, jobs: list):
         """The tbc_compaction[] array of a job list (cached for a repeated list)."""
         key = tuple(id(j) for j in jobs)
