@@ -284,3 +284,35 @@ def kway_merge(streams: list, descending: bool = False) -> list:
         previous = value[0]
         out.append(value)
     return out
+
+
+def manifest_blocks(table_infos: np.ndarray, addresses, cluster: int, block_size: int,
+                    previous_checksum: int = 0, previous_address: int = 0):
+    """ManifestLog.acquire_block/append/close_block (src/lsm/manifest_log.zig:
+    876-952) with schema.ManifestNode (src/lsm/schema.zig:451-595), restated
+    on the CPU with this oracle's KAT-pinned vsr.checksum. Returns (disk
+    images [0, sector_ceil(size)), header checksums)."""
+    infos = np.ascontiguousarray(table_infos, dtype=np.uint8).reshape(-1, 128)
+    entry_max = (block_size - 256) // 128                      # schema.zig:454
+    out, sums = [], []
+    prev_c, prev_a = int(previous_checksum), int(previous_address)
+    for b, start in enumerate(range(0, len(infos), entry_max)):
+        chunk = infos[start:start + entry_max]
+        size = 256 + 128 * len(chunk)                          # ManifestNode.size, :574-580
+        blk = bytearray(-(-size // 4096) * 4096)
+        blk[80:96] = int(cluster).to_bytes(16, "little")       # header.cluster (:893)
+        blk[96:100] = size.to_bytes(4, "little")               # header.size (:921)
+        blk[110] = 20                                          # command = .block
+        blk[128:144] = prev_c.to_bytes(16, "little")           # Metadata (:925-929, schema.zig:475-486)
+        blk[160:168] = prev_a.to_bytes(8, "little")
+        blk[168:172] = len(chunk).to_bytes(4, "little")
+        blk[224:232] = int(addresses[b]).to_bytes(8, "little")  # header.address (:889,894)
+        blk[240] = 3                                           # block_type = .manifest
+        blk[256:size] = chunk.tobytes()
+        blk[32:48] = checksum(bytes(blk[256:size])).to_bytes(16, "little")   # set_checksum_body (:934)
+        c = checksum(bytes(blk[16:256]))                       # set_checksum (:935)
+        blk[0:16] = c.to_bytes(16, "little")
+        out.append(np.frombuffer(bytes(blk), np.uint8))
+        sums.append(c)
+        prev_c, prev_a = c, int(addresses[b])                  # log_block_checksums/addresses push (:938-939)
+    return out, sums
