@@ -366,17 +366,22 @@ tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment
         return TBC_ERR_INVALID_ARGUMENT;
     *out_count = 0;
     uint64_t n = 0;
-    std::vector<uint64_t> tab(2 * (size_t)stream_count + 2, 0); // value pointers, then u32 prefix counts
-    uint32_t *pre = (uint32_t *)(tab.data() + stream_count);
+    // value pointers, then u32 prefix counts of values and of 256-value tiles
+    std::vector<uint64_t> tab(2 * (size_t)stream_count + 2, 0);
+    uint32_t *pre = (uint32_t *)(tab.data() + stream_count), *tile_pre = pre + stream_count + 1;
+    uint32_t tiles = 0;
     for (uint32_t s = 0; s < stream_count; s++) {
         if (streams[s].count && (!streams[s].values || ((uintptr_t)streams[s].values & 15)))
             return TBC_ERR_INVALID_ARGUMENT;
         tab[s] = (uint64_t)(uintptr_t)streams[s].values;
         pre[s] = (uint32_t)n;
+        tile_pre[s] = tiles;
         n += streams[s].count;
+        tiles += (streams[s].count + 255) / 256;
     }
     if (n >= 0x7fffffffull) return TBC_ERR_INVALID_ARGUMENT;
     pre[stream_count] = (uint32_t)n;
+    tile_pre[stream_count] = tiles;
     if (!n) return TBC_OK;
     if (!out_values) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
@@ -390,7 +395,7 @@ tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment
     tbc_status st = TBC_OK;
     if (hipMemcpyAsync(d, tab.data(), 8 * tab.size(), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         launch_kway(tree->key_kind, descending != 0, (const uint64_t *)d, (const uint32_t *)(d + 8ull * stream_count),
-                    stream_count, (uint32_t)n, tree->value_size, tree->timestamp_offset, flags, scan, cub, cub_bytes,
+                    (const uint32_t *)(d + 8ull * stream_count) + stream_count + 1, tiles, stream_count, (uint32_t)n, tree->value_size, tree->timestamp_offset, flags, scan, cub, cub_bytes,
                     (uint8_t *)out_values, e->stream) != 0)
         st = TBC_ERR_DEVICE;
     uint32_t total = 0;

@@ -13,13 +13,15 @@
 //                                 s' whose key comes before it (direction order).
 //
 // Kernels: emit flags (binary searches in the higher streams) -> exclusive scan
-// of the flags (hipCUB) -> scatter (one binary search per stream). Each
+// of the flags (hipCUB) -> scatter (one binary search per stream), both
+// searching only a per-tile window of each other stream. Each
 // element is read once per kernel plus O(k log n) key probes; the scatter
 // moves each emitted value once (16-byte copies).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include "keys.h"
+#include "tbc.h"
 
 namespace tbc {
 
@@ -41,72 +43,111 @@ __device__ __forceinline__ uint32_t kway_lower_bound(const uint8_t *v, uint32_t 
     return lo;
 }
 
-__device__ __forceinline__ uint32_t stream_of(const uint32_t *pre, uint32_t k, uint32_t g) {
-    uint32_t s = 0;
-    while (s + 1 < k && gld<uint32_t>(pre + s + 1) <= g) s++;
-    return s;
+constexpr uint32_t kKwayTile = 256;
+
+// Workgroups take 256 consecutive values of ONE stream (tiles never straddle
+// streams). The lower bounds of any key of the tile in another stream t lie
+// between those of the tile's first and last keys, so lanes 0..k-1 search
+// those two once and every thread then searches only that window (usually a
+// few hundred values, cache-resident) instead of the whole stream.
+struct KwayTile {
+    uint32_t s, i0, n_s;
+};
+
+__device__ __forceinline__ KwayTile kway_tile(const uint32_t *pre, const uint32_t *tile_pre, uint32_t k) {
+    KwayTile t{0, 0, 0};
+    while (t.s + 1 < k && gld<uint32_t>(tile_pre + t.s + 1) <= blockIdx.x) t.s++;
+    t.i0 = (blockIdx.x - gld<uint32_t>(tile_pre + t.s)) * kKwayTile;
+    t.n_s = gld<uint32_t>(pre + t.s + 1) - gld<uint32_t>(pre + t.s);
+    return t;
 }
 
 template <int KIND, bool DESC>
-__global__ __launch_bounds__(256) void k_kway_flags(const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t n,
-                                                    uint32_t vs, uint32_t ts, uint32_t *flags) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g > n) return;
-    if (g == n) { // the scan's total lands in flags[n]'s slot
-        gst<uint32_t>(flags + n, 0u);
-        return;
+__device__ __forceinline__ void kway_windows(const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t vs,
+                                             uint32_t ts, const KwayTile &tl, uint32_t *lo, uint32_t *hi) {
+    const uint32_t t = threadIdx.x;
+    if (t < k && t != tl.s) {
+        const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + tl.s);
+        const uint32_t last = min(tl.i0 + kKwayTile, tl.n_s) - 1;
+        const uint8_t *w = (const uint8_t *)gld<uint64_t>(ptr + t);
+        const uint32_t len = gld<uint32_t>(pre + t + 1) - gld<uint32_t>(pre + t);
+        lo[t] = kway_lower_bound<KIND, DESC>(w, len, vs, ts, load_key<KIND>(v + (size_t)tl.i0 * vs, ts));
+        hi[t] = kway_lower_bound<KIND, DESC>(w, len, vs, ts, load_key<KIND>(v + (size_t)last * vs, ts));
     }
-    const uint32_t s = stream_of(pre, k, g);
-    const uint32_t i = g - gld<uint32_t>(pre + s);
-    const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + s);
+    __syncthreads();
+}
+
+// lower bound of `key` in stream t, known to lie in [lo, hi].
+template <int KIND, bool DESC, int KL = KeyLimbs<KIND>::value>
+__device__ __forceinline__ uint32_t kway_window_search(const uint8_t *w, uint32_t lo, uint32_t hi, uint32_t vs,
+                                                       uint32_t ts, const Key<KL> &key) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (before<KIND, DESC>(load_key<KIND>(w + (size_t)mid * vs, ts), key)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int KIND, bool DESC>
+__global__ __launch_bounds__(256) void k_kway_flags(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
+                                                    uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags) {
+    __shared__ uint32_t lo[TBC_KWAY_STREAMS_MAX], hi[TBC_KWAY_STREAMS_MAX];
+    const KwayTile tl = kway_tile(pre, tile_pre, k);
+    kway_windows<KIND, DESC>(ptr, pre, k, vs, ts, tl, lo, hi);
+    const uint32_t i = tl.i0 + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) gst<uint32_t>(flags + n, 0u); // the scan's total lands there
+    if (i >= tl.n_s) return;
+    const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + tl.s);
     const auto key = load_key<KIND>(v + (size_t)i * vs, ts);
     bool emit = i == 0 || !key_eq(load_key<KIND>(v + (size_t)(i - 1) * vs, ts), key);
-    for (uint32_t t = s + 1; emit && t < k; t++) {
-        const uint32_t base = gld<uint32_t>(pre + t), len = gld<uint32_t>(pre + t + 1) - base;
+    for (uint32_t t = tl.s + 1; emit && t < k; t++) {
+        const uint32_t len = gld<uint32_t>(pre + t + 1) - gld<uint32_t>(pre + t);
         const uint8_t *w = (const uint8_t *)gld<uint64_t>(ptr + t);
-        const uint32_t j = kway_lower_bound<KIND, DESC>(w, len, vs, ts, key);
+        const uint32_t j = kway_window_search<KIND, DESC>(w, lo[t], hi[t], vs, ts, key);
         if (j < len && key_eq(load_key<KIND>(w + (size_t)j * vs, ts), key)) emit = false;
     }
-    gst<uint32_t>(flags + g, emit ? 1u : 0u);
+    gst<uint32_t>(flags + gld<uint32_t>(pre + tl.s) + i, emit ? 1u : 0u);
 }
 
 template <int KIND, bool DESC>
-__global__ __launch_bounds__(256) void k_kway_scatter(const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t n,
-                                                      uint32_t vs, uint32_t ts, const uint32_t *flags,
+__global__ __launch_bounds__(256) void k_kway_scatter(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
+                                                      uint32_t k, uint32_t vs, uint32_t ts, const uint32_t *flags,
                                                       const uint32_t *scan, uint8_t *out) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n || !gld<uint32_t>(flags + g)) return;
-    const uint32_t s = stream_of(pre, k, g);
-    const uint32_t i = g - gld<uint32_t>(pre + s);
-    const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + s) + (size_t)i * vs;
+    __shared__ uint32_t lo[TBC_KWAY_STREAMS_MAX], hi[TBC_KWAY_STREAMS_MAX];
+    const KwayTile tl = kway_tile(pre, tile_pre, k);
+    kway_windows<KIND, DESC>(ptr, pre, k, vs, ts, tl, lo, hi);
+    const uint32_t i = tl.i0 + threadIdx.x;
+    if (i >= tl.n_s || !gld<uint32_t>(flags + gld<uint32_t>(pre + tl.s) + i)) return;
+    const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + tl.s) + (size_t)i * vs;
     const auto key = load_key<KIND>(v, ts);
     uint32_t pos = 0;
     for (uint32_t t = 0; t < k; t++) {
-        const uint32_t base = gld<uint32_t>(pre + t), len = gld<uint32_t>(pre + t + 1) - base;
-        const uint32_t j = t == s ? i : kway_lower_bound<KIND, DESC>((const uint8_t *)gld<uint64_t>(ptr + t), len, vs, ts, key);
+        const uint32_t base = gld<uint32_t>(pre + t);
+        const uint32_t j = t == tl.s ? i
+                                     : kway_window_search<KIND, DESC>((const uint8_t *)gld<uint64_t>(ptr + t), lo[t],
+                                                                      hi[t], vs, ts, key);
         pos += gld<uint32_t>(scan + base + j) - gld<uint32_t>(scan + base);
     }
     uint8_t *d = out + (size_t)pos * vs;
     for (uint32_t o = 0; o < vs; o += 16) { // 16-byte moves (value sizes are multiples of 16)
-        const uint64_t lo = gld<uint64_t>(v + o), hi = gld<uint64_t>(v + o + 8);
-        gst<uint64_t>(d + o, lo);
-        gst<uint64_t>(d + o + 8, hi);
+        const uint64_t a = gld<uint64_t>(v + o), b = gld<uint64_t>(v + o + 8);
+        gst<uint64_t>(d + o, a);
+        gst<uint64_t>(d + o + 8, b);
     }
 }
 
 template <int KIND, bool DESC>
-static int launch_kway_t(const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t n, uint32_t vs, uint32_t ts,
-                         uint32_t *flags, uint32_t *scan, void *cub_tmp, size_t cub_bytes, uint8_t *out, hipStream_t s) {
-    const uint32_t grid1 = (n + 1 + 255) / 256, grid2 = (n + 255) / 256;
-    hipLaunchKernelGGL((k_kway_flags<KIND, DESC>), dim3(grid1), dim3(256), 0, s, ptr, pre, k, n, vs, ts, flags);
+static int launch_kway_t(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre, uint32_t tiles, uint32_t k,
+                         uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan, void *cub_tmp,
+                         size_t cub_bytes, uint8_t *out, hipStream_t s) {
+    hipLaunchKernelGGL((k_kway_flags<KIND, DESC>), dim3(tiles), dim3(kKwayTile), 0, s, ptr, pre, tile_pre, k, n, vs, ts,
+                       flags);
     if (hipGetLastError() != hipSuccess) return -1;
     if (hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, flags, scan, (int)n + 1, s) != hipSuccess) return -1;
-    if (n) {
-        hipLaunchKernelGGL((k_kway_scatter<KIND, DESC>), dim3(grid2), dim3(256), 0, s, ptr, pre, k, n, vs, ts, flags,
-                           scan, out);
-        if (hipGetLastError() != hipSuccess) return -1;
-    }
-    return 0;
+    hipLaunchKernelGGL((k_kway_scatter<KIND, DESC>), dim3(tiles), dim3(kKwayTile), 0, s, ptr, pre, tile_pre, k, vs, ts,
+                       flags, scan, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 size_t kway_scan_tmp_bytes(uint32_t n) {
@@ -115,13 +156,13 @@ size_t kway_scan_tmp_bytes(uint32_t n) {
     return bytes;
 }
 
-int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t n,
-                uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan, void *cub_tmp, size_t cub_bytes,
-                uint8_t *out, void *stream) {
+int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
+                uint32_t tiles, uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan,
+                void *cub_tmp, size_t cub_bytes, uint8_t *out, void *stream) {
     hipStream_t s = (hipStream_t)stream;
 #define TBC_KWAY(KIND)                                                                                    \
-    return descending ? launch_kway_t<KIND, true>(ptr, pre, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes, out, s) \
-                      : launch_kway_t<KIND, false>(ptr, pre, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes, out, s)
+    return descending ? launch_kway_t<KIND, true>(ptr, pre, tile_pre, tiles, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes, out, s) \
+                      : launch_kway_t<KIND, false>(ptr, pre, tile_pre, tiles, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes, out, s)
     switch (key_kind) {
     case kKeyTimestamp: TBC_KWAY(kKeyTimestamp);
     case kKeyIdU128: TBC_KWAY(kKeyIdU128);

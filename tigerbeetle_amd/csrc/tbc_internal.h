@@ -142,7 +142,7 @@ struct SortItem {
 int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *stream);
 uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count);
 size_t kway_scan_tmp_bytes(uint32_t n);
-int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t n,
-                uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan, void *cub_tmp, size_t cub_bytes,
-                uint8_t *out, void *stream);
+int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
+                uint32_t tiles, uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan,
+                void *cub_tmp, size_t cub_bytes, uint8_t *out, void *stream);
 } // namespace tbc
