@@ -201,3 +201,91 @@ def test_split_exchange_over_gloo(oracle_lib, world, case):
     images = [im for _, ims, _ in out for im in ims]
     assert images == [bytes(disk_image(b)) for b in whole.blocks]
     assert b"".join(inf for _, _, inf in out) == whole.table_infos.tobytes()
+
+
+# --- TorchExchange.all_gather_heads (host-staged gloo path) on CPU -----------
+
+class _FakeBuffer:
+    def __init__(self, mem, ptr, n):
+        self.mem, self.ptr, self.nbytes = mem, ptr, n
+
+    def download(self, n):
+        return np.frombuffer(bytes(self.mem.read(self.ptr, n)), np.uint8)
+
+    def free(self):
+        pass
+
+
+class _FakeMemory:
+    """Flat byte-addressed stand-in for device memory (no GPU on this host)."""
+
+    def __init__(self):
+        self.heap = bytearray(1 << 20)
+        self.top = 4096
+
+    def alloc(self, n):
+        p = self.top
+        self.top += (n + 15) // 16 * 16
+        return p
+
+    def read(self, p, n):
+        return self.heap[p:p + n]
+
+    def write(self, p, b):
+        self.heap[p:p + len(b)] = b
+
+
+class _FakeEngine:
+    def __init__(self):
+        self.mem = _FakeMemory()
+
+    def alloc(self, n):
+        return _FakeBuffer(self.mem, self.mem.alloc(n), n)
+
+    def upload(self, a):
+        b = self.alloc(a.nbytes)
+        self.mem.write(b.ptr, a.tobytes())
+        return b
+
+    def copy_device_async(self, dst, src, n):
+        self.mem.write(dst, bytes(self.mem.read(src, n)))
+
+    def synchronize(self):
+        pass
+
+
+def _heads_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _FakeEngine()
+    vals = np.arange(100, dtype=np.uint64).reshape(-1, 2).view(np.uint8) + rank  # 50 values of 16 B
+    buf = eng.upload(vals)
+    need = [0, 7, 3][rank]
+    segs = [(buf.ptr, 16 * min(need, 4)), (buf.ptr + 64, 16 * max(0, need - 4))]  # head in two pieces
+    ex = split.TorchExchange(dist)
+    _, ptrs = ex.all_gather_heads(eng, [s for s in segs if s[1]], 7 * 16)
+    got = [bytes(eng.mem.read(p, 7 * 16)) for p in ptrs]
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_gather_heads_host_path_over_gloo():
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_heads_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        for q_ in range(world):
+            need = [0, 7, 3][q_]
+            vals = (np.arange(100, dtype=np.uint64).reshape(-1, 2).view(np.uint8) + q_).tobytes()
+            assert out[r][q_][:16 * need] == vals[:16 * need]
+            assert out[r][q_][16 * need:] == bytes(16 * (7 - need))
