@@ -307,3 +307,36 @@ def test_blocks_validate_matches_grid_read_block_validate(engine_small, oracle_l
     assert corrupt(0, 232, blocks[0][232] ^ 1, fix_header=True) == 4  # valid, but not the expected checksum
     wrong = engine_small.validate_blocks([ptrs[1]], [cks[1]], [adr[1] + 1])
     assert int(wrong[0]) == 5                                  # address mismatch
+
+
+@pytest.mark.parametrize("bs", [4096, 1 << 20])
+def test_heavy_dedup_jobs_pre_assembled(bs, engine, engine_small, oracle_lib):
+    """Jobs with < 1/4 survivors (aegis.hip sparse_job: bodies by k_assemble
+    before the fused chains) batched with dense ones; byte-exact vs oracle."""
+    eng = engine if bs == 1 << 20 else engine_small
+    rng = np.random.default_rng(0xDED0 + bs)
+    def tree(name):
+        t = trees.BY_NAME[name]
+        return t if bs == 1 << 20 else trees.with_table_size(t, 3 * (bs - 256) // t.value_size + 5)
+    acc = tree("accounts.timestamp")
+    scale = 1 if bs == 1 << 20 else 40
+    jobs = [
+        workloads.make_job_inputs(acc, rng, n_a=200_000 // scale, b_table_sizes=[20_000 // scale],
+                                  a_immutable=True, dup_frac=0.97, tomb_frac=0.02, overlap=0.5),
+        workloads.make_job_inputs(acc, rng, n_a=5_000 // scale, b_table_sizes=[400_000 // scale],
+                                  a_immutable=False, tomb_frac=0.9, drop_tombstones=True, overlap=0.0),
+        workloads.make_job_inputs(tree("transfers.id"), rng, n_a=60_000 // scale,
+                                  b_table_sizes=[70_000 // scale], a_immutable=True, dup_frac=0.05),
+    ]
+    addrs = [workloads.addresses_for(workloads.worst_case_blocks(ji.tree, len(ji.a_values) + sum(map(len, ji.b_tables)),
+                                                                 bs) + 2, rng, 50 + 1000 * i) for i, ji in enumerate(jobs)]
+    results, _ = gpu_run(eng, jobs, bs, addrs)
+    for ji, a, (r, infos, blocks) in zip(jobs, addrs, results):
+        o = run_oracle(oracle_lib, ji, bs, a)
+        assert r.status == 0 and o.status == 0 and r.value_count == o.value_count
+        assert len(blocks) == len(o.blocks)
+        for g, w in zip(blocks, o.blocks):
+            assert np.array_equal(disk_image(g), disk_image(w))
+        assert np.array_equal(infos, o.table_infos)
+    n0 = len(jobs[0].a_values) + sum(map(len, jobs[0].b_tables))
+    assert results[0][0].value_count * 4 < n0  # the sparse path was taken

@@ -632,6 +632,15 @@ struct SegCursor {
     }
 };
 
+// A job whose survivors are under a quarter of its merged positions (heavy
+// dedup, e.g. an object tree updated many times per key) leaves its survivors
+// scattered: one producer wave gathering them sequentially cannot keep ahead
+// of the chain. Such jobs' bodies are assembled beforehand by k_assemble,
+// parallel over the whole chip, and their producers only publish.
+__device__ __forceinline__ bool sparse_job(const JobDesc &j, const JobResultDev *res) {
+    return res[j.job_index].value_count * 4 < (uint64_t)(j.a.n + j.b.n);
+}
+
 __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint32_t cnt, const uint64_t *status,
                                              const uint64_t *masks, const uint32_t *block_tile,
                                              const SplitDesc *splits, uint8_t *body, uint32_t *prog,
@@ -793,6 +802,12 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
         const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
         if (!locate(mine, ji, k)) return;
         const JobDesc &j = jobs[ji];
+        if (sparse_job(j, res)) { // body written by k_assemble<true> (stream order)
+            if (lane == 0)
+                __hip_atomic_store(&sProg[p], block_count(j, k) * j.value_size, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
         uint8_t *blk = j.out_blocks + (size_t)data_block_slot(k, j.dbcm) * j.block_size;
         produce_body(j, k, block_count(j, k), status, masks, block_tile, splits, blk + kHeaderSize, &sProg[p],
                      const_cast<uint32_t *>(&res[j.job_index].invariant), sStage[Fused ? p : 0]);
@@ -866,9 +881,11 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
 // wave then copies its word's survivors cooperatively, 16 bytes per lane, so
 // consecutive lanes read and write consecutive bytes. HBM-bound: every
 // survivor is read once and written once.
+template <bool SparseOnly>
 __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs, uint32_t total_tiles,
                                                   const uint64_t *status, const uint64_t *masks,
-                                                  const SplitDesc *splits, uint32_t *ready) {
+                                                  const SplitDesc *splits, uint32_t *ready,
+                                                  const JobResultDev *res) {
     constexpr uint32_t W = kMergeTile / 64; // mask words per kind per tile
     __shared__ uint32_t s_pre[3][W + 1];    // survivors, A taken, B taken before word w
     __shared__ uint64_t s_src[4][64], s_dst[4][64];
@@ -877,6 +894,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
     for (uint32_t g = blockIdx.x; g < total_tiles; g += gridDim.x) {
         const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.tile_base; });
         const JobDesc &j = jobs[ji];
+        if (SparseOnly && !sparse_job(j, res)) continue; // uniform per workgroup
         const uint32_t t = g - j.tile_base;
         const uint32_t n = j.a.n + j.b.n, vs = j.value_size, vcm = j.vcm;
         const uint64_t *m = masks + (size_t)g * (2 * W);
@@ -1098,7 +1116,8 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
-                  const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, void *stream,
+                  const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, bool maybe_sparse,
+                  void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
@@ -1107,8 +1126,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         // and no index blocks.
         if (total_dblocks) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-            hipLaunchKernelGGL(k_assemble, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready);
+            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
             if (hipGetLastError() != hipSuccess) return -1;
         }
         if (mark) mark(mark_ctx, "assemble");
@@ -1117,6 +1136,13 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
     if (total_dblocks && waves <= kFusedMaxChainWaves) {
         // Latency regime: every chain is in flight at once; producers fill
         // the bodies while the chains absorb them.
+        if (maybe_sparse) { // heavy-dedup jobs: bodies first, parallel (sparse_job decides on device)
+            const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+            hipLaunchKernelGGL(k_assemble<true>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
+            if (hipGetLastError() != hipSuccess) return -1;
+            if (mark) mark(mark_ctx, "assemble");
+        }
         uint32_t c = waves_per_block(waves);
         c = c > kMaxChainWaves ? kMaxChainWaves : c;
         hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
@@ -1131,8 +1157,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         // The counts stay as a check: a chain whose block is short of values
         // reports an invariant error instead of checksumming a partial body.
         const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-        hipLaunchKernelGGL(k_assemble, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status, d_masks,
-                           d_splits, d_ready);
+        hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status, d_masks,
+                           d_splits, d_ready, (const JobResultDev *)d_results);
         if (hipGetLastError() != hipSuccess) return -1;
         if (mark) mark(mark_ctx, "assemble");
         const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);

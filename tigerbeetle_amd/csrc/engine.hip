@@ -424,6 +424,10 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     std::vector<uint32_t> order(count);
     uint64_t seg_words = 0, addr_words = 0;
     const uint8_t flags0 = count ? jobs_in[0].flags : 0;
+    // Dedup (immutable A) or tombstone drops can leave a job's survivors
+    // sparse; only then may the block phase pre-assemble (aegis.hip sparse_job).
+    bool maybe_sparse = false;
+    for (uint32_t i = 0; i < count; i++) maybe_sparse |= jobs_in[i].a_immutable || jobs_in[i].drop_tombstones;
     for (uint32_t i = 0; i < count; i++) {
         const tbc_compaction &c = jobs_in[i];
         JobDesc &d = hj[i];
@@ -626,7 +630,8 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
                           d_order, d_res, s, mark_cb, b) == 0;
     if (ok && count)
         ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
-                           d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0, s, mark_cb, b) == 0;
+                           d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0, maybe_sparse, s, mark_cb,
+                           b) == 0;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     if (!ok) {

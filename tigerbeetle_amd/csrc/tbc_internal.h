@@ -129,7 +129,8 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
-                  const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, void *stream,
+                  const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, bool maybe_sparse,
+                  void *stream,
                   void (*mark)(void *, const char *), void *mark_ctx);
 int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uint32_t count, uint32_t block_size,
                           uint8_t *d_out, void *stream);
