@@ -64,3 +64,9 @@ def test_gpu_manifest_blocks_equal_oracle(bs, n):
     want, wsums = oracle.manifest_blocks(_infos(n, n), addrs, CLUSTER, bs, previous_checksum=7, previous_address=3)
     assert gsums == wsums
     assert all(np.array_equal(g, w) for g, w in zip(got, want)) and len(got) == len(want)
+
+
+def test_no_entries_no_blocks():
+    # close_block asserts entry_count > 0 (manifest_log.zig:913): nothing to close
+    assert manifest.pack_blocks(np.zeros((0, 128), np.uint8), [], CLUSTER, 4096) == []
+    assert oracle.manifest_blocks(np.zeros((0, 128), np.uint8), [], CLUSTER, 4096) == ([], [])
