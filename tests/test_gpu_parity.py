@@ -327,6 +327,11 @@ def test_heavy_dedup_jobs_pre_assembled(bs, engine, engine_small, oracle_lib):
                                   a_immutable=False, tomb_frac=0.9, drop_tombstones=True, overlap=0.0),
         workloads.make_job_inputs(tree("transfers.id"), rng, n_a=60_000 // scale,
                                   b_table_sizes=[70_000 // scale], a_immutable=True, dup_frac=0.05),
+        # Secondary index, disk A, no tombstone drop: A's removes cancel 90 %
+        # of B's puts (both vanish), so the job is sparse without dedup or
+        # drop_tombstones (the host must still pre-assemble it).
+        workloads.make_job_inputs(tree("transfers.debit_account_id"), rng, n_a=100_000 // scale,
+                                  b_table_sizes=[100_000 // scale], a_immutable=False, overlap=0.9),
     ]
     addrs = [workloads.addresses_for(workloads.worst_case_blocks(ji.tree, len(ji.a_values) + sum(map(len, ji.b_tables)),
                                                                  bs) + 2, rng, 50 + 1000 * i) for i, ji in enumerate(jobs)]
@@ -338,5 +343,6 @@ def test_heavy_dedup_jobs_pre_assembled(bs, engine, engine_small, oracle_lib):
         for g, w in zip(blocks, o.blocks):
             assert np.array_equal(disk_image(g), disk_image(w))
         assert np.array_equal(infos, o.table_infos)
-    n0 = len(jobs[0].a_values) + sum(map(len, jobs[0].b_tables))
-    assert results[0][0].value_count * 4 < n0  # the sparse path was taken
+    for k in (0, 3):  # the sparse path was taken
+        nk = len(jobs[k].a_values) + sum(map(len, jobs[k].b_tables))
+        assert results[k][0].value_count * 4 < nk, k

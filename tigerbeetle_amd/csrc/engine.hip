@@ -424,10 +424,14 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     std::vector<uint32_t> order(count);
     uint64_t seg_words = 0, addr_words = 0;
     const uint8_t flags0 = count ? jobs_in[0].flags : 0;
-    // Dedup (immutable A) or tombstone drops can leave a job's survivors
-    // sparse; only then may the block phase pre-assemble (aegis.hip sparse_job).
+    // Dedup (immutable A), tombstone drops or secondary-index put/remove
+    // cancellation (an A tombstone and its B put both vanish, merge.hip) can
+    // leave a job's survivors sparse; only then may the block phase
+    // pre-assemble (aegis.hip sparse_job decides per job on the device).
     bool maybe_sparse = false;
-    for (uint32_t i = 0; i < count; i++) maybe_sparse |= jobs_in[i].a_immutable || jobs_in[i].drop_tombstones;
+    for (uint32_t i = 0; i < count; i++)
+        maybe_sparse |= jobs_in[i].a_immutable || jobs_in[i].drop_tombstones ||
+                        jobs_in[i].tree.usage == TBC_USAGE_SECONDARY_INDEX;
     for (uint32_t i = 0; i < count; i++) {
         const tbc_compaction &c = jobs_in[i];
         JobDesc &d = hj[i];

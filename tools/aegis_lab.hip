@@ -1,7 +1,21 @@
-// aegis_lab.hip — microbenchmark of the AEGIS-128L chain (tools only, not the
-// product path). Instantiates the production aegis_mac32 loop with different
-// per-update step policies, times them on N 1-MiB messages with hipEvents and
-// checks every variant's tags against the production step.
+// aegis_lab.hip — microbenchmark of AEGIS-128L update layouts (tools only,
+// not the product path). Every variant computes vsr.checksum of N 1-MiB data
+// block bodies (1,048,320 bytes = 32,760 absorbs + 7 finalisation updates,
+// src/vsr/checksum.zig:50-59) and is checked against the production
+// k_checksum_batch; times are hipEvents, reported per sequential update.
+//
+// Variants:
+//   prod        production aegis_mac32 (StepValuKey), 2 messages per wave;
+//   col4/L0     simplified full-block loop, lane (slot p, column c) = 4p + c,
+//               round key by row_ror:12 + permlane16_swap + 2 selects;
+//   col4/L1     same, slots interleaved over the two rows of a 32-lane group
+//               (even slots row 0, odd slots row 1): the round key is
+//               row_ror:12 + permlane16_swap + ONE select;
+//   col2        16 lanes per message (4 messages per wave): lane (p, h) holds
+//               columns h and h+2 of slot p, 8 T-table lookups, the round key
+//               is one row_ror:14 DPP operand, the partner pair exchange one
+//               quad_perm DPP operand;
+//   lds-chain   dependent ds_read_b32 chain (x = T[x]) to calibrate latency.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include aegis_lab.hip -o aegis_lab
 #include "../tigerbeetle_amd/csrc/aegis.hip"
@@ -13,11 +27,62 @@
 
 namespace tbc {
 
-// Table reads issued first; the round key (ds_bpermute) after them and
-// folded in last.
-struct StepLateKey {
-    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t key_src,
-                                                    uint32_t x, uint32_t m) {
+constexpr uint32_t kLen = 1048320;        // one 1 MiB data block body (constants.zig:500)
+constexpr uint32_t kAbs = kLen / 32;      // 32,760 absorbs
+constexpr uint32_t kWin = kAbs / 8;       // 4,095 windows of 8 updates
+constexpr uint32_t kGrp = 8;              // windows per prefetch group
+
+__device__ __forceinline__ uint32_t dpp_row_ror12(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12C, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_row_ror14(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12E, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_pair_swap(uint32_t v) { // quad_perm [1,0,3,2]
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, true);
+}
+
+// ---------------------------------------------------------------------------
+// One column per lane (32 lanes per message, 2 messages per wave).
+// ---------------------------------------------------------------------------
+template <bool INTERLEAVED>
+struct Col4 {
+    uint32_t g, row, p, c;
+    __device__ __forceinline__ Col4() {
+        g = threadIdx.x & 31;
+        row = g >> 4;
+        c = g & 3;
+        p = INTERLEAVED ? 2 * ((g >> 2) & 3) + row : g >> 2;
+    }
+    // lane (inside the wave) of slot q, same column
+    __device__ __forceinline__ uint32_t lane_of(uint32_t q) const {
+        const uint32_t half = threadIdx.x & 32;
+        return half + (INTERLEAVED ? 16 * (q & 1) + 4 * (q >> 1) : 4 * q) + c;
+    }
+    __device__ __forceinline__ uint32_t key(uint32_t x) const {
+        const uint32_t r = dpp_row_ror12(x);
+        if constexpr (INTERLEAVED) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(x, r, false, false);
+            return row == 0 ? sw[1] : sw[0];
+        } else {
+            return key_valu(x);
+        }
+    }
+};
+
+template <bool INTERLEAVED>
+__device__ __forceinline__ uint32_t mac_col4(const uint32_t *sT, const uint8_t *msg) {
+    const Col4<INTERLEAVED> L;
+    const TableBase tb;
+    uint32_t x = c_seed.s[L.p][L.c];
+    const uint32_t k_lo = (3 - L.p) & 3;
+    const uint32_t lab_lo = (L.p + k_lo + 1) & 7;
+    const uint32_t off_lo = 32 * k_lo + 4 * (lab_lo + L.c);
+    const uint32_t off_hi = 32 * (k_lo + 4) + 4 * ((lab_lo ^ 4) + L.c);
+    bool need[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) need[k] = ((L.p + k + 1) & 3) == 0;
+    auto step = [&](uint32_t m) {
         const uint32_t a0 = __builtin_amdgcn_perm(x, tb.lo, 0x03020400u);
         const uint32_t a1 = __builtin_amdgcn_perm(x, tb.lo, 0x03020500u);
         const uint32_t a2 = __builtin_amdgcn_perm(x, tb.hi, 0x03020600u);
@@ -26,33 +91,182 @@ struct StepLateKey {
         const uint32_t t1 = lds_u32(sT, a1 + 128);
         const uint32_t t2 = lds_u32(sT, a2);
         const uint32_t t3 = lds_u32(sT, a3 + 128);
-        const uint32_t key = bpermute(key_src, x);
-        uint32_t r = t0 ^ m;
+        uint32_t r = (L.key(x) ^ m) ^ t0;
         r ^= quad_perm<1, 2, 3, 0>(t1);
         r ^= quad_perm<2, 3, 0, 1>(t2);
         r ^= quad_perm<3, 0, 1, 2>(t3);
-        return r ^ key;
+        x = r;
+    };
+    auto word = [&](uint32_t off) { return gld<uint32_t>(msg + (off < kLen ? off : kLen - 4)); };
+    uint32_t cur[2 * kGrp], nxt[2 * kGrp];
+#pragma unroll
+    for (uint32_t d = 0; d < kGrp; d++) {
+        cur[2 * d] = word(256 * d + off_lo);
+        cur[2 * d + 1] = word(256 * d + off_hi);
     }
-};
+    for (uint32_t w0 = 0; w0 < kWin; w0 += kGrp) {
+#pragma unroll
+        for (uint32_t d = 0; d < kGrp; d++) {
+            nxt[2 * d] = word(256 * (w0 + kGrp + d) + off_lo);
+            nxt[2 * d + 1] = word(256 * (w0 + kGrp + d) + off_hi);
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < kGrp; d++) {
+            if (w0 + d < kWin) {
+#pragma unroll
+                for (uint32_t k = 0; k < 8; k++) step(need[k & 3] ? (k < 4 ? cur[2 * d] : cur[2 * d + 1]) : 0u);
+            }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 2 * kGrp; i++) cur[i] = nxt[i];
+    }
+    // Finalisation: t = LE64(len * 8) || 0 ^ S2, injected 7 times.
+    const uint32_t q2 = (2 - kAbs) & 7;
+    uint32_t t = (uint32_t)__shfl((int)x, (int)L.lane_of(q2), 64);
+    const uint64_t bits = (uint64_t)kLen * 8;
+    t ^= L.c == 0 ? (uint32_t)bits : L.c == 1 ? (uint32_t)(bits >> 32) : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 7; k++) step(need[k & 3] ? t : 0u);
+    const uint32_t q7 = (7 - (kAbs + 7)) & 7;
+    const uint32_t s7 = (uint32_t)__shfl((int)x, (int)L.lane_of(q7), 64);
+    uint32_t tag = x;
+    tag ^= (uint32_t)__shfl_xor((int)tag, 4, 64);
+    tag ^= (uint32_t)__shfl_xor((int)tag, 8, 64);
+    tag ^= (uint32_t)__shfl_xor((int)tag, 16, 64);
+    return tag ^ s7;
+}
 
-// One message per 32-lane group; `per_wave` = 2 (production) or 1 (upper
-// half duplicates the lower half's message).
-template <class Step>
-__global__ __launch_bounds__(1024) void k_lab(const uint8_t *base, uint32_t len, uint32_t count, uint32_t per_wave,
-                                              uint8_t *out) {
+template <bool INTERLEAVED>
+__global__ __launch_bounds__(1024) void k_col4(const uint8_t *base, uint32_t count, uint32_t per_wave, uint8_t *out) {
     __shared__ uint32_t sT[kTableDwords];
     load_tables(sT);
     __syncthreads();
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t half = (threadIdx.x >> 5) & 1;
-    const uint32_t first = wave * per_wave;
-    if (first >= count) return;
-    uint32_t id = first + (per_wave == 2 ? half : 0);
+    if (wave * per_wave >= count) return;
+    uint32_t id = wave * per_wave + (per_wave == 2 ? half : 0);
     if (id >= count) id = count - 1;
-    GlobalMsg m(base + ((size_t)id << 20), len);
-    const uint32_t tag = aegis_mac32<GlobalMsg, Step>(sT, m);
-    const uint32_t g = threadIdx.x & 31;
-    if (g < 4 && (per_wave == 2 || half == 0)) gst<uint32_t>(out + 16 * (size_t)id + 4 * g, tag);
+    const uint32_t tag = mac_col4<INTERLEAVED>(sT, base + ((size_t)id << 20));
+    const Col4<INTERLEAVED> L;
+    // tag column c lives in every slot's lane; slot 0 writes
+    if (L.p == 0 && (per_wave == 2 || half == 0)) gst<uint32_t>(out + 16 * (size_t)id + 4 * L.c, tag);
+}
+
+// ---------------------------------------------------------------------------
+// Two columns per lane (16 lanes per message, 4 messages per wave).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mac_col2(const uint32_t *sT, const uint8_t *msg, uint32_t &tag_v) {
+    const uint32_t lane = threadIdx.x & 63, i = lane & 15, rowbase = lane & 48;
+    const uint32_t p = i >> 1, h = i & 1;
+    const TableBase tb;
+    uint32_t u = c_seed.s[p][h], v = c_seed.s[p][h + 2];
+    const uint32_t k_lo = (3 - p) & 3;
+    const uint32_t lab_lo = (p + k_lo + 1) & 7;
+    // word offsets of (u, v) for the lo and hi injection of a window
+    const uint32_t off_lo = 32 * k_lo + 4 * (lab_lo + h);
+    const uint32_t off_hi = 32 * (k_lo + 4) + 4 * ((lab_lo ^ 4) + h);
+    bool need[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) need[k] = ((p + k + 1) & 3) == 0;
+    const bool h0 = h == 0;
+    auto step = [&](uint32_t mu, uint32_t mv) {
+        const uint32_t f1 = h0 ? v : u, f3 = h0 ? u : v;
+        const uint32_t au = lds_u32(sT, __builtin_amdgcn_perm(u, tb.lo, 0x03020400u));
+        const uint32_t av = lds_u32(sT, __builtin_amdgcn_perm(v, tb.lo, 0x03020400u));
+        const uint32_t cu = lds_u32(sT, __builtin_amdgcn_perm(u, tb.hi, 0x03020600u));
+        const uint32_t cv = lds_u32(sT, __builtin_amdgcn_perm(v, tb.hi, 0x03020600u));
+        const uint32_t b1 = lds_u32(sT, __builtin_amdgcn_perm(f1, tb.lo, 0x03020500u) + 128);
+        const uint32_t b3 = lds_u32(sT, __builtin_amdgcn_perm(f1, tb.hi, 0x03020700u) + 128);
+        const uint32_t d1 = lds_u32(sT, __builtin_amdgcn_perm(f3, tb.lo, 0x03020500u) + 128);
+        const uint32_t d3 = lds_u32(sT, __builtin_amdgcn_perm(f3, tb.hi, 0x03020700u) + 128);
+        const uint32_t ku = dpp_row_ror14(u) ^ mu, kv = dpp_row_ror14(v) ^ mv;
+        const uint32_t F = b1 ^ d3; // T1(f1) ^ T3(f3)
+        const uint32_t G = d1 ^ b3; // T1(f3) ^ T3(f1)
+        u = (au ^ cv ^ ku) ^ dpp_pair_swap(F);
+        v = (av ^ cu ^ kv) ^ dpp_pair_swap(G);
+    };
+    auto word = [&](uint32_t off) { return gld<uint32_t>(msg + (off < kLen ? off : kLen - 4)); };
+    // per window: u-lo, v-lo (+8 bytes), u-hi, v-hi
+    uint32_t cur[4 * kGrp], nxt[4 * kGrp];
+#pragma unroll
+    for (uint32_t d = 0; d < kGrp; d++) {
+        cur[4 * d] = word(256 * d + off_lo);
+        cur[4 * d + 1] = word(256 * d + off_lo + 8);
+        cur[4 * d + 2] = word(256 * d + off_hi);
+        cur[4 * d + 3] = word(256 * d + off_hi + 8);
+    }
+    for (uint32_t w0 = 0; w0 < kWin; w0 += kGrp) {
+#pragma unroll
+        for (uint32_t d = 0; d < kGrp; d++) {
+            const uint32_t b = 256 * (w0 + kGrp + d);
+            nxt[4 * d] = word(b + off_lo);
+            nxt[4 * d + 1] = word(b + off_lo + 8);
+            nxt[4 * d + 2] = word(b + off_hi);
+            nxt[4 * d + 3] = word(b + off_hi + 8);
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < kGrp; d++) {
+            if (w0 + d < kWin) {
+#pragma unroll
+                for (uint32_t k = 0; k < 8; k++) {
+                    const bool n = need[k & 3];
+                    const uint32_t mu = n ? (k < 4 ? cur[4 * d] : cur[4 * d + 2]) : 0u;
+                    const uint32_t mv = n ? (k < 4 ? cur[4 * d + 1] : cur[4 * d + 3]) : 0u;
+                    step(mu, mv);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 4 * kGrp; q++) cur[q] = nxt[q];
+    }
+    const uint32_t q2 = (2 - kAbs) & 7;
+    const uint32_t src2 = rowbase + 2 * q2 + h;
+    uint32_t tu = (uint32_t)__shfl((int)u, (int)src2, 64);
+    const uint32_t tv = (uint32_t)__shfl((int)v, (int)src2, 64);
+    const uint64_t bits = (uint64_t)kLen * 8;
+    tu ^= h0 ? (uint32_t)bits : (uint32_t)(bits >> 32);
+#pragma unroll
+    for (uint32_t k = 0; k < 7; k++) step(need[k & 3] ? tu : 0u, need[k & 3] ? tv : 0u);
+    const uint32_t q7 = (7 - (kAbs + 7)) & 7;
+    const uint32_t src7 = rowbase + 2 * q7 + h;
+    const uint32_t s7u = (uint32_t)__shfl((int)u, (int)src7, 64), s7v = (uint32_t)__shfl((int)v, (int)src7, 64);
+    uint32_t tagu = u, tagv = v;
+    for (int o = 2; o <= 8; o <<= 1) {
+        tagu ^= (uint32_t)__shfl_xor((int)tagu, o, 64);
+        tagv ^= (uint32_t)__shfl_xor((int)tagv, o, 64);
+    }
+    tag_v = tagv ^ s7v;
+    return tagu ^ s7u;
+}
+
+__global__ __launch_bounds__(1024) void k_col2(const uint8_t *base, uint32_t count, uint8_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (4 * wave >= count) return;
+    uint32_t id = 4 * wave + (lane >> 4);
+    const bool real = id < count;
+    if (!real) id = count - 1;
+    uint32_t tv;
+    const uint32_t tu = mac_col2(sT, base + ((size_t)id << 20), tv);
+    const uint32_t i = lane & 15;
+    if (real && i < 2) {
+        gst<uint32_t>(out + 16 * (size_t)id + 4 * i, tu);
+        gst<uint32_t>(out + 16 * (size_t)id + 4 * (i + 2), tv);
+    }
+}
+
+// Dependent LDS reads: iters x (perm + ds_read_b32), one chain per lane.
+__global__ __launch_bounds__(64) void k_lds_chain(uint32_t iters, uint32_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
+    for (uint32_t i = threadIdx.x; i < kTableDwords; i += 64) sT[i] = (i * 2654435761u) >> 8;
+    __syncthreads();
+    const TableBase tb;
+    uint32_t x = threadIdx.x;
+    for (uint32_t k = 0; k < iters; k++) x = lds_u32(sT, __builtin_amdgcn_perm(x, tb.lo, 0x03020400u));
+    out[threadIdx.x] = x;
 }
 
 __global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
@@ -65,6 +279,23 @@ __global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
         x ^= x >> 16;
         p[i] = x;
     }
+}
+
+// Production loop (reference timing): k_checksum_batch semantics on 1 MiB bodies.
+template <class Step>
+__global__ __launch_bounds__(1024) void k_prod(const uint8_t *base, uint32_t count, uint32_t per_wave, uint8_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t half = (threadIdx.x >> 5) & 1;
+    if (wave * per_wave >= count) return;
+    uint32_t id = wave * per_wave + (per_wave == 2 ? half : 0);
+    if (id >= count) id = count - 1;
+    GlobalMsg m(base + ((size_t)id << 20), kLen);
+    const uint32_t tag = aegis_mac32<GlobalMsg, Step>(sT, m);
+    const uint32_t g = threadIdx.x & 31;
+    if (g < 4 && (per_wave == 2 || half == 0)) gst<uint32_t>(out + 16 * (size_t)id + 4 * g, tag);
 }
 
 } // namespace tbc
@@ -80,71 +311,112 @@ using namespace tbc;
         }                                                                                       \
     } while (0)
 
-template <class Step>
-static float run(const char *name, const uint8_t *d_msgs, uint32_t count, uint32_t per_wave, uint8_t *d_out,
-                 uint32_t len) {
-    const uint32_t waves = (count + per_wave - 1) / per_wave;
-    uint32_t wpb = (waves + 255) / 256;
-    wpb = wpb < 1 ? 1 : (wpb > 16 ? 16 : wpb);
-    const uint32_t blocks = (waves + wpb - 1) / wpb;
+static uint32_t wpb_for(uint32_t waves, uint32_t max_wpb) {
+    uint32_t w = (waves + 255) / 256;
+    return w < 1 ? 1 : (w > max_wpb ? max_wpb : w);
+}
+
+template <class Launch>
+static float timed(Launch launch) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    hipLaunchKernelGGL(k_lab<Step>, dim3(blocks), dim3(64 * wpb), 0, 0, d_msgs, len, count, per_wave, d_out);
+    launch();
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
     float best = 1e30f;
     for (int r = 0; r < 3; r++) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL(k_lab<Step>, dim3(blocks), dim3(64 * wpb), 0, 0, d_msgs, len, count, per_wave, d_out);
+        launch();
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
         CK(hipEventElapsedTime(&ms, a, b));
         best = ms < best ? ms : best;
     }
-    const double updates = (len + 31) / 32 + 7;
-    printf("%-16s count=%5u per_wave=%u waves=%5u wg=%4u x %2u  %8.3f ms  %6.1f ns/update  %7.1f GB/s\n", name,
-           count, per_wave, waves, blocks, wpb, best, best * 1e6 / updates, (double)count * len / best / 1e6);
-    fflush(stdout);
     CK(hipEventDestroy(a));
     CK(hipEventDestroy(b));
     return best;
 }
 
+static void report(const char *name, uint32_t count, uint32_t waves, uint32_t wpb, float ms) {
+    const double updates = kAbs + 7;
+    printf("{\"variant\": \"%s\", \"messages\": %u, \"waves\": %u, \"waves_per_wg\": %u, \"ms\": %.4f, "
+           "\"ns_per_update\": %.2f, \"GBps\": %.1f}\n",
+           name, count, waves, wpb, ms, ms * 1e6 / updates, (double)count * kLen / ms / 1e6);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
-    const uint32_t nmax = argc > 1 ? (uint32_t)atoi(argv[1]) : 2072;
-    const uint32_t len = 1048320; // one 1 MiB data block body (constants.zig:500)
+    const uint32_t nmax = argc > 1 ? (uint32_t)atoi(argv[1]) : 16384;
     uint8_t *d_msgs, *d_out, *d_ref;
     CK(hipMalloc(&d_msgs, (size_t)nmax << 20));
     CK(hipMalloc(&d_out, 16ull * nmax));
     CK(hipMalloc(&d_ref, 16ull * nmax));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint32_t *)d_msgs, ((size_t)nmax << 20) / 4, 7u);
     CK(hipDeviceSynchronize());
+    {
+        uint32_t *d_c;
+        CK(hipMalloc(&d_c, 256));
+        const uint32_t iters = 1u << 20;
+        float ms = timed([&] { hipLaunchKernelGGL(k_lds_chain, dim3(1), dim3(64), 0, 0, iters, d_c); });
+        printf("{\"variant\": \"lds-chain\", \"ns_per_read\": %.2f}\n", ms * 1e6 / iters);
+        CK(hipFree(d_c));
+    }
     std::vector<uint8_t> h_ref(16ull * nmax), h_out(16ull * nmax);
-    const uint32_t counts[] = {2, 64, 2016, nmax};
+    const uint32_t counts[] = {2, 4, 1008, 2016, 4096, 8192, 13824, 16384};
     int bad = 0;
     for (uint32_t count : counts) {
         if (count > nmax) continue;
-        run<StepBpermute>("bpermute", d_msgs, count, 2, d_ref, len);
-        CK(hipMemcpy(h_ref.data(), d_ref, 16ull * count, hipMemcpyDeviceToHost));
+        // Reference tags: production kernel.
+        {
+            const uint32_t waves = (count + 1) / 2, wpb = wpb_for(waves, 16);
+            const float ms = timed([&] {
+                hipLaunchKernelGGL(k_prod<StepValuKey>, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs,
+                                   count, 2u, d_ref);
+            });
+            report("prod-valukey", count, waves, wpb, ms);
+            CK(hipMemcpy(h_ref.data(), d_ref, 16ull * count, hipMemcpyDeviceToHost));
+        }
         auto check = [&](const char *what) {
             CK(hipMemcpy(h_out.data(), d_out, 16ull * count, hipMemcpyDeviceToHost));
             if (memcmp(h_out.data(), h_ref.data(), 16ull * count)) {
-                printf("  MISMATCH %s\n", what);
+                printf("{\"variant\": \"%s\", \"messages\": %u, \"MISMATCH\": true}\n", what, count);
                 bad++;
             }
         };
-        CK(hipMemset(d_out, 0, 16ull * count));
-        run<StepBpermute>("bpermute/1", d_msgs, count, 1, d_out, len);
-        check("bpermute/1");
-        CK(hipMemset(d_out, 0, 16ull * count));
-        run<StepLateKey>("late-key", d_msgs, count, 2, d_out, len);
-        check("late-key");
-        CK(hipMemset(d_out, 0, 16ull * count));
-        run<StepValuKey>("valu-key", d_msgs, count, 2, d_out, len);
-        check("valu-key");
-
+        if (count >= 8192) {
+            const uint32_t waves = (count + 1) / 2, wpb = wpb_for(waves, 16);
+            const float ms = timed([&] {
+                hipLaunchKernelGGL(k_prod<StepBpermute>, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs,
+                                   count, 2u, d_out);
+            });
+            report("prod-bpermute", count, waves, wpb, ms);
+            check("prod-bpermute");
+        }
+        for (int il = 0; il < 2; il++) {
+            const uint32_t waves = (count + 1) / 2, wpb = wpb_for(waves, 16);
+            CK(hipMemset(d_out, 0, 16ull * count));
+            const float ms = timed([&] {
+                if (il)
+                    hipLaunchKernelGGL(k_col4<true>, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs, count,
+                                       2u, d_out);
+                else
+                    hipLaunchKernelGGL(k_col4<false>, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs,
+                                       count, 2u, d_out);
+            });
+            report(il ? "col4-L1" : "col4-L0", count, waves, wpb, ms);
+            check(il ? "col4-L1" : "col4-L0");
+        }
+        {
+            const uint32_t waves = (count + 3) / 4, wpb = wpb_for(waves, 16);
+            CK(hipMemset(d_out, 0, 16ull * count));
+            const float ms = timed([&] {
+                hipLaunchKernelGGL(k_col2, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs, count, d_out);
+            });
+            report("col2", count, waves, wpb, ms);
+            check("col2");
+        }
     }
     printf(bad ? "LAB FAILED (%d mismatches)\n" : "LAB OK\n", bad);
     return bad ? 1 : 0;
