@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TBC_ABI_VERSION 1u
+#define TBC_ABI_VERSION 2u
 
 typedef enum tbc_status {
     TBC_OK = 0,
@@ -39,6 +39,8 @@ typedef enum tbc_status {
     TBC_ERR_OUT_OF_MEMORY = 4,    /* static arena exhausted (reference panics: compaction.zig:307-318) */
     TBC_ERR_CAPACITY = 5,         /* address list / output too small for the worst case */
     TBC_ERR_INVARIANT = 6,        /* an input broke a reference invariant (e.g. unsorted table) */
+    TBC_ERR_BLOCK_INVALID = 7,    /* a grid input block failed read_block_from_cache's checks or
+                                     read_block_validate (grid.zig:802-841, 1059-1084) */
 } tbc_status;
 
 /* Key of a tree's Value (src/lsm/groove.zig:22-76, src/lsm/composite_key.zig:7-70). */
@@ -102,8 +104,36 @@ typedef struct tbc_segment {
 /* tbc_compaction.flags. VALUES_ONLY: the survivors only — data-block bodies
  * (values at +256 of each data-block slot) and the result counts; no headers,
  * checksums, index blocks or TableInfos. Phase 1 of a job split by key range
- * across GPUs (tigerbeetle_amd/split.py); every job of a batch must agree. */
+ * across GPUs (tigerbeetle_amd/split.py); every job of a batch must agree.
+ * GRID: inputs and outputs live in a tbc_grid, see below: disk tables are
+ * named by table reference (tables_a / tables_b; an immutable A still comes
+ * as one segment), their data blocks are found through their index blocks
+ * on the device, and every output block is written to the grid at its
+ * acquired address (segments_b and output_blocks are ignored). */
 #define TBC_COMPACTION_VALUES_ONLY 1u
+#define TBC_COMPACTION_GRID 2u
+
+/* ---- GPU-resident grid (src/vsr/grid.zig, src/lsm/set_associative_cache.zig) ----
+ * The blocks of the data file's grid zone for addresses [1, block_count],
+ * resident in HBM (block `address` at slot address - 1; one MI355X holds
+ * ~270k 1 MiB blocks). A compaction's output blocks stay there and are the
+ * next compaction's inputs with no PCIe round trip. Blocks written by the
+ * engine are trusted like grid cache hits (read_block_from_cache compares
+ * the header checksum with the expected one, grid.zig:802-841); blocks staged
+ * from storage are fully validated (read_block_validate: header and body
+ * AEGIS, grid.zig:1059-1084) by the first batch that reads them, on a second
+ * stream concurrently with its compaction. */
+typedef struct tbc_grid tbc_grid;
+
+/* A disk table as Compaction.Context names it (TableInfoReference,
+ * compaction.zig:84-99; manifest TableInfo, schema.zig:489-509): its index
+ * block's address and checksum, and its value count (every data block of a
+ * table is full except the last, compaction.zig:806-850). */
+typedef struct tbc_table_ref {
+    uint64_t address;     /* index block address */
+    uint64_t checksum[2]; /* index block checksum, u128 little-endian words */
+    uint64_t value_count;
+} tbc_table_ref;
 
 /* One `Compaction.start(Context)` (src/lsm/compaction.zig:84-99, 280-404). */
 typedef struct tbc_compaction {
@@ -123,6 +153,12 @@ typedef struct tbc_compaction {
     uint32_t address_count;        /* >= (|B tables| + 1) * block_count_max, the reservation size */
     uint32_t reserved2;
     void *output_blocks;           /* device: address_count * block_size bytes; block i <-> addresses[i] */
+    /* TBC_COMPACTION_GRID only: */
+    tbc_grid *grid;
+    const tbc_table_ref *tables_a; /* host array: table_info_a.disk (0 or 1 table; none if immutable) */
+    const tbc_table_ref *tables_b; /* host array: range_b.tables in ascending key order */
+    uint32_t table_count_a;
+    uint32_t table_count_b;
 } tbc_compaction;
 
 /* Per-compaction result (after tbc_batch_poll returned TBC_OK). */
@@ -139,6 +175,41 @@ uint32_t tbc_abi_version(void);
 tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine);
 void tbc_engine_deinit(tbc_engine *engine);
 tbc_status tbc_tree_layout_get(const tbc_engine *engine, const tbc_tree *tree, tbc_tree_layout *out_layout);
+
+/* ---- grid ------------------------------------------------------------------- */
+tbc_status tbc_grid_init(tbc_engine *engine, uint64_t block_count, tbc_grid **out_grid);
+void tbc_grid_deinit(tbc_grid *grid);
+/* Device pointer of the block at `address` (1 <= address <= block_count). */
+tbc_status tbc_grid_block_pointer(const tbc_grid *grid, uint64_t address, void **out_ptr);
+/* grid.read_block from storage: stage `count` host block images (block_size
+ * bytes each, the on-disk image [0, sector_ceil(size)) is what matters) into
+ * the grid, enqueued on the engine stream (no host wait beyond the pinned
+ * staging copy). The blocks are marked unverified until a batch validates
+ * them. */
+tbc_status tbc_grid_put_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_blocks,
+                               uint32_t count);
+/* grid.write_block towards storage: copy `count` blocks' images
+ * [0, block_size) to host buffers. Enqueued on the engine stream; the
+ * buffers are valid after tbc_synchronize (or a later batch's completion). */
+tbc_status tbc_grid_get_blocks(tbc_grid *grid, const uint64_t *addresses, void *const *host_blocks,
+                               uint32_t count);
+
+/* ---- TableMemory on the device (src/lsm/table_memory.zig:79-124) ------------
+ * Groove.insert/update -> Tree.put (groove.zig:911-1006, tree.zig:268-270)
+ * append values to the mutable table; here the appends stream into device
+ * memory through pinned staging (host memcpy + async H2D on the engine
+ * stream), so the bar-end sort (tbc_sort_values_batch) and the immutable
+ * table's compaction read it in place: no H2D step at the bar end. */
+typedef struct tbc_memtable tbc_memtable;
+tbc_status tbc_memtable_init(tbc_engine *engine, const tbc_tree *tree, uint32_t capacity, tbc_memtable **out);
+void tbc_memtable_deinit(tbc_memtable *memtable);
+/* TableMemory.put of `count` values (host memory, value_size bytes each):
+ * TBC_ERR_CAPACITY past value_count_max (the reference asserts). */
+tbc_status tbc_memtable_put(tbc_memtable *memtable, const void *values, uint32_t count);
+/* Device pointer and value count (for sort jobs and immutable compactions). */
+tbc_status tbc_memtable_values(const tbc_memtable *memtable, void **out_values, uint32_t *out_count);
+/* make_mutable: empty the table (after its immutable compaction flushed it). */
+tbc_status tbc_memtable_reset(tbc_memtable *memtable);
 
 /* ---- device memory (staging for the host adapter; synchronous copies) ------ */
 tbc_status tbc_device_alloc(tbc_engine *engine, uint64_t bytes, void **out_ptr);
@@ -168,6 +239,8 @@ typedef enum tbc_block_check {
     TBC_BLOCK_UNEXPECTED_CHECKSUM = 4,   /* header checksum != the expected (manifest/index) checksum */
     TBC_BLOCK_UNEXPECTED_ADDRESS = 5,    /* header address != the expected address (reference asserts) */
     TBC_BLOCK_INVALID_SIZE = 6,          /* size outside [256, block_size] (reference asserts) */
+    TBC_BLOCK_UNEXPECTED_HEADER = 7,     /* grid input: cluster, block type, tree, value count or size
+                                            differ from the table it was reached from (reference asserts) */
 } tbc_block_check;
 /* Synchronous batched validation of device-resident blocks (16-byte aligned
  * device pointers, block_size readable). expect_checksums: 2 u64 (u128 LE)

@@ -19,7 +19,7 @@ def test_abi_version_and_struct_layout_match_c():
     """ctypes mirrors of the ABI structs have the C compiler's sizes/offsets."""
     import subprocess
     import tempfile
-    assert abi.lib().tbc_abi_version() == 1
+    assert abi.lib().tbc_abi_version() == abi.ABI_VERSION
     checks = {
         "tbc_tree": (abi.Tree, ["tree_id", "key_kind", "usage", "value_size", "timestamp_offset",
                                 "table_value_count_max"]),
@@ -29,6 +29,7 @@ def test_abi_version_and_struct_layout_match_c():
         "tbc_compaction": (abi.Compaction, [f for f, _ in abi.Compaction._fields_ if not f.startswith("reserved")]),
         "tbc_compaction_result": (abi.CompactionResult, [f for f, _ in abi.CompactionResult._fields_]),
         "tbc_tree_layout": (abi.TreeLayout, [f for f, _ in abi.TreeLayout._fields_]),
+        "tbc_table_ref": (abi.TableRef, ["address", "checksum", "value_count"]),
     }
     lines = ['#include "tbc.h"', "#include <stdio.h>", "#include <stddef.h>", "int main(void) {"]
     expect = []

@@ -21,15 +21,18 @@ TBC_ERR_DEVICE = 3
 TBC_ERR_OUT_OF_MEMORY = 4
 TBC_ERR_CAPACITY = 5
 TBC_ERR_INVARIANT = 6
+TBC_ERR_BLOCK_INVALID = 7
 STATUS_NAMES = {
     0: "OK", 1: "PENDING", 2: "ERR_INVALID_ARGUMENT", 3: "ERR_DEVICE", 4: "ERR_OUT_OF_MEMORY",
-    5: "ERR_CAPACITY", 6: "ERR_INVARIANT",
+    5: "ERR_CAPACITY", 6: "ERR_INVARIANT", 7: "ERR_BLOCK_INVALID",
 }
 
 KEY_TIMESTAMP, KEY_ID_U128, KEY_COMPOSITE_U64, KEY_COMPOSITE_U128 = 0, 1, 2, 3
 USAGE_GENERAL, USAGE_SECONDARY_INDEX = 0, 1
 CONFIG_PROFILE = 1
 COMPACTION_VALUES_ONLY = 1  # tbc_compaction.flags
+COMPACTION_GRID = 2
+ABI_VERSION = 2
 
 
 class TbcError(RuntimeError):
@@ -81,6 +84,10 @@ class SortJob(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class TableRef(ctypes.Structure):
+    _fields_ = [("address", ctypes.c_uint64), ("checksum", ctypes.c_uint64 * 2), ("value_count", ctypes.c_uint64)]
+
+
 class Compaction(ctypes.Structure):
     _fields_ = [
         ("tree", Tree),
@@ -99,6 +106,11 @@ class Compaction(ctypes.Structure):
         ("address_count", ctypes.c_uint32),
         ("reserved2", ctypes.c_uint32),
         ("output_blocks", ctypes.c_void_p),
+        ("grid", ctypes.c_void_p),
+        ("tables_a", ctypes.POINTER(TableRef)),
+        ("tables_b", ctypes.POINTER(TableRef)),
+        ("table_count_a", ctypes.c_uint32),
+        ("table_count_b", ctypes.c_uint32),
     ]
 
 
@@ -144,6 +156,16 @@ _SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_double), ctypes.c_uint32,
                                               ctypes.POINTER(ctypes.c_uint32)]),
     "tbc_batch_release": (None, [_P]),
+    "tbc_grid_init": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
+    "tbc_grid_deinit": (None, [_P]),
+    "tbc_grid_block_pointer": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
+    "tbc_grid_put_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
+    "tbc_grid_get_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
+    "tbc_memtable_init": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "tbc_memtable_deinit": (None, [_P]),
+    "tbc_memtable_put": (ctypes.c_int, [_P, _P, ctypes.c_uint32]),
+    "tbc_memtable_values": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint32)]),
+    "tbc_memtable_reset": (ctypes.c_int, [_P]),
 }
 
 _lib = None

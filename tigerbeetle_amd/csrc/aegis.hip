@@ -495,15 +495,11 @@ __global__ __launch_bounds__(1024) void k_checksum_batch(const uint64_t *ptrs, c
 // blocks: one wave per block, the lower 32-lane group checksums the header
 // (bytes [16, 256)), the upper group the body ([256, size)); then the checks
 // in the reference's order. Result codes: tbc_block_check (tbc.h).
-__global__ __launch_bounds__(1024) void k_validate_blocks(const uint64_t *ptrs, const uint64_t *expect, uint32_t count,
-                                                          uint32_t block_size, uint8_t *out) {
-    __shared__ uint32_t sT[kTableDwords];
-    load_tables(sT);
-    __syncthreads();
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (wave >= count) return;
+// One wave: the checks of read_block_validate in its order; the result is
+// valid in lane 0.
+__device__ __forceinline__ uint32_t validate_block_wave(const uint32_t *sT, const uint8_t *blk, uint32_t block_size,
+                                                        uint64_t expect_lo, uint64_t expect_hi, uint64_t address) {
     const uint32_t lane = threadIdx.x & 63, g = lane & 31;
-    const uint8_t *blk = (const uint8_t *)ptrs[wave];
     const uint32_t size = gld<uint32_t>(blk + 96);
     const bool size_ok = size >= kHeaderSize && size <= block_size;
     const bool upper = lane >= 32;
@@ -512,18 +508,65 @@ __global__ __launch_bounds__(1024) void k_validate_blocks(const uint64_t *ptrs, 
     // Lane g < 4 of each group compares its column with the stored checksum.
     const uint32_t stored = g < 4 ? gld<uint32_t>(blk + (upper ? 32 : 0) + 4 * g) : tag;
     const uint64_t bad = __ballot(tag != stored);
-    if (lane != 0) return;
     const bool header_ok = (bad & 0xfull) == 0, body_ok = ((bad >> 32) & 0xfull) == 0;
-    uint8_t r;
-    if (!header_ok) r = 1;                                       // invalid_checksum
-    else if (blk[110] != 20) r = 2;                              // unexpected_command (Command.block)
-    else if (!size_ok) r = 6;                                    // size out of bounds (reference asserts)
-    else if (!body_ok) r = 3;                                    // invalid_checksum_body
-    else if (gld<uint64_t>(blk) != expect[3 * wave] || gld<uint64_t>(blk + 8) != expect[3 * wave + 1])
-        r = 4;                                                   // unexpected_checksum
-    else if (gld<uint64_t>(blk + 224) != expect[3 * wave + 2]) r = 5; // address (reference asserts)
-    else r = 0;
-    out[wave] = r;
+    if (!header_ok) return 1;                                           // invalid_checksum
+    if (blk[110] != 20) return 2;                                       // unexpected_command (Command.block)
+    if (!size_ok) return 6;                                             // size out of bounds (reference asserts)
+    if (!body_ok) return 3;                                             // invalid_checksum_body
+    if (gld<uint64_t>(blk) != expect_lo || gld<uint64_t>(blk + 8) != expect_hi) return 4; // unexpected_checksum
+    if (gld<uint64_t>(blk + 224) != address) return 5;                  // address (reference asserts)
+    return 0;
+}
+
+__global__ __launch_bounds__(1024) void k_validate_blocks(const uint64_t *ptrs, const uint64_t *expect, uint32_t count,
+                                                          uint32_t block_size, uint8_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= count) return;
+    const uint32_t r = validate_block_wave(sT, (const uint8_t *)ptrs[wave], block_size, expect[3 * wave],
+                                           expect[3 * wave + 1], expect[3 * wave + 2]);
+    if ((threadIdx.x & 63) == 0) out[wave] = (uint8_t)r;
+}
+
+__device__ __forceinline__ void report_block_error(uint32_t *slot, uint32_t code) {
+    uint32_t expected = 0;
+    __hip_atomic_compare_exchange_strong(slot, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid inputs of a batch that were staged from storage (unverified):
+// read_block_validate, one wave per block, failures reported on the owning
+// job (first code wins), validated blocks marked trusted. Workgroups whose
+// blocks are all verified leave before loading the tables.
+__global__ __launch_bounds__(1024) void k_grid_validate(const InputCheck *checks, uint32_t count, uint8_t *verified,
+                                                        const JobDesc *jobs, int njobs, JobResultDev *res,
+                                                        uint32_t block_size) {
+    __shared__ uint32_t sT[kTableDwords];
+    __shared__ uint32_t s_any;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    InputCheck c{};
+    bool todo = false;
+    if (wave < count) {
+        c = checks[wave];
+        todo = c.address && !verified[c.address - 1];
+    }
+    if (todo && (threadIdx.x & 63) == 0) atomicOr(&s_any, 1u);
+    __syncthreads();
+    if (!s_any) return;
+    load_tables(sT);
+    __syncthreads();
+    if (!todo) return;
+    uint32_t r = validate_block_wave(sT, (const uint8_t *)(uintptr_t)c.ptr, block_size, c.checksum[0],
+                                     c.checksum[1], c.address);
+    if (r == 0) r = grid_header_check(job_of_result(jobs, njobs, c.job), c, block_size);
+    if ((threadIdx.x & 63) == 0) {
+        if (r) report_block_error(&res[c.job].block_error, r);
+        else verified[c.address - 1] = 1;
+    }
 }
 
 __device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return gld<uint64_t>(p); }
@@ -808,7 +851,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
-        uint8_t *blk = j.out_blocks + (size_t)data_block_slot(k, j.dbcm) * j.block_size;
+        uint8_t *blk = block_ptr(j, data_block_slot(k, j.dbcm));
         produce_body(j, k, block_count(j, k), status, masks, block_tile, splits, blk + kHeaderSize, &sProg[p],
                      const_cast<uint32_t *>(&res[j.job_index].invariant), sStage[Fused ? p : 0]);
         return;
@@ -827,7 +870,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
     const uint32_t cnt = block_count(j, k);
     const uint32_t size = kHeaderSize + cnt * j.value_size;
     const uint32_t slot = data_block_slot(k, j.dbcm);
-    uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
+    uint8_t *blk = block_ptr(j, slot);
 
     uint32_t body_tag;
     if constexpr (Fused) {
@@ -941,7 +984,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
                 const uint8_t *src = ((am >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(am & lt), vs)
                                                         : cb.elem(bb + __builtin_popcountll(valid & ~am & lt), vs);
                 const uint32_t k = o / vcm;
-                uint8_t *dst = j.out_blocks + (size_t)data_block_slot(k, j.dbcm) * j.block_size + kHeaderSize +
+                uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize +
                                (size_t)(o - k * vcm) * vs;
                 s_src[wv][r] = (uint64_t)(uintptr_t)src;
                 s_dst[wv][r] = (uint64_t)(uintptr_t)dst;
@@ -1019,7 +1062,7 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
         const uint64_t first = (uint64_t)k * j.vcm;
         const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
         const uint32_t slot = data_block_slot(k, j.dbcm);
-        const uint8_t *blk = j.out_blocks + (size_t)slot * j.block_size;
+        const uint8_t *blk = block_ptr(j, slot);
         uint64_t kmin[4], kmax[4];
         value_key(j, blk + kHeaderSize, kmin);
         value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
@@ -1056,7 +1099,7 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
     wave_sync();
     if (lane < 4) sIdx[lane] = hdr_tag;
     wave_sync();
-    uint8_t *blk = j.out_blocks + (size_t)index_slot * j.block_size;
+    uint8_t *blk = block_ptr(j, index_slot);
     for (uint32_t i = lane; i < j.index_size / 4; i += 64) gst<uint32_t>(blk + 4 * i, sIdx[i]);
     const uint32_t end = (uint32_t)sector_ceil(j.index_size);
     for (uint32_t o = j.index_size + 4 * lane; o < end; o += 256) gst<uint32_t>(blk + o, 0u);
@@ -1101,6 +1144,15 @@ int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uin
     const uint32_t wpb = waves_per_block(count);
     hipLaunchKernelGGL(k_validate_blocks, dim3((count + wpb - 1) / wpb), dim3(64 * wpb), 0, (hipStream_t)stream,
                        d_ptrs, d_expect, count, block_size, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_verified, const JobDesc *d_jobs,
+                         int njobs, JobResultDev *d_results, uint32_t block_size, void *stream) {
+    if (count == 0) return 0;
+    const uint32_t wpb = waves_per_block(count);
+    hipLaunchKernelGGL(k_grid_validate, dim3((count + wpb - 1) / wpb), dim3(64 * wpb), 0, (hipStream_t)stream,
+                       d_checks, count, d_verified, d_jobs, njobs, d_results, block_size);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

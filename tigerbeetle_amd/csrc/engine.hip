@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <new>
 #include <vector>
 
@@ -77,12 +78,27 @@ bool compute_layout(const tbc_tree *t, uint32_t block_size, Layout *L) {
 
 } // namespace
 
+// Pinned staging ring for host -> device streams (TableMemory.put, blocks read
+// from storage): the host copies into a slot, the engine stream copies the
+// slot to the device; a slot is reused once its copy's event has passed, so
+// a producer only waits when it runs kSlots slots ahead of the device.
+struct Staging {
+    static constexpr int kSlots = 8;
+    static constexpr uint64_t kSlotBytes = 8ull << 20;
+    uint8_t *base = nullptr;
+    hipEvent_t ev[kSlots] = {};
+    bool used[kSlots] = {};
+    int next = 0;
+};
+
 struct tbc_engine {
     int device = 0;
     uint32_t block_size = 0;
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr; // grid input validation beside the compaction (joined before results)
     Arena dev, host;
+    Staging staging;
     std::vector<hipEvent_t> event_pool;
     // Merge mask buffer (2 bits per merged position of a batch: 512 bytes
     // per tile). Batches run in stream order, so one buffer serves them all;
@@ -90,6 +106,76 @@ struct tbc_engine {
     uint64_t *masks = nullptr;
     uint64_t mask_words = 0;
 };
+
+struct tbc_grid {
+    tbc_engine *engine = nullptr;
+    uint8_t *base = nullptr;
+    uint64_t block_count = 0;
+    uint8_t *verified = nullptr; // device, per slot: written by the engine or validated (trusted like a cache hit)
+};
+
+struct tbc_memtable {
+    tbc_engine *engine = nullptr;
+    tbc_tree tree{};
+    uint8_t *values = nullptr;
+    uint32_t capacity = 0, count = 0;
+};
+
+static hipEvent_t take_event(tbc_engine *e) {
+    if (e->event_pool.empty()) {
+        hipEvent_t ev;
+        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+        return ev;
+    }
+    hipEvent_t ev = e->event_pool.back();
+    e->event_pool.pop_back();
+    return ev;
+}
+
+// Host -> device through the pinned ring, enqueued on the engine stream.
+static bool stage_h2d(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    Staging &st = e->staging;
+    const uint8_t *s = (const uint8_t *)src;
+    uint8_t *d = (uint8_t *)dst;
+    while (bytes) {
+        const int slot = st.next;
+        st.next = (st.next + 1) % Staging::kSlots;
+        if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return false;
+        const uint64_t n = bytes < Staging::kSlotBytes ? bytes : Staging::kSlotBytes;
+        uint8_t *p = st.base + (uint64_t)slot * Staging::kSlotBytes;
+        memcpy(p, s, n);
+        if (hipMemcpyAsync(d, p, n, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            hipEventRecord(st.ev[slot], e->stream) != hipSuccess)
+            return false;
+        st.used[slot] = true;
+        s += n;
+        d += n;
+        bytes -= n;
+    }
+    return true;
+}
+
+// Device -> host through the pinned ring (waits for each chunk).
+static bool stage_d2h(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    Staging &st = e->staging;
+    const uint8_t *s = (const uint8_t *)src;
+    uint8_t *d = (uint8_t *)dst;
+    while (bytes) {
+        const int slot = st.next;
+        st.next = (st.next + 1) % Staging::kSlots;
+        const uint64_t n = bytes < Staging::kSlotBytes ? bytes : Staging::kSlotBytes;
+        uint8_t *p = st.base + (uint64_t)slot * Staging::kSlotBytes;
+        if (hipMemcpyAsync(p, s, n, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipEventRecord(st.ev[slot], e->stream) != hipSuccess || hipEventSynchronize(st.ev[slot]) != hipSuccess)
+            return false;
+        st.used[slot] = true;
+        memcpy(d, p, n);
+        s += n;
+        d += n;
+        bytes -= n;
+    }
+    return true;
+}
 
 static bool ensure_masks(tbc_engine *e, uint64_t words) {
     if (words <= e->mask_words) return true;
@@ -116,6 +202,7 @@ struct tbc_batch {
     std::vector<uint32_t> info_base; // per original job index
     std::vector<uint32_t> status;    // host-side validation status per job
     hipEvent_t done = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;          // side-stream validation (grid inputs)
     hipEvent_t marks[kMaxMarks] = {};
     const char *mark_names[kMaxMarks] = {};
     int nmarks = 0;
@@ -123,8 +210,30 @@ struct tbc_batch {
     tbc_status result = TBC_PENDING;
 };
 
+// TBC_DEBUG_SYNC=1 (tools only): wait up to 5 s for every stage of a batch
+// and name the one that does not finish.
+static void debug_stage(hipStream_t s, const char *name) {
+    static const bool on = getenv("TBC_DEBUG_SYNC") != nullptr;
+    if (!on) return;
+    for (int i = 0; i < 5000; i++) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) {
+            fprintf(stderr, "tbc debug: stage %s done\n", name);
+            return;
+        }
+        if (q != hipErrorNotReady) {
+            fprintf(stderr, "tbc debug: stage %s error %d\n", name, (int)q);
+            return;
+        }
+        struct timespec ts = {0, 1000000};
+        nanosleep(&ts, nullptr);
+    }
+    fprintf(stderr, "tbc debug: stage %s NOT DONE after 5 s\n", name);
+}
+
 static void mark_cb(void *ctx, const char *name) {
     tbc_batch *b = (tbc_batch *)ctx;
+    debug_stage(b->engine->stream, name);
     if (!(b->engine->flags & TBC_CONFIG_PROFILE) || b->nmarks >= kMaxMarks) return;
     hipEventRecord(b->marks[b->nmarks], b->engine->stream);
     b->mark_names[b->nmarks++] = name;
@@ -165,6 +274,15 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
         delete e;
         return TBC_ERR_OUT_OF_MEMORY;
     }
+    bool ok = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
+              hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
+                  hipSuccess;
+    for (int s = 0; ok && s < Staging::kSlots; s++)
+        ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        tbc_engine_deinit(e);
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
     *out_engine = e;
     return TBC_OK;
 }
@@ -173,12 +291,135 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (!e) return;
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
+    if (e->side) hipStreamSynchronize(e->side);
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
+    for (int s = 0; s < Staging::kSlots; s++)
+        if (e->staging.ev[s]) hipEventDestroy(e->staging.ev[s]);
+    if (e->staging.base) hipHostFree(e->staging.base);
     hipHostFree(e->host.base);
     hipFree(e->dev.base);
     if (e->masks) hipFree(e->masks);
+    if (e->side) hipStreamDestroy(e->side);
     hipStreamDestroy(e->stream);
     delete e;
+}
+
+tbc_status tbc_grid_init(tbc_engine *e, uint64_t block_count, tbc_grid **out) {
+    if (!e || !out || block_count == 0) return TBC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    hipSetDevice(e->device);
+    tbc_grid *g = new (std::nothrow) tbc_grid();
+    if (!g) return TBC_ERR_OUT_OF_MEMORY;
+    g->engine = e;
+    g->block_count = block_count;
+    if (hipMalloc((void **)&g->base, block_count * e->block_size) != hipSuccess) {
+        delete g;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    if (hipMalloc((void **)&g->verified, block_count) != hipSuccess ||
+        hipMemsetAsync(g->verified, 0, block_count, e->stream) != hipSuccess) {
+        if (g->verified) hipFree(g->verified);
+        hipFree(g->base);
+        delete g;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    *out = g;
+    return TBC_OK;
+}
+
+void tbc_grid_deinit(tbc_grid *g) {
+    if (!g) return;
+    hipSetDevice(g->engine->device);
+    hipStreamSynchronize(g->engine->stream);
+    hipStreamSynchronize(g->engine->side);
+    hipFree(g->verified);
+    hipFree(g->base);
+    delete g;
+}
+
+tbc_status tbc_grid_block_pointer(const tbc_grid *g, uint64_t address, void **out) {
+    if (!g || !out || address == 0 || address > g->block_count) return TBC_ERR_INVALID_ARGUMENT;
+    *out = g->base + (address - 1) * g->engine->block_size;
+    return TBC_OK;
+}
+
+tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *blocks, uint32_t count) {
+    if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < count; i++)
+        if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
+    tbc_engine *e = g->engine;
+    hipSetDevice(e->device);
+    for (uint32_t i = 0; i < count; i++) {
+        if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size) ||
+            hipMemsetAsync(g->verified + addresses[i] - 1, 0, 1, e->stream) != hipSuccess) // validate before trusting
+            return TBC_ERR_DEVICE;
+    }
+    return TBC_OK;
+}
+
+tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *const *blocks, uint32_t count) {
+    if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < count; i++)
+        if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
+    tbc_engine *e = g->engine;
+    hipSetDevice(e->device);
+    for (uint32_t i = 0; i < count; i++)
+        if (!stage_d2h(e, blocks[i], g->base + (addresses[i] - 1) * e->block_size, e->block_size))
+            return TBC_ERR_DEVICE;
+    return TBC_OK;
+}
+
+tbc_status tbc_memtable_init(tbc_engine *e, const tbc_tree *tree, uint32_t capacity, tbc_memtable **out) {
+    if (!e || !tree || !out) return TBC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    Layout L;
+    if (!compute_layout(tree, e->block_size, &L) || capacity == 0 || capacity > tree->table_value_count_max)
+        return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    tbc_memtable *m = new (std::nothrow) tbc_memtable();
+    if (!m) return TBC_ERR_OUT_OF_MEMORY;
+    m->engine = e;
+    m->tree = *tree;
+    m->capacity = capacity;
+    // +16: buffers are readable past the last value (sort/merge key loads of a 16-byte value).
+    if (hipMalloc((void **)&m->values, (uint64_t)capacity * tree->value_size + 16) != hipSuccess) {
+        delete m;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    *out = m;
+    return TBC_OK;
+}
+
+void tbc_memtable_deinit(tbc_memtable *m) {
+    if (!m) return;
+    hipSetDevice(m->engine->device);
+    hipStreamSynchronize(m->engine->stream);
+    hipFree(m->values);
+    delete m;
+}
+
+tbc_status tbc_memtable_put(tbc_memtable *m, const void *values, uint32_t count) {
+    if (!m || (count && !values)) return TBC_ERR_INVALID_ARGUMENT;
+    if ((uint64_t)m->count + count > m->capacity) return TBC_ERR_CAPACITY; // table_memory.zig:80
+    if (!count) return TBC_OK;
+    hipSetDevice(m->engine->device);
+    const uint64_t vs = m->tree.value_size;
+    if (!stage_h2d(m->engine, m->values + m->count * vs, values, count * vs)) return TBC_ERR_DEVICE;
+    m->count += count;
+    return TBC_OK;
+}
+
+tbc_status tbc_memtable_values(const tbc_memtable *m, void **out_values, uint32_t *out_count) {
+    if (!m || !out_values || !out_count) return TBC_ERR_INVALID_ARGUMENT;
+    *out_values = m->values;
+    *out_count = m->count;
+    return TBC_OK;
+}
+
+tbc_status tbc_memtable_reset(tbc_memtable *m) {
+    if (!m) return TBC_ERR_INVALID_ARGUMENT;
+    m->count = 0;
+    return TBC_OK;
 }
 
 tbc_status tbc_tree_layout_get(const tbc_engine *e, const tbc_tree *tree, tbc_tree_layout *out) {
@@ -432,28 +673,68 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     for (uint32_t i = 0; i < count; i++)
         maybe_sparse |= jobs_in[i].a_immutable || jobs_in[i].drop_tombstones ||
                         jobs_in[i].tree.usage == TBC_USAGE_SECONDARY_INDEX;
+    // Input segments per job (device pointer of the first value, count): given
+    // directly, or (grid) one per data block of each input table, the
+    // pointers filled on the device from the tables' index blocks.
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> seg_in(2 * (size_t)count);
+    std::vector<InputCheck> checks;      // index blocks now, data blocks' slots filled by k_grid_resolve
+    std::vector<ResolveItem> resolve;    // seg field: (job, side, segment) until the bases are known
+    std::vector<uint32_t> resolve_side;
+    const bool grid_mode = (flags0 & TBC_COMPACTION_GRID) != 0;
+    tbc_grid *grid0 = grid_mode && count ? jobs_in[0].grid : nullptr;
     for (uint32_t i = 0; i < count; i++) {
         const tbc_compaction &c = jobs_in[i];
         JobDesc &d = hj[i];
         memset(&d, 0, sizeof d);
         Layout L;
+        const bool grid = (c.flags & TBC_COMPACTION_GRID) != 0;
         if (!compute_layout(&c.tree, e->block_size, &L) || L.index_size > kIndexLdsMax ||
-            (c.a_immutable && c.segment_count_a > 1) || !c.output_blocks ||
-            (c.segment_count_a && !c.segments_a) || (c.segment_count_b && !c.segments_b) ||
-            (c.address_count && !c.addresses) || (c.flags & ~TBC_COMPACTION_VALUES_ONLY) || c.flags != flags0) {
+            (c.a_immutable && c.segment_count_a > 1) || (!grid && !c.output_blocks) ||
+            (c.segment_count_a && !c.segments_a) || (!grid && c.segment_count_b && !c.segments_b) ||
+            (c.address_count && !c.addresses) ||
+            (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID)) || c.flags != flags0 ||
+            (grid && ((c.flags & TBC_COMPACTION_VALUES_ONLY) || c.grid != grid0 || !c.grid || c.grid->engine != e ||
+                      (c.table_count_a && (c.a_immutable || !c.tables_a)) || (c.table_count_b && !c.tables_b) ||
+                      (!c.a_immutable && c.segment_count_a)))) {
             delete b;
             return TBC_ERR_INVALID_ARGUMENT;
         }
+        if (grid)
+            for (uint32_t a = 0; a < c.address_count; a++)
+                if (c.addresses[a] == 0 || c.addresses[a] > c.grid->block_count) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
         uint64_t na = 0, nb = 0;
-        for (uint32_t s = 0; s < c.segment_count_a; s++) {
-            const tbc_segment &g = c.segments_a[s];
-            if (!g.count || !g.values || ((uintptr_t)g.values & 15)) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
-            na += g.count;
-        }
-        for (uint32_t s = 0; s < c.segment_count_b; s++) {
-            const tbc_segment &g = c.segments_b[s];
-            if (!g.count || !g.values || ((uintptr_t)g.values & 15)) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
-            nb += g.count;
+        for (int side = 0; side < 2; side++) {
+            auto &out_segs = seg_in[2 * (size_t)i + side];
+            uint64_t &n_side = side == 0 ? na : nb;
+            const uint32_t ntab = grid ? (side == 0 ? c.table_count_a : c.table_count_b) : 0;
+            for (uint32_t t = 0; t < ntab; t++) {
+                const tbc_table_ref &r = (side == 0 ? c.tables_a : c.tables_b)[t];
+                const uint64_t nblk = (r.value_count + L.vcm - 1) / L.vcm;
+                if (r.address == 0 || r.address > c.grid->block_count || r.value_count == 0 || nblk > L.dbcm) {
+                    delete b;
+                    return TBC_ERR_INVALID_ARGUMENT;
+                }
+                const uint64_t index_ptr = (uint64_t)(uintptr_t)c.grid->base + (r.address - 1) * e->block_size;
+                checks.push_back(InputCheck{index_ptr, r.address, {r.checksum[0], r.checksum[1]}, (uint32_t)nblk, i,
+                                            4u, 0u});
+                for (uint64_t k = 0; k < nblk; k++) {
+                    const uint32_t cnt = (uint32_t)std::min<uint64_t>(L.vcm, r.value_count - k * L.vcm);
+                    resolve.push_back(ResolveItem{index_ptr, (uint32_t)k, (uint32_t)out_segs.size(), 0u, cnt, i,
+                                                  L.cks_off, L.addr_off, 0u});
+                    resolve_side.push_back((uint32_t)side);
+                    out_segs.push_back({0, cnt}); // pointer from the index block, on the device
+                    n_side += cnt;
+                }
+            }
+            const uint32_t ns = grid ? (side == 0 && c.a_immutable ? c.segment_count_a : 0)
+                                     : (side == 0 ? c.segment_count_a : c.segment_count_b);
+            for (uint32_t s = 0; s < ns; s++) {
+                const tbc_segment &g = (side == 0 ? c.segments_a : c.segments_b)[s];
+                const uint64_t ptr = (uint64_t)(uintptr_t)g.values;
+                if (!g.count || !ptr || (ptr & 15)) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
+                out_segs.push_back({ptr, g.count});
+                n_side += g.count;
+            }
         }
         if (na + nb > 0xffff0000ull) { delete b; return TBC_ERR_INVALID_ARGUMENT; }
         const uint64_t n = na + nb;
@@ -480,17 +761,18 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         d.cluster_lo = c.cluster[0];
         d.cluster_hi = c.cluster[1];
         d.snapshot_min = c.snapshot_min;
-        d.a.nseg = c.segment_count_a;
+        d.a.nseg = (uint32_t)seg_in[2 * (size_t)i].size();
         d.a.n = (uint32_t)na;
-        d.b.nseg = c.segment_count_b;
+        d.b.nseg = (uint32_t)seg_in[2 * (size_t)i + 1].size();
         d.b.n = (uint32_t)nb;
         d.address_count = c.address_count;
-        d.out_blocks = (uint8_t *)c.output_blocks;
+        d.out_blocks = grid ? nullptr : (uint8_t *)c.output_blocks;
+        d.grid_base = grid ? c.grid->base : nullptr;
         d.tile_count = (uint32_t)((n + kMergeTile - 1) / kMergeTile);
         d.dblock_max = (uint32_t)db_max;
         d.table_max = (uint32_t)tables_max;
         d.job_index = i;
-        seg_words += 2ull * (c.segment_count_a + c.segment_count_b) + 2;
+        seg_words += 2ull * (seg_in[2 * (size_t)i].size() + seg_in[2 * (size_t)i + 1].size()) + 2;
         addr_words += c.address_count;
         order[i] = i;
     }
@@ -526,7 +808,10 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
     const uint64_t sz_addr = align_up(8 * addr_words, 256);
     const uint64_t sz_order = align_up(sizeof(TileRef) * (uint64_t)tiles, 256);
-    const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order;
+    const uint64_t n_checks = checks.size() + resolve.size(); // index blocks, then data blocks
+    const uint64_t sz_checks = align_up(sizeof(InputCheck) * n_checks, 256);
+    const uint64_t sz_resolve = align_up(sizeof(ResolveItem) * (uint64_t)resolve.size(), 256);
+    const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order + sz_checks + sz_resolve;
     const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8, 256);
@@ -565,20 +850,22 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     const uint64_t dev_pre = dev_seg + 8 * seg_ptr_words;
     const uint64_t dev_addr = (uint64_t)(uintptr_t)(d_in + sz_jobs + sz_segs);
     uint64_t sp = 0, ap = 0;
+    std::vector<uint64_t> seg_base(2 * (size_t)count);
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
         const tbc_compaction &c = jobs_in[d.job_index];
         for (int side = 0; side < 2; side++) {
-            const tbc_segment *segs = side == 0 ? c.segments_a : c.segments_b;
-            const uint32_t ns = side == 0 ? c.segment_count_a : c.segment_count_b;
+            const auto &segs = seg_in[2 * (size_t)d.job_index + side];
+            seg_base[2 * (size_t)d.job_index + side] = sp;
+            const uint32_t ns = (uint32_t)segs.size();
             Stream &st = side == 0 ? d.a : d.b;
             st.seg_ptr = (const uint64_t *)(uintptr_t)(dev_seg + 8 * sp);
             st.seg_pre = (const uint32_t *)(uintptr_t)(dev_pre + 4 * sp);
             uint32_t pre = 0;
             for (uint32_t s = 0; s < ns; s++) {
-                hseg[sp + s] = (uint64_t)(uintptr_t)segs[s].values;
+                hseg[sp + s] = segs[s].first;
                 hpre[sp + s] = pre;
-                pre += segs[s].count;
+                pre += segs[s].second;
             }
             hpre[sp + ns] = pre;
             sp += ns + 1;
@@ -588,6 +875,17 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         ap += c.address_count;
     }
     memcpy(h_in, sj.data(), sizeof(JobDesc) * count);
+    InputCheck *hchecks = (InputCheck *)(h_in + sz_jobs + sz_segs + sz_addr + sz_order);
+    InputCheck *d_checks = (InputCheck *)(d_in + sz_jobs + sz_segs + sz_addr + sz_order);
+    ResolveItem *hres = (ResolveItem *)(h_in + sz_jobs + sz_segs + sz_addr + sz_order + sz_checks);
+    const ResolveItem *d_resolve = (const ResolveItem *)(d_in + sz_jobs + sz_segs + sz_addr + sz_order + sz_checks);
+    if (!checks.empty()) memcpy(hchecks, checks.data(), sizeof(InputCheck) * checks.size());
+    for (size_t r = 0; r < resolve.size(); r++) {
+        ResolveItem it = resolve[r];
+        it.seg = (uint32_t)(seg_base[2 * (size_t)it.job + resolve_side[r]] + it.seg);
+        it.check = (uint32_t)(checks.size() + r);
+        hres[r] = it;
+    }
     // Tile order: per key kind (contiguous jobs), round-robin over the jobs.
     TileRef *horder = (TileRef *)(h_in + sz_jobs + sz_segs + sz_addr);
     const TileRef *d_order = (const TileRef *)(d_in + sz_jobs + sz_segs + sz_addr);
@@ -629,6 +927,28 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     // Tile status, block tiles and results start zeroed (contiguous).
     ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");
+    // Grid inputs: the data blocks found through the index blocks, the header
+    // checks of every input block in stream order (cheap), and the blocks
+    // staged from storage validated (AEGIS, latency-bound) on the side
+    // stream concurrently with the compaction; joined before the results.
+    if (ok && grid_mode && n_checks) {
+        ok = launch_grid_resolve(d_resolve, (uint32_t)resolve.size(), (uint64_t *)(uintptr_t)dev_seg,
+                                 d_checks, grid0->base, grid0->block_count, e->block_size, d_res,
+                                 s) == 0 &&
+             launch_grid_checks(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
+                                d_res, e->block_size, s) == 0;
+        b->fork = take_event(e);
+        b->join = take_event(e);
+        ok = ok && b->fork && b->join && hipEventRecord(b->fork, s) == hipSuccess &&
+             hipStreamWaitEvent(e->side, b->fork, 0) == hipSuccess &&
+             launch_grid_validate(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
+                                  d_res, e->block_size, e->side) == 0 &&
+             hipEventRecord(b->join, e->side) == hipSuccess;
+    }
+    if (grid_mode && n_checks) {
+        debug_stage(e->side, "grid_validate(side)");
+        mark_cb(b, "grid_check");
+    }
     if (ok && count)
         ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile,
                           d_order, d_res, s, mark_cb, b) == 0;
@@ -636,10 +956,15 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
                            d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0, maybe_sparse, s, mark_cb,
                            b) == 0;
+    // Outputs written by the engine are trusted like the reference's grid
+    // cache entries (grid.zig:802-841).
+    if (ok && grid_mode) ok = launch_grid_mark((const JobDesc *)d_in, (int)count, grid0->verified, s) == 0;
+    if (ok && b->join) ok = hipStreamWaitEvent(s, b->join, 0) == hipSuccess;
     ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     if (!ok) {
         hipStreamSynchronize(s);
+        hipStreamSynchronize(e->side);
         tbc_batch_release(b);
         return TBC_ERR_DEVICE;
     }
@@ -653,6 +978,7 @@ static tbc_status batch_finish(tbc_batch *b) {
     for (uint32_t i = 0; i < b->count; i++) {
         JobResultDev &r = b->h_results[i];
         if (r.invariant) r.status = TBC_ERR_INVARIANT;
+        if (r.block_error) r.status = TBC_ERR_BLOCK_INVALID;
         if (r.status != TBC_OK && b->result == TBC_OK) b->result = (tbc_status)r.status;
     }
     return b->result;
@@ -665,6 +991,7 @@ tbc_status tbc_batch_poll(tbc_batch *b) {
     hipError_t q = hipEventQuery(b->done);
     if (q == hipErrorNotReady) return TBC_PENDING;
     if (q != hipSuccess) {
+        fprintf(stderr, "tbc: batch failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
         b->complete = true;
         b->result = TBC_ERR_DEVICE;
         return b->result;
@@ -682,6 +1009,7 @@ tbc_status tbc_batch_wait(tbc_batch *b) {
     while ((q = hipEventQuery(b->done)) == hipErrorNotReady) {
     }
     if (q != hipSuccess) {
+        fprintf(stderr, "tbc: batch failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
         b->complete = true;
         b->result = TBC_ERR_DEVICE;
         return b->result;
@@ -732,6 +1060,8 @@ void tbc_batch_release(tbc_batch *b) {
     for (int m = 0; m < kMaxMarks; m++)
         if (b->marks[m]) e->event_pool.push_back(b->marks[m]);
     if (b->done) e->event_pool.push_back(b->done);
+    if (b->fork) e->event_pool.push_back(b->fork);
+    if (b->join) e->event_pool.push_back(b->join);
     if (b->h_results) {
         // LIFO release restores the arena tops; otherwise reclaim when idle.
         if (e->dev.live) e->dev.live--;

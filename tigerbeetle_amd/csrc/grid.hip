@@ -1,0 +1,118 @@
+// grid.hip — the GPU-resident grid's side of a compaction batch.
+//
+// The reference reads a compaction's inputs through the grid
+// (src/vsr/grid.zig:843-890): a cache hit is trusted once its header
+// checksum equals the one the index block (or manifest) expects
+// (read_block_from_cache, :802-841); a block read from storage is validated
+// first (read_block_validate, :1059-1084). The table iterators then walk an
+// input table's index block for its data blocks' addresses and checksums
+// (table_data_iterator.zig, level_data_iterator.zig:142-224). Here the whole
+// grid zone is resident in HBM, so a batch:
+//   k_grid_resolve  finds every input data block through its table's index
+//                   block (address, checksum) and fills the merge's segment
+//                   table — the host only knows TableInfos, as Compaction does;
+//   k_grid_check    applies read_block_from_cache's checks plus the header
+//                   fields the iterators assert, to every input block (cheap);
+//   k_grid_validate (aegis.hip) runs read_block_validate on the blocks staged
+//                   from storage, on a second stream beside the compaction;
+//   k_grid_mark     trusts the batch's outputs (written by the engine itself).
+#include <hip/hip_runtime.h>
+
+#include "tbc_internal.h"
+
+namespace tbc {
+
+__device__ __forceinline__ void grid_error(uint32_t *slot, uint32_t code) {
+    uint32_t expected = 0;
+    __hip_atomic_compare_exchange_strong(slot, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One thread per input data block: TableIndex.data_addresses[k] and
+// data_checksums[k] (schema.zig:80-260) from the table's index block. An
+// address outside the grid (a corrupt index block that slipped past its
+// checks) is reported and replaced by the index block itself, so every later
+// load stays inside the grid.
+__global__ __launch_bounds__(256) void k_grid_resolve(const ResolveItem *items, uint32_t count, uint64_t *seg_ptr,
+                                                      InputCheck *checks, const uint8_t *grid_base,
+                                                      uint64_t grid_blocks, uint32_t block_size, JobResultDev *res) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const ResolveItem it = items[i];
+    const uint8_t *idx = (const uint8_t *)(uintptr_t)it.index_ptr;
+    uint64_t address = gld<uint64_t>(idx + it.addr_off + 8 * it.k);
+    const uint64_t ck_lo = gld<uint64_t>(idx + it.cks_off + 32 * it.k);
+    const uint64_t ck_hi = gld<uint64_t>(idx + it.cks_off + 32 * it.k + 8);
+    uint64_t blk = (uint64_t)(uintptr_t)grid_base + (address - 1) * block_size;
+    if (address == 0 || address > grid_blocks) {
+        grid_error(&res[it.job].block_error, 7u);
+        blk = it.index_ptr;
+        address = 0; // k_grid_check / k_grid_validate skip it
+    }
+    seg_ptr[it.seg] = blk + kHeaderSize;
+    InputCheck c;
+    c.ptr = blk;
+    c.address = address;
+    c.checksum[0] = ck_lo;
+    c.checksum[1] = ck_hi;
+    c.value_count = it.value_count;
+    c.job = it.job;
+    c.kind = 5; // BlockType.data
+    c.pad = 0;
+    checks[it.check] = c;
+}
+
+// One thread per trusted input block (index and data; blocks staged from
+// storage are k_grid_validate's): read_block_from_cache's cache-hit test (the
+// header checksum is the expected one; address and cluster match,
+// grid.zig:818-835) and the header fields the compaction's iterators assert.
+__global__ __launch_bounds__(256) void k_grid_check(const InputCheck *checks, uint32_t count, const uint8_t *verified,
+                                                    const JobDesc *jobs, int njobs, JobResultDev *res,
+                                                    uint32_t block_size) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const InputCheck c = checks[i];
+    if (c.address == 0 || !verified[c.address - 1]) return; // resolve reported it / the validation's
+    const uint8_t *blk = (const uint8_t *)(uintptr_t)c.ptr;
+    uint32_t r;
+    if (gld<uint64_t>(blk) != c.checksum[0] || gld<uint64_t>(blk + 8) != c.checksum[1])
+        r = 4; // not the block the index/manifest names (a cache miss in the reference)
+    else if (gld<uint64_t>(blk + 224) != c.address)
+        r = 5;
+    else
+        r = grid_header_check(job_of_result(jobs, njobs, c.job), c, block_size);
+    if (r) grid_error(&res[c.job].block_error, r);
+}
+
+// Outputs of the batch's grid jobs are trusted from now on (every reserved
+// address: unused ones are never named by an index block of this batch).
+__global__ __launch_bounds__(256) void k_grid_mark(const JobDesc *jobs, int njobs, uint8_t *verified) {
+    const JobDesc &j = jobs[blockIdx.x];
+    if (!j.grid_base) return;
+    for (uint32_t a = threadIdx.x; a < j.address_count; a += 256) verified[gld<uint64_t>(j.addresses + a) - 1] = 1;
+}
+
+int launch_grid_resolve(const ResolveItem *d_items, uint32_t count, uint64_t *d_seg_ptr, InputCheck *d_checks,
+                        const uint8_t *grid_base, uint64_t grid_blocks, uint32_t block_size, JobResultDev *d_results,
+                        void *stream) {
+    if (!count) return 0;
+    hipLaunchKernelGGL(k_grid_resolve, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_items, count,
+                       d_seg_ptr, d_checks, grid_base, grid_blocks, block_size, d_results);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t *d_verified, const JobDesc *d_jobs,
+                       int njobs, JobResultDev *d_results, uint32_t block_size, void *stream) {
+    if (!count) return 0;
+    hipLaunchKernelGGL(k_grid_check, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_checks, count,
+                       d_verified, d_jobs, njobs, d_results, block_size);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, void *stream) {
+    if (!njobs) return 0;
+    hipLaunchKernelGGL(k_grid_mark, dim3(njobs), dim3(256), 0, (hipStream_t)stream, d_jobs, njobs, d_verified);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace tbc

@@ -62,6 +62,8 @@ struct JobDesc {
     uint32_t table_base, table_max;      // index-block groups (upper bound)
     uint32_t info_base;                  // first TableInfo slot in the batch's info buffer
     uint32_t job_index;
+    // TBC_COMPACTION_GRID: output block `slot` lives at grid_base + (addresses[slot] - 1) * block_size.
+    uint8_t *grid_base;
 };
 
 struct SplitDesc {
@@ -84,7 +86,34 @@ struct JobResultDev {
     uint32_t table_count;
     uint32_t block_count;
     uint32_t status;
-    uint32_t invariant; // nonzero if an input broke a reference invariant
+    uint32_t invariant;   // nonzero if an input broke a reference invariant
+    uint32_t block_error; // nonzero if a grid input block failed its checks (tbc_block_check code)
+};
+
+// One grid input block of a batch (TBC_COMPACTION_GRID): the cache-hit checks
+// of read_block_from_cache (grid.zig:802-841) plus the header fields the
+// compaction relies on, and for blocks staged from storage the full
+// read_block_validate (grid.zig:1059-1084).
+struct InputCheck {
+    uint64_t ptr;         // device pointer of the block
+    uint64_t address;
+    uint64_t checksum[2]; // expected header checksum
+    uint32_t value_count; // data block: its values; index block: the table's data blocks
+    uint32_t job;         // JobResultDev index
+    uint32_t kind;        // schema.zig BlockType: 5 data, 4 index
+    uint32_t pad;
+};
+
+// One data block of a grid input table, found through the table's index
+// block (TableIndex.data_addresses / data_checksums, schema.zig:80-260).
+struct ResolveItem {
+    uint64_t index_ptr;    // the table's index block in the grid
+    uint32_t k;            // data block ordinal in the table
+    uint32_t seg;          // global segment slot (Stream::seg_ptr entry) to fill
+    uint32_t check;        // InputCheck slot to fill
+    uint32_t value_count;  // values of the block (full except the table's last)
+    uint32_t job;          // JobResultDev index
+    uint32_t cks_off, addr_off; // index layout of the job's tree
     uint32_t pad;
 };
 
@@ -105,6 +134,40 @@ __host__ __device__ inline uint64_t sector_ceil(uint64_t x) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <class T> __device__ __forceinline__ T gld(const void *p) { return *(const TBC_GLOBAL T *)p; }
 template <class T> __device__ __forceinline__ void gst(void *p, const T &v) { *(TBC_GLOBAL T *)p = v; }
+
+// Output block `slot` of job j (acquire order): a per-job arena, or the grid
+// slot of its acquired address.
+__device__ inline uint8_t *block_ptr(const JobDesc &j, uint32_t slot) {
+    if (j.grid_base) return j.grid_base + (size_t)(gld<uint64_t>(j.addresses + slot) - 1) * j.block_size;
+    return j.out_blocks + (size_t)slot * j.block_size;
+}
+
+// The header fields a compaction's table iterators assert of a grid input
+// block once its checksum and address are the expected ones: cluster,
+// command, block type and tree, and for a data block its value count, value
+// size and size (TableData.Metadata, schema.zig:264-275), for an index block
+// its data block count and layout (TableIndex.Metadata, schema.zig:87-98).
+// Returns 0, or 7 (TBC_BLOCK_UNEXPECTED_HEADER).
+__device__ inline uint32_t grid_header_check(const JobDesc &j, const InputCheck &c, uint32_t block_size) {
+    const uint8_t *blk = (const uint8_t *)(uintptr_t)c.ptr;
+    const uint32_t size = gld<uint32_t>(blk + 96);
+    bool ok = gld<uint64_t>(blk + 80) == j.cluster_lo && gld<uint64_t>(blk + 88) == j.cluster_hi &&
+              blk[110] == 20 && blk[240] == c.kind && gld<uint16_t>(blk + 140) == j.tree_id && size <= block_size;
+    if (c.kind == 5)
+        ok = ok && gld<uint32_t>(blk + 132) == c.value_count && gld<uint32_t>(blk + 136) == j.value_size &&
+             size == 256 + c.value_count * j.value_size;
+    else
+        ok = ok && gld<uint32_t>(blk + 128) == c.value_count && gld<uint32_t>(blk + 132) == j.dbcm &&
+             gld<uint32_t>(blk + 136) == j.key_size && size == j.index_size;
+    return ok ? 0u : 7u;
+}
+
+__device__ inline const JobDesc &job_of_result(const JobDesc *jobs, int njobs, uint32_t job_index) {
+    int found = 0;
+    for (int k = 0; k < njobs; k++)
+        if (jobs[k].job_index == job_index) found = k;
+    return jobs[found];
+}
 
 // Find the job owning global index `g` given a per-job base field (ascending).
 template <class F>
@@ -134,6 +197,18 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
                   void (*mark)(void *, const char *), void *mark_ctx);
 int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uint32_t count, uint32_t block_size,
                           uint8_t *d_out, void *stream);
+// Grid inputs of a batch (engine.hip): resolve data blocks from the index
+// blocks, header checks of every input block (cheap), the full
+// read_block_validate of the unverified ones (side stream), and marking the
+// outputs as trusted.
+int launch_grid_resolve(const ResolveItem *d_items, uint32_t count, uint64_t *d_seg_ptr, InputCheck *d_checks,
+                        const uint8_t *grid_base, uint64_t grid_blocks, uint32_t block_size, JobResultDev *d_results,
+                        void *stream);
+int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t *d_verified, const JobDesc *d_jobs,
+                       int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
+int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_verified, const JobDesc *d_jobs,
+                         int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
+int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, void *stream);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
 struct SortItem {

@@ -69,7 +69,10 @@ class Job:
     snapshot_min: int
     addresses: np.ndarray  # uint64, acquire order
     output: DeviceBuffer
-    flags: int = 0  # TBC_COMPACTION_* (abi.COMPACTION_VALUES_ONLY)
+    flags: int = 0  # TBC_COMPACTION_* (abi.COMPACTION_VALUES_ONLY, abi.COMPACTION_GRID)
+    grid: "Grid | None" = None   # COMPACTION_GRID: disk tables by reference, outputs into the grid
+    tables_a: list = field(default_factory=list)  # [(index address, index checksum u128, value_count)]
+    tables_b: list = field(default_factory=list)
     _keep: list = field(default_factory=list)
     _ctype: object = field(default=None, repr=False)
 
@@ -87,17 +90,24 @@ class Job:
         c.flags = self.flags
         sa, sb = _segment_table(self.segments_a), _segment_table(self.segments_b)
         addrs = np.ascontiguousarray(self.addresses, dtype=np.uint64)
-        self._keep = [sa, sb, addrs]
+        ra, rb = _table_ref_table(self.tables_a), _table_ref_table(self.tables_b)
+        self._keep = [sa, sb, addrs, ra, rb]
         c.segments_a = ctypes.cast(sa.ctypes.data, ctypes.POINTER(abi.Segment))
         c.segment_count_a = len(self.segments_a)
         c.segments_b = ctypes.cast(sb.ctypes.data, ctypes.POINTER(abi.Segment))
         c.segment_count_b = len(self.segments_b)
+        if self.flags & abi.COMPACTION_GRID:
+            c.grid = self.grid.handle
+            c.tables_a = ctypes.cast(ra.ctypes.data, ctypes.POINTER(abi.TableRef))
+            c.tables_b = ctypes.cast(rb.ctypes.data, ctypes.POINTER(abi.TableRef))
+            c.table_count_a = len(self.tables_a)
+            c.table_count_b = len(self.tables_b)
         c.cluster[0] = self.cluster & ((1 << 64) - 1)
         c.cluster[1] = self.cluster >> 64
         c.snapshot_min = self.snapshot_min
         c.addresses = addrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         c.address_count = len(addrs)
-        c.output_blocks = self.output.ptr
+        c.output_blocks = self.output.ptr if self.output is not None else None
         self._ctype = c
         return c
 
@@ -108,6 +118,83 @@ def _segment_table(segments: list) -> np.ndarray:
     if segments:
         t[: len(segments)] = np.asarray(segments, dtype=np.uint64).reshape(-1, 2)
     return t
+
+
+def _table_ref_table(refs: list) -> np.ndarray:
+    """tbc_table_ref[] as a (n, 4) uint64 array: {address, checksum lo, hi, value_count}."""
+    t = np.zeros((max(1, len(refs)), 4), dtype=np.uint64)
+    for i, (address, checksum, count) in enumerate(refs):
+        t[i] = (address, checksum & ((1 << 64) - 1), checksum >> 64, count)
+    return t
+
+
+class Grid:
+    """The GPU-resident grid (tbc_grid): blocks of addresses [1, block_count] in HBM."""
+
+    def __init__(self, engine: "Engine", block_count: int):
+        self.engine = engine
+        self.block_count = int(block_count)
+        h = ctypes.c_void_p()
+        check(lib().tbc_grid_init(engine.handle, self.block_count, ctypes.byref(h)), "tbc_grid_init")
+        self.handle = h.value
+
+    def pointer(self, address: int) -> int:
+        p = ctypes.c_void_p()
+        check(lib().tbc_grid_block_pointer(self.handle, int(address), ctypes.byref(p)), "tbc_grid_block_pointer")
+        return p.value
+
+    def put_blocks(self, addresses, images: np.ndarray) -> None:
+        """Stage host block images (n, block_size) uint8 as blocks read from storage."""
+        images = np.ascontiguousarray(images, dtype=np.uint8)
+        n = len(addresses)
+        A = np.ascontiguousarray(addresses, dtype=np.uint64)
+        P = (ctypes.c_void_p * max(1, n))(*[images.ctypes.data + i * images.shape[1] for i in range(n)])
+        check(lib().tbc_grid_put_blocks(self.handle, A.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), P, n),
+              "tbc_grid_put_blocks")
+
+    def get_blocks(self, addresses) -> np.ndarray:
+        n = len(addresses)
+        out = np.zeros((max(1, n), self.engine.block_size), dtype=np.uint8)
+        A = np.ascontiguousarray(addresses, dtype=np.uint64)
+        P = (ctypes.c_void_p * max(1, n))(*[out.ctypes.data + i * self.engine.block_size for i in range(n)])
+        check(lib().tbc_grid_get_blocks(self.handle, A.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), P, n),
+              "tbc_grid_get_blocks")
+        return out[:n]
+
+    def close(self) -> None:
+        if self.handle:
+            lib().tbc_grid_deinit(self.handle)
+            self.handle = None
+
+
+class Memtable:
+    """A TableMemory on the device (tbc_memtable): puts stream in through pinned staging."""
+
+    def __init__(self, engine: "Engine", tree: TreeSpec, capacity: int | None = None):
+        self.engine, self.tree = engine, tree
+        t = tree.ctype()
+        h = ctypes.c_void_p()
+        check(lib().tbc_memtable_init(engine.handle, ctypes.byref(t), int(capacity or tree.value_count_max),
+                                      ctypes.byref(h)), "tbc_memtable_init")
+        self.handle = h.value
+
+    def put(self, values: np.ndarray) -> None:
+        v = np.ascontiguousarray(values, dtype=np.uint8)
+        assert v.ndim == 2 and v.shape[1] == self.tree.value_size
+        check(lib().tbc_memtable_put(self.handle, v.ctypes.data, len(v)), "tbc_memtable_put")
+
+    def values(self):
+        p, n = ctypes.c_void_p(), ctypes.c_uint32()
+        check(lib().tbc_memtable_values(self.handle, ctypes.byref(p), ctypes.byref(n)), "tbc_memtable_values")
+        return p.value, n.value
+
+    def reset(self) -> None:
+        check(lib().tbc_memtable_reset(self.handle), "tbc_memtable_reset")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().tbc_memtable_deinit(self.handle)
+            self.handle = None
 
 
 class Batch:

@@ -1,0 +1,397 @@
+"""Host side of the forest's compaction schedule (restated for replays).
+
+In a TigerBeetle replica the GPU path sits under Zig code that stays on the
+host: `Forest.compact` -> `Groove.compact` -> `Tree.compact` decide, per
+beat, which compactions start (src/lsm/tree.zig:612-712) from the Manifest's
+levels (src/lsm/manifest.zig:470-574, manifest_level.zig:550-731), reserve
+their blocks in the FreeSet (src/vsr/free_set.zig:225-345), and apply their
+output tables to the Manifest at the half-bar end (tree.zig:876-976,
+compaction.zig:936-985). To replay a workload through the engine (BASELINE
+config 1: `tigerbeetle benchmark`'s load, benchmark_load.py) this module
+restates that host logic; the compactions themselves run on an `executor`
+(the GPU grid executor below, or the oracle in tests).
+
+Simplifications, stated in DESIGN.md §10: blocks released by compactions
+go to the FreeSet's staging and are only reusable after a checkpoint
+(free_set.zig:383-390); a replay never checkpoints, so they are never
+reused. The manifest log's own block reservations are not simulated
+(manifest_log.zig:647-684), so addresses differ from a replica's by those
+blocks; every address a compaction uses is still a FreeSet acquire from its
+own reservation.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, replace
+
+import numpy as np
+
+from . import trees
+from .tables import SNAPSHOT_LATEST, TableInfo
+
+LSM_LEVELS = trees.LSM_LEVELS            # config.zig:140
+GROWTH = trees.LSM_GROWTH_FACTOR         # config.zig:141
+BAR = trees.LSM_BATCH_MULTIPLE           # config.zig:142
+HALF = BAR // 2
+
+
+def table_count_max_for_level(level: int) -> int:
+    """tree.zig:1114-1119."""
+    return GROWTH ** (level + 1)
+
+
+def compaction_op_min(op: int) -> int:
+    """tree.zig:1093-1095."""
+    return op - op % HALF
+
+
+def snapshot_min_for_table_output(op_min: int) -> int:
+    """compaction.zig:981-985."""
+    return op_min + HALF
+
+
+def snapshot_max_for_table_input(op_min: int) -> int:
+    """compaction.zig:977-979."""
+    return snapshot_min_for_table_output(op_min) - 1
+
+
+class FreeSet:
+    """FreeSet.reserve/acquire/forfeit (free_set.zig:225-345) over a bitmap."""
+
+    def __init__(self, block_count: int):
+        self.acquired = np.zeros(block_count, dtype=bool)
+        self.reservation_blocks = 0
+        self.reservation_count = 0
+
+    def reserve(self, count: int) -> tuple:
+        base = self.reservation_blocks
+        free = np.flatnonzero(~self.acquired[base:])
+        if len(free) < count:
+            raise RuntimeError("grid full: raise the replay's block count")
+        end = base + int(free[count - 1]) + 1
+        self.reservation_blocks = end
+        self.reservation_count += 1
+        return (base, end - base)
+
+    def addresses(self, reservation: tuple) -> np.ndarray:
+        """The acquire() sequence of a reservation: its free blocks in order."""
+        base, count = reservation
+        return (np.flatnonzero(~self.acquired[base:base + count]) + base + 1).astype(np.uint64)
+
+    def acquire(self, addresses) -> None:
+        a = np.asarray(addresses, dtype=np.int64)
+        assert not self.acquired[a - 1].any()
+        self.acquired[a - 1] = True
+
+    def forfeit(self) -> None:
+        self.reservation_count -= 1
+        if self.reservation_count == 0:
+            self.reservation_blocks = 0
+
+
+class Level:
+    """ManifestLevel: tables ordered by (key_max, snapshot_min)."""
+
+    def __init__(self):
+        self.tables: list = []
+
+    def visible(self) -> list:
+        return [t for t in self.tables if t.snapshot_max == SNAPSHOT_LATEST]
+
+    def insert(self, t: TableInfo) -> None:
+        self.tables.append(t)
+        self.tables.sort(key=lambda x: (x.key_max, x.snapshot_min))
+
+    def overlapping(self, key_min: int, key_max: int, max_tables: int):
+        """tables_overlapping_with_key_range (manifest_level.zig:677-731)."""
+        kmin, kmax, found = key_min, key_max, []
+        for t in self.visible():
+            if t.key_max < key_min or t.key_min > key_max:
+                continue
+            kmin, kmax = min(kmin, t.key_min), max(kmax, t.key_max)
+            if len(found) == max_tables:
+                return None
+            found.append(t)
+        return (kmin, kmax, found)
+
+
+@dataclass
+class Compaction:
+    """One started Compaction (compaction.zig:84-99, 280-404)."""
+    tree: trees.TreeSpec
+    level_b: int
+    op_min: int
+    table_a: TableInfo | None           # None: the immutable table
+    range_b: tuple                      # (key_min, key_max, [TableInfo])
+    drop_tombstones: bool
+    move: bool
+    reservation: tuple | None = None
+    addresses: np.ndarray | None = None
+    outputs: list = field(default_factory=list)  # TableInfos (after the batch)
+    result: object = None
+
+    @property
+    def snapshot_min(self) -> int:
+        return snapshot_min_for_table_output(self.op_min)
+
+
+class Tree:
+    """One LSM tree's host state: mutable/immutable table bookkeeping, the
+    manifest's levels and the per-half-bar compactions."""
+
+    def __init__(self, spec: trees.TreeSpec):
+        self.spec = spec
+        self.levels = [Level() for _ in range(LSM_LEVELS)]
+        self.mutable_count = 0
+        self.mutable_keys = [None, None]      # (min, max) of the mutable table's keys
+        self.immutable_count = 0
+        self.immutable_keys = [None, None]
+        self.immutable_flushed = True
+        self.compactions: list = []
+
+    # -- TableMemory ------------------------------------------------------
+    def put_keys(self, n: int, key_min: int, key_max: int) -> None:
+        self.mutable_count += n
+        lo, hi = self.mutable_keys
+        self.mutable_keys = [key_min if lo is None else min(lo, key_min), key_max if hi is None else max(hi, key_max)]
+        assert self.mutable_count <= self.spec.value_count_max
+
+    def swap_mutable_and_immutable(self) -> bool:
+        """tree.zig:979-999; returns whether the new immutable table has values."""
+        assert self.immutable_flushed
+        self.immutable_count, self.immutable_keys = self.mutable_count, self.mutable_keys
+        self.immutable_flushed = self.immutable_count == 0
+        self.mutable_count, self.mutable_keys = 0, [None, None]
+        return self.immutable_count > 0
+
+    # -- Manifest ---------------------------------------------------------
+    def must_drop_tombstones(self, level_b: int, rng: tuple) -> bool:
+        """manifest.zig:547-574."""
+        for level_c in range(level_b + 1, LSM_LEVELS):
+            if self.levels[level_c].overlapping(rng[0], rng[1], 1 << 30)[2]:
+                return False
+        return True
+
+    def compaction_table(self, level_a: int):
+        """manifest.zig:484-512 + manifest_level.zig:550-594."""
+        la, lb = self.levels[level_a], self.levels[level_a + 1]
+        if len(la.visible()) < table_count_max_for_level(level_a):
+            return None
+        best = None
+        for t in la.visible():
+            r = lb.overlapping(t.key_min, t.key_max, GROWTH)
+            if r is None:
+                continue
+            if best is None or len(r[2]) < len(best[1][2]):
+                best = (t, r)
+            if not best[1][2]:
+                break
+        assert best is not None
+        return best
+
+    def start_half_bar(self, op: int, free_set: FreeSet) -> list:
+        """Tree.compact at a half-bar start (tree.zig:661-690): the immutable
+        table's compaction (odd half), then one per level pair."""
+        beat = op % BAR
+        odd = beat == HALF
+        op_min = compaction_op_min(op)
+        started = []
+        if odd and not self.immutable_flushed:
+            r = self.levels[0].overlapping(self.immutable_keys[0], self.immutable_keys[1], GROWTH)
+            assert r is not None
+            started.append(Compaction(self.spec, 0, op_min, None, r, self.must_drop_tombstones(0, r), False))
+        for level_a in range(1 if odd else 0, LSM_LEVELS - 1, 2):
+            sel = self.compaction_table(level_a)
+            if sel is None:
+                continue
+            t, r = sel
+            move = not r[2]
+            started.append(Compaction(self.spec, level_a + 1, op_min, t, r,
+                                      self.must_drop_tombstones(level_a + 1, r), move))
+        block_count_max = self.spec.layout()["block_count_max"]
+        for c in started:
+            if not c.move:  # compaction.zig:300-318
+                c.reservation = free_set.reserve((len(c.range_b[2]) + 1) * block_count_max)
+                c.addresses = free_set.addresses(c.reservation)
+        self.compactions = started
+        return started
+
+    def apply(self, c: Compaction) -> None:
+        """Compaction.apply_to_manifest (compaction.zig:939-973) and the
+        remove_invisible_tables calls of Tree.compact_end (tree.zig:905-960)."""
+        snap_max = snapshot_max_for_table_input(c.op_min)
+        lb = self.levels[c.level_b]
+        if c.move:
+            la = self.levels[c.level_b - 1]
+            la.tables.remove(c.table_a)
+            lb.insert(replace(c.table_a, level=c.level_b))
+            return
+        if c.table_a is not None:
+            la = self.levels[c.level_b - 1]
+            la.tables[la.tables.index(c.table_a)] = replace(c.table_a, snapshot_max=snap_max)
+        for t in c.range_b[2]:
+            lb.tables[lb.tables.index(t)] = replace(t, snapshot_max=snap_max)
+        for t in c.outputs:
+            lb.insert(t)
+        for level in {c.level_b, c.level_b - 1} - {-1}:
+            self.levels[level].tables = [t for t in self.levels[level].tables if t.snapshot_max == SNAPSHOT_LATEST]
+
+
+class Forest:
+    """Forest.compact over the trees a workload touches, in the forest's
+    order (grooves accounts, transfers; per groove: ids, objects, indexes:
+    forest.zig:319-342, groove.zig:1084-1104)."""
+
+    ORDER = ["accounts.id", "accounts.timestamp", "accounts.user_data_128", "accounts.user_data_64",
+             "accounts.user_data_32", "accounts.ledger", "accounts.code",
+             "transfers.id", "transfers.timestamp", "transfers.debit_account_id", "transfers.credit_account_id",
+             "transfers.amount", "transfers.pending_id", "transfers.user_data_128", "transfers.user_data_64",
+             "transfers.user_data_32", "transfers.timeout", "transfers.ledger", "transfers.code"]
+
+    def __init__(self, executor, block_count: int, cluster: int = 0):
+        self.executor = executor
+        self.free_set = FreeSet(block_count)
+        self.trees = {name: Tree(trees.BY_NAME[name]) for name in self.ORDER}
+        self.cluster = cluster
+        self.pending = None       # (batch handle, [Compaction]) of the running half-bar
+        self.history: list = []   # per half-bar: (op, [Compaction]) once applied
+
+    def put(self, name: str, values: np.ndarray, key_min: int, key_max: int) -> None:
+        self.trees[name].put_keys(len(values), key_min, key_max)
+        self.executor.put(name, values)
+
+    def compact(self, op: int) -> None:
+        """Forest.compact(op) (forest.zig:319-342) then compact_end."""
+        beat = op % BAR
+        if op >= BAR and beat in (0, HALF):
+            started = []
+            for name in self.ORDER:
+                for c in self.trees[name].start_half_bar(op, self.free_set):
+                    started.append((name, c))
+            jobs = [(name, c) for name, c in started if not c.move]
+            handle = self.executor.submit(jobs, self.cluster) if jobs else None
+            self.pending = (handle, started)
+        if op >= BAR and beat in (HALF - 1, BAR - 1):
+            handle, started = self.pending
+            if handle is not None:
+                self.executor.wait(handle, [c for _, c in started if not c.move])
+            odd = beat == BAR - 1
+            for name, c in started:  # immutable compactions first (tree.zig:905-927)
+                if c.table_a is None:
+                    self.trees[name].apply(c)
+                    self.trees[name].immutable_flushed = True
+                    self.executor.flushed(name)
+            for name, c in started:
+                if not c.move:
+                    self.free_set.acquire(c.addresses[:c.result.block_count])
+                    self.free_set.forfeit()
+                if c.table_a is not None:
+                    self.trees[name].apply(c)
+            assert odd or not any(c.table_a is None for _, c in started)
+            self.history.append((op, started))
+            self.pending = None
+        if beat == BAR - 1:
+            swapped = [name for name in self.ORDER if self.trees[name].swap_mutable_and_immutable()]
+            self.executor.swap(swapped)
+
+    def run(self, load_ops, progress=None) -> None:
+        """Commit every op of a workload: its puts, then Forest.compact(op)."""
+        for op in load_ops:
+            for name, values in op.puts.items():
+                spec = self.trees[name].spec
+                keys = key_range(values, spec)
+                self.put(name, values, keys[0], keys[1])
+            self.compact(op.op)
+            if progress:
+                progress(op.op)
+
+
+def key_range(values: np.ndarray, spec: trees.TreeSpec) -> tuple:
+    """(min, max) of key_from_value over a put batch, as integers."""
+    from . import workloads
+    limbs = workloads.keys_of(values, spec)
+
+    def extreme(pick):
+        idx = np.arange(len(limbs[0]))
+        for l in reversed(limbs):  # most significant limb first
+            v = l[idx]
+            idx = idx[v == pick(v)]
+        return sum(int(l[idx[0]]) << (64 * i) for i, l in enumerate(limbs))
+
+    return extreme(np.min), extreme(np.max)
+
+
+class GridExecutor:
+    """Runs a Forest's compactions on the GPU: memtables on the device
+    (tbc_memtable), the bar-end sorts as one segmented batch, each half-bar's
+    compactions as one batch over the GPU-resident grid."""
+
+    def __init__(self, engine, grid, record: bool = False):
+        from .engine import Memtable
+        self.engine, self.grid = engine, grid
+        self._Memtable = Memtable
+        self.mutable, self.immutable = {}, {}
+        # record=True keeps every GPU work item and a device copy of each
+        # memtable as it was before its sort, so that the whole replay can be
+        # re-executed with its inputs resident in HBM (bench.py --config 1).
+        self.recording = record
+        self.record: list = []
+        self.archive: list = []
+        self.puts_bytes = 0
+
+    def _mem(self, name: str):
+        if name not in self.mutable:
+            spec = trees.BY_NAME[name]
+            self.mutable[name] = self._Memtable(self.engine, spec)
+            self.immutable[name] = self._Memtable(self.engine, spec)
+        return self.mutable[name]
+
+    def put(self, name: str, values: np.ndarray) -> None:
+        self._mem(name).put(values)
+        self.puts_bytes += values.nbytes
+
+    def swap(self, names: list) -> None:
+        for name in list(self.mutable):
+            self.mutable[name], self.immutable[name] = self.immutable[name], self.mutable[name]
+            self.mutable[name].reset()
+        jobs = []
+        for name in names:
+            ptr, n = self.immutable[name].values()
+            jobs.append((trees.BY_NAME[name], ptr, n))
+        if jobs:
+            landings = []
+            if self.recording:
+                for s, p, n in jobs:
+                    copy = self.engine.alloc(max(1, n * s.value_size))
+                    self.engine.copy_device_async(copy.ptr, p, n * s.value_size)
+                    self.archive.append(copy)
+                    landings.append((p, copy.ptr, n * s.value_size))
+                self.record.append(("sort", jobs, landings))
+            self.engine.sort_values_batch(jobs)
+
+    def flushed(self, name: str) -> None:
+        pass  # the immutable memtable is reset when it becomes mutable again (swap)
+
+    def submit(self, jobs: list, cluster: int):
+        from . import abi
+        from .engine import Job
+        js = []
+        for name, c in jobs:
+            if c.table_a is None:
+                ptr, n = self.immutable[name].values()
+                segs_a, tables_a = [(ptr, n)], []
+            else:
+                segs_a, tables_a = [], [c.table_a.ref()]
+            js.append(Job(c.tree, segs_a, [], c.table_a is None, c.drop_tombstones, c.level_b, cluster,
+                          c.snapshot_min, c.addresses, None, flags=abi.COMPACTION_GRID, grid=self.grid,
+                          tables_a=tables_a, tables_b=[t.ref() for t in c.range_b[2]]))
+        if self.recording:
+            self.record.append(("batch", js))
+        return self.engine.submit(js)
+
+    def wait(self, handle, compactions: list) -> None:
+        handle.wait()
+        for i, c in enumerate(compactions):
+            r, infos = handle.result(i)
+            c.result = r
+            c.outputs = [TableInfo.decode(raw, c.tree.key_size) for raw in infos]
+        handle.release()
