@@ -24,7 +24,7 @@ def test_config1_first_bars_bit_exact(engine, oracle_lib):
         lock = LockstepExecutor(GridExecutor(engine, grid), OracleExecutor(oracle_lib))
         f = forest.Forest(lock, block_count=grid.block_count, cluster=0)
         load = benchmark_load.BenchmarkLoad(transfer_count=BARS * 32 * benchmark_load.BATCH)
-        f.run(load.ops())
+        f.run(load.ops(), progress=lambda op: op % 32 == 0 and print(f"bar {op // 32}: {lock.jobs_checked} jobs checked", flush=True))
         kinds = {(c.table_a is None, c.move, c.level_b) for _, cs in f.history for _, c in cs}
         assert (True, False, 0) in kinds              # immutable -> level 0
         assert (False, True, 1) in kinds              # level 0 -> level 1 moves

@@ -105,6 +105,10 @@ struct tbc_engine {
     // it only grows (after a stream drain), which a steady-state caller sees once.
     uint64_t *masks = nullptr;
     uint64_t mask_words = 0;
+    // Memtable sort scratch (keys, indices, histograms, look-back words, the
+    // tables' copies): grown on demand like the masks.
+    uint8_t *sort_scratch = nullptr;
+    uint64_t sort_scratch_size = 0;
 };
 
 struct tbc_grid {
@@ -299,6 +303,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     hipHostFree(e->host.base);
     hipFree(e->dev.base);
     if (e->masks) hipFree(e->masks);
+    if (e->sort_scratch) hipFree(e->sort_scratch);
     if (e->side) hipStreamDestroy(e->side);
     hipStreamDestroy(e->stream);
     delete e;
@@ -570,13 +575,30 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     }
     hipSetDevice(e->device);
     const uint64_t need = sort_scratch_bytes(items.data(), count);
-    const uint64_t dt = e->dev.top;
-    uint8_t *scratch = e->dev.alloc(need);
-    if (!scratch) return TBC_ERR_OUT_OF_MEMORY;
-    int rc = launch_sort_batch(items.data(), count, scratch, need, e->stream);
-    // Stream order protects the scratch: the next user of this arena range is
-    // enqueued on the same stream after the sort.
-    e->dev.top = dt;
+    const uint64_t host_need = sort_host_bytes(items.data(), count);
+    if (host_need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
+    if (need > e->sort_scratch_size) { // grows once per larger bar (a stream drain)
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (e->sort_scratch) hipFree(e->sort_scratch);
+        e->sort_scratch = nullptr;
+        e->sort_scratch_size = 0;
+        const uint64_t want = align_up(need + need / 8, 1ull << 24);
+        if (hipMalloc((void **)&e->sort_scratch, want) != hipSuccess) {
+            e->sort_scratch = nullptr;
+            return TBC_ERR_OUT_OF_MEMORY;
+        }
+        e->sort_scratch_size = want;
+    }
+    // The descriptors go through a pinned staging slot, reusable once the
+    // stream has passed this sort.
+    Staging &st = e->staging;
+    const int slot = st.next;
+    st.next = (st.next + 1) % Staging::kSlots;
+    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
+    uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, host, e->stream);
+    if (hipEventRecord(st.ev[slot], e->stream) != hipSuccess) rc = -1;
+    st.used[slot] = true;
     return rc == 0 ? TBC_OK : TBC_ERR_DEVICE;
 }
 

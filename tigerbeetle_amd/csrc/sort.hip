@@ -5,22 +5,32 @@
 // (table_memory.zig:83-87). Stability is load-bearing: fill_immutable_values
 // keeps the LAST of a run of equal keys (compaction.zig:519-522).
 //
-// A batch of memtables (every tree's at the bar end) is sorted by ONE
-// launch sequence (segmented: tiles never straddle memtables).
-// Here: a stable LSD radix sort of (key limbs, original index) items with
-// 4-bit digits, skipping every digit that is constant across the table (one
-// probe pass computes OR/AND of all keys and the sortedness flag), then one
-// gather of the Values by original index. Per pass:
-//   hist    — per-tile digit counts (16 bins x tiles, digit-major);
-//   scan    — exclusive scan of the [table][digit][tile] counts (chunk sums,
-//             their scan, chunk rescans: three short coalesced launches);
-//   scatter — each tile is staged through LDS so every thread owns 8
-//             consecutive items, per-thread digit counts are scanned across
-//             the tile in digit-major order, and items are written to
-//             (tile offset of digit) + (rank among earlier same-digit items):
-//             stable by construction.
+// A batch of memtables (every tree's at the bar end) is sorted by one
+// enqueued launch sequence that never waits on the host:
+//
+//   k_sort_extract  per tile of 2,048 items: key limbs (limb-major) and item
+//                   indices, a copy of the values (the gather's source),
+//                   OR/AND of the keys, per-table sortedness, and the 8-bit
+//                   digit histograms of every pass, per table;
+//   k_sort_plan     per table: which passes move anything (a digit that is
+//                   constant over the batch cannot reorder), each pass's
+//                   source buffer, and every digit's start in its table;
+//   k_sort_pass x P one launch per potential pass (P = 8 per key limb); an
+//                   inactive pass returns at once. Onesweep: each tile ranks
+//                   its items by digit (wave match ballots + per-wave counts:
+//                   stable), publishes its digit counts, looks back over the
+//                   tiles before it in its table for their prefix (decoupled
+//                   look-back, one 32-bit flag|count word per tile and digit),
+//                   and writes the tile out through LDS so each digit's run
+//                   is contiguous;
+//   k_sort_gather   values[i] = copy[idx[i]] for tables that were unsorted.
+//
+// Tiles never straddle tables, so a table's passes are independent of the
+// others' (a segmented sort with no table digit). Tables whose puts arrived
+// in order are left untouched (table_memory.zig:141).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <vector>
 
 #include "tbc_internal.h"
@@ -28,31 +38,32 @@
 namespace tbc {
 
 constexpr uint32_t kSortThreads = 256;
-constexpr uint32_t kSortPer = 8;
-constexpr uint32_t kSortTile = kSortThreads * kSortPer; // 2048 items per tile
-constexpr uint32_t kDigitBits = 4;
-constexpr uint32_t kBins = 1u << kDigitBits;
+constexpr uint32_t kSortWaves = kSortThreads / 64;
+constexpr uint32_t kSortRounds = 8;
+constexpr uint32_t kSortTile = kSortThreads * kSortRounds; // 2,048 items
+constexpr uint32_t kRadix = 256;
+constexpr uint32_t kMaxLimbs = 3;
+constexpr uint32_t kMaxPasses = 8 * kMaxLimbs;
 
-struct SortProbe {
-    uint64_t or_[4];
-    uint64_t and_[4];
-};
-// Workgroups fold their OR/AND into one of kProbeBuckets probes (one hot
-// address per limb serialised thousands of atomics in L2); the host folds
-// the buckets.
-constexpr uint32_t kProbeBuckets = 64;
+// Look-back words: flag in the top two bits, count below (counts < 2^30).
+constexpr uint32_t kFlagAggregate = 1u << 30;
+constexpr uint32_t kFlagPrefix = 2u << 30;
+constexpr uint32_t kCountMask = (1u << 30) - 1;
 
-// One memtable of the batch. Items of all segments live in one global item
-// space (segment s at [item_base, item_base + n)); tiles never straddle a
-// segment, so every tile knows its segment and the digit-major histograms of
-// a segment are contiguous: ONE exclusive scan over [segment][digit][tile]
-// yields global, segment-grouped destinations (a segmented stable sort with
-// no segment digit).
 struct SortSeg {
     uint8_t *values;
-    uint8_t *scratch; // n * vs bytes: the unsorted table, the gather's source
+    uint8_t *copy; // n * vs bytes: the table as put, the gather's source
     uint32_t n, vs, ts_off, kind;
     uint32_t item_base, tile_base, tiles, unsorted;
+};
+
+struct SortPlan {
+    uint64_t key_or[kMaxLimbs], key_and[kMaxLimbs];
+    uint32_t active[kMaxPasses]; // pass moves items
+    uint32_t src[kMaxPasses];    // ping-pong buffer the pass reads
+    uint32_t final_buf;          // buffer holding the sorted indices
+    uint32_t kl;                 // key limbs of the batch
+    uint32_t any_unsorted;
 };
 
 __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t ts_off, uint64_t k[3]) {
@@ -65,40 +76,45 @@ __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t
     }
 }
 
-// One workgroup per tile: extract keys (limb-major, global item positions)
-// and item indices; OR/AND of all keys; per-segment sortedness
-// (table_memory.zig:83-87 tracks it on put; here it is recomputed).
-__global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint32_t *tile_seg, uint32_t kl,
-                                                      uint32_t N, uint64_t *keys, uint32_t *idx, SortProbe *probe) {
-    __shared__ uint64_t s_or[3][4], s_and[3][4];
+// hist layout: [segment][pass][digit] u32.
+__device__ __forceinline__ uint32_t *seg_hist(uint32_t *hist, uint32_t s) { return hist + (size_t)s * kMaxPasses * kRadix; }
+
+// --------------------------------------------------------------------------
+// Extract: one workgroup per tile.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, const uint32_t *tile_seg, uint32_t kl,
+                                                               uint32_t N, uint64_t *keys, uint32_t *idx,
+                                                               SortPlan *plan, uint32_t *hist) {
+    __shared__ uint32_t s_hist[kMaxPasses * kRadix];
+    __shared__ uint64_t s_or[kMaxLimbs][kSortWaves], s_and[kMaxLimbs][kSortWaves];
     __shared__ uint32_t s_uns;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t sg = tile_seg[blockIdx.x];
     const SortSeg S = segs[sg];
     const uint32_t lt = blockIdx.x - S.tile_base;
+    for (uint32_t i = tid; i < 8 * kl * kRadix; i += kSortThreads) s_hist[i] = 0;
     if (tid == 0) s_uns = 0;
-    uint64_t o[3] = {0, 0, 0}, a[3] = {~0ull, ~0ull, ~0ull};
+    __syncthreads();
+    uint64_t o[kMaxLimbs] = {0, 0, 0}, a[kMaxLimbs] = {~0ull, ~0ull, ~0ull};
     uint32_t uns = 0;
-    for (uint32_t r = 0; r < kSortPer; r++) {
+    for (uint32_t r = 0; r < kSortRounds; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
         if (lt * kSortTile + r * kSortThreads >= S.n) break; // wave-uniform (whole row past the end)
         const bool in = li < S.n;
         const uint32_t i = S.item_base + li;
         uint64_t k[3] = {0, 0, 0}, kn[3];
         if (in) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
-        // The next item's key comes from the next lane (one value read per
-        // item); lane 63 reads its neighbour itself.
+        // The next item's key comes from the next lane; lane 63 reads its neighbour.
         for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
         if (lane == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
         if (!in) continue;
-        // Stage the value in the table's scratch (the gather reads from there
-        // and writes the table in place: no copy-back pass).
         for (uint32_t q = 0; q < S.vs; q += 16)
-            gst<u32x4>(S.scratch + (size_t)li * S.vs + q, gld<u32x4>(S.values + (size_t)li * S.vs + q));
+            gst<u32x4>(S.copy + (size_t)li * S.vs + q, gld<u32x4>(S.values + (size_t)li * S.vs + q));
         for (uint32_t l = 0; l < kl; l++) {
             keys[(size_t)l * N + i] = k[l];
             o[l] |= k[l];
             a[l] &= k[l];
+            for (uint32_t b = 0; b < 8; b++) atomicAdd(&s_hist[(8 * l + b) * kRadix + ((k[l] >> (8 * b)) & 255)], 1u);
         }
         idx[i] = i;
         if (li + 1 < S.n) {
@@ -112,7 +128,7 @@ __global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint3
             uns |= gt ? 1u : 0u;
         }
     }
-    for (uint32_t l = 0; l < 3; l++) {
+    for (uint32_t l = 0; l < kMaxLimbs; l++) {
         for (int off = 32; off > 0; off >>= 1) {
             o[l] |= __shfl_xor(o[l], off, 64);
             a[l] &= __shfl_xor(a[l], off, 64);
@@ -122,218 +138,223 @@ __global__ __launch_bounds__(256) void k_sort_extract(SortSeg *segs, const uint3
             s_and[l][wave] = a[l];
         }
     }
-    __syncthreads();
     if (uns) atomicOr(&s_uns, 1u);
     __syncthreads();
-    if (tid == 0) {
-        for (uint32_t l = 0; l < kl; l++) {
-            uint64_t oo = 0, aa = ~0ull;
-            for (int w = 0; w < 4; w++) {
-                oo |= s_or[l][w];
-                aa &= s_and[l][w];
-            }
-            SortProbe *pb = probe + (blockIdx.x % kProbeBuckets);
-            atomicOr((unsigned long long *)&pb->or_[l], (unsigned long long)oo);
-            atomicAnd((unsigned long long *)&pb->and_[l], (unsigned long long)aa);
+    uint32_t *h = seg_hist(hist, sg);
+    for (uint32_t i = tid; i < 8 * kl * kRadix; i += kSortThreads)
+        if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
+    if (tid < kl) {
+        uint64_t oo = 0, aa = ~0ull;
+        for (uint32_t w = 0; w < kSortWaves; w++) {
+            oo |= s_or[tid][w];
+            aa &= s_and[tid][w];
         }
-        if (s_uns) atomicOr(&segs[sg].unsorted, 1u);
+        atomicOr((unsigned long long *)&plan->key_or[tid], (unsigned long long)oo);
+        atomicAnd((unsigned long long *)&plan->key_and[tid], (unsigned long long)aa);
+    }
+    if (tid == 0 && s_uns) {
+        atomicOr(&segs[sg].unsorted, 1u);
+        atomicOr(&plan->any_unsorted, 1u);
     }
 }
 
-__device__ __forceinline__ uint32_t hist_slot(const SortSeg &S, uint32_t d, uint32_t lt) {
-    return S.tile_base * kBins + d * S.tiles + lt;
-}
-
-__global__ __launch_bounds__(kSortThreads) void k_sort_hist(const SortSeg *segs, const uint32_t *tile_seg,
-                                                            const uint64_t *keys, uint32_t N, uint32_t limb,
-                                                            uint32_t shift, uint32_t *hist) {
-    __shared__ uint32_t cnt[kBins];
-    const uint32_t tid = threadIdx.x;
-    const SortSeg S = segs[tile_seg[blockIdx.x]];
-    const uint32_t lt = blockIdx.x - S.tile_base;
-    if (tid < kBins) cnt[tid] = 0;
-    __syncthreads();
-    for (uint32_t r = 0; r < kSortPer; r++) {
-        const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-        if (li < S.n) {
-            const uint32_t i = S.item_base + li;
-            atomicAdd(&cnt[(uint32_t)(gld<uint64_t>(keys + (size_t)limb * N + i) >> shift) & (kBins - 1)], 1u);
+// --------------------------------------------------------------------------
+// Plan: one workgroup per table (block 0 also fills the batch-wide plan).
+// bins[segment][pass][digit] = the digit's first item in the global item
+// space (table base + exclusive prefix of the table's histogram).
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kRadix) void k_sort_plan(const SortSeg *segs, SortPlan *plan, const uint32_t *hist,
+                                                      uint32_t *bins) {
+    const uint32_t s = blockIdx.x, d = threadIdx.x, lane = d & 63, wave = d >> 6;
+    __shared__ uint32_t wsum[kRadix / 64];
+    const uint32_t kl = plan->kl;
+    if (s == 0 && d == 0) {
+        uint32_t buf = 0;
+        for (uint32_t p = 0; p < kMaxPasses; p++) {
+            const uint32_t l = p >> 3;
+            const bool act = l < kl && plan->any_unsorted &&
+                             (((plan->key_or[l] ^ plan->key_and[l]) >> (8 * (p & 7))) & 255) != 0;
+            plan->active[p] = act ? 1u : 0u;
+            plan->src[p] = buf;
+            if (act) buf ^= 1u;
         }
+        plan->final_buf = buf;
     }
-    __syncthreads();
-    if (tid < kBins) hist[hist_slot(S, tid, lt)] = cnt[tid];
-}
-
-// Exclusive scan of the m histogram entries in place, in three short
-// launches (all loads coalesced): per-chunk sums, a scan of the chunk sums,
-// then every chunk rescanned with its offset. kScanChunk entries per chunk.
-constexpr uint32_t kScanChunk = 2048;
-
-__device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t *wsum, uint32_t &total) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t off = 0;
-    total = 0;
-    for (uint32_t w = 0; w < 4; w++) {
-        off += w < wave ? wsum[w] : 0u;
-        total += wsum[w];
-    }
-    __syncthreads();
-    return off + incl - v;
-}
-
-__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *hist, uint32_t m, uint32_t *chunk_sums) {
-    __shared__ uint32_t wsum[4];
-    const uint32_t base = blockIdx.x * kScanChunk;
-    uint32_t sum = 0;
-    for (uint32_t k = threadIdx.x; k < kScanChunk; k += 256)
-        sum += base + k < m ? hist[base + k] : 0u;
-    uint32_t total;
-    block_excl_scan_256(sum, wsum, total);
-    if (threadIdx.x == 0) chunk_sums[blockIdx.x] = total;
-}
-
-// One workgroup: exclusive scan of the chunk sums in place.
-__global__ __launch_bounds__(256) void k_scan_top(uint32_t *chunk_sums, uint32_t chunks) {
-    __shared__ uint32_t wsum[4];
-    uint32_t carry = 0;
-    for (uint32_t b = 0; b < chunks; b += 256) {
-        const uint32_t i = b + threadIdx.x;
-        const uint32_t v = i < chunks ? chunk_sums[i] : 0u;
-        uint32_t total;
-        const uint32_t ex = block_excl_scan_256(v, wsum, total);
-        if (i < chunks) chunk_sums[i] = carry + ex;
-        carry += total;
+    const uint32_t *h = hist + (size_t)s * kMaxPasses * kRadix;
+    uint32_t *out = bins + (size_t)s * kMaxPasses * kRadix;
+    for (uint32_t p = 0; p < 8 * kl; p++) {
+        const uint32_t c = h[p * kRadix + d];
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t off = 0;
+        for (uint32_t w = 0; w < wave; w++) off += wsum[w];
+        out[p * kRadix + d] = segs[s].item_base + off + incl - c;
+        __syncthreads();
     }
 }
 
-// Each thread owns 8 consecutive entries of the chunk (loaded as 2 x 16 B).
-__global__ __launch_bounds__(256) void k_scan_apply(uint32_t *hist, uint32_t m, const uint32_t *chunk_sums) {
-    __shared__ uint32_t wsum[4];
-    const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * 8;
-    uint32_t v[8], sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-        v[k] = base + k < m ? hist[base + k] : 0u;
-        sum += v[k];
-    }
-    uint32_t total;
-    uint32_t run = chunk_sums[blockIdx.x] + block_excl_scan_256(sum, wsum, total);
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-        if (base + k < m) hist[base + k] = run;
-        run += v[k];
-    }
+// --------------------------------------------------------------------------
+// One onesweep pass (digit = byte `p & 7` of limb `p >> 3`).
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lb_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int KL>
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(const SortSeg *segs, const uint32_t *tile_seg,
-                                                               const uint64_t *keys_in, const uint32_t *idx_in,
-                                                               uint64_t *keys_out, uint32_t *idx_out, uint32_t N,
-                                                               uint32_t limb, uint32_t shift, const uint32_t *hist) {
+template <uint32_t KL>
+__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const uint32_t *tile_seg,
+                                                            const SortPlan *plan, uint32_t p, uint32_t ntiles,
+                                                            uint32_t N, uint64_t *keys0, uint64_t *keys1,
+                                                            uint32_t *idx0, uint32_t *idx1, const uint32_t *bins,
+                                                            uint32_t *status, uint32_t *tile_counter) {
+    if (!plan->active[p]) return; // uniform: a constant digit cannot reorder anything
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_wcnt[kSortWaves][kRadix]; // per wave: running, then total counts
+    __shared__ uint32_t s_start[kRadix];            // local start of each digit in the tile
+    __shared__ uint32_t s_excl[kRadix];             // items of the digit in the table's earlier tiles
     __shared__ uint64_t s_key[KL][kSortTile];
     __shared__ uint32_t s_idx[kSortTile];
-    __shared__ uint32_t s_cnt[kBins][kSortThreads + 1]; // digit-major per-thread counts
-    __shared__ uint32_t s_tot[kBins], s_dstart[kBins], s_gbase[kBins];
-    __shared__ uint16_t s_perm[kSortTile]; // tile position in digit order -> item
-    const uint32_t tid = threadIdx.x;
-    const SortSeg S = segs[tile_seg[blockIdx.x]];
-    const uint32_t lt = blockIdx.x - S.tile_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // Dynamic tile ids in arrival order: every tile a workgroup looks back on
+    // was taken by a workgroup that is running or done (forward progress).
+    if (tid == 0) s_tile = atomicAdd(&tile_counter[p], 1u);
+    for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    if (t >= ntiles) return;
+    const uint32_t sg = tile_seg[t];
+    const SortSeg S = segs[sg];
+    if (!S.unsorted) return; // tables put in order are left as they are
+    const uint32_t lt = t - S.tile_base;
     const uint32_t base = S.item_base + lt * kSortTile;
     const uint32_t m = (S.n - lt * kSortTile) < kSortTile ? (S.n - lt * kSortTile) : kSortTile;
-    // Coalesced load into LDS.
-    for (uint32_t r = 0; r < kSortPer; r++) {
-        const uint32_t e = r * kSortThreads + tid;
-        if (e < m) {
+    const uint32_t limb = p >> 3, shift = 8 * (p & 7);
+    const uint32_t live = plan->kl - limb; // limbs [limb, kl) still move with the items
+    const uint64_t *ksrc = plan->src[p] ? keys1 : keys0;
+    uint64_t *kdst = plan->src[p] ? keys0 : keys1;
+    const uint32_t *isrc = plan->src[p] ? idx1 : idx0;
+    uint32_t *idst = plan->src[p] ? idx0 : idx1;
+
+    // Wave w owns items [512 w, 512 w + 512) of the tile, 64 per round in
+    // lane order: stable rank = (earlier waves) + (earlier rounds of this
+    // wave, counted in s_wcnt) + (earlier lanes with the same digit).
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    uint32_t rank[kSortRounds], dig[kSortRounds];
+    uint64_t k[kSortRounds][KL];
+    uint32_t ix[kSortRounds];
 #pragma unroll
-            for (int l = 0; l < KL; l++) s_key[l][e] = gld<uint64_t>(keys_in + (size_t)(limb + l) * N + base + e);
-            s_idx[e] = gld<uint32_t>(idx_in + base + e);
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const uint32_t e = wave * (64 * kSortRounds) + r * 64 + lane;
+        const bool in = e < m;
+#pragma unroll
+        for (uint32_t l = 0; l < KL; l++)
+            k[r][l] = in && l < live ? gld<uint64_t>(ksrc + (size_t)(limb + l) * N + base + e) : 0ull;
+        ix[r] = in ? gld<uint32_t>(isrc + base + e) : 0u;
+        const uint32_t d = in ? (uint32_t)(k[r][0] >> shift) & 255u : 0u;
+        dig[r] = d;
+        uint64_t peers = __ballot(in);
+#pragma unroll
+        for (uint32_t b = 0; b < 8; b++) {
+            const uint64_t bal = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bal : ~bal;
         }
+        const uint32_t before = __builtin_popcountll(peers & lt_mask);
+        const uint32_t prior = in ? s_wcnt[wave][d] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (in && before == 0) s_wcnt[wave][d] = prior + (uint32_t)__builtin_popcountll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        rank[r] = prior + before;
     }
     __syncthreads();
-    // Thread tid owns items [tid*8, tid*8+8) in order.
-    uint32_t dig[kSortPer];
-    uint32_t c[kBins];
+    // Per digit (thread d): counts of the tile, exclusive prefix over waves,
+    // and the tile-local start (exclusive scan over digits).
+    const uint32_t d = tid;
+    uint32_t cnt = 0, wpre[kSortWaves];
 #pragma unroll
-    for (uint32_t d = 0; d < kBins; d++) c[d] = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kSortPer; k++) {
-        const uint32_t e = tid * kSortPer + k;
-        dig[k] = e < m ? (uint32_t)(s_key[0][e] >> shift) & (kBins - 1) : kBins; // kBins = none
-#pragma unroll
-        for (uint32_t d = 0; d < kBins; d++) c[d] += dig[k] == d ? 1u : 0u;
+    for (uint32_t w = 0; w < kSortWaves; w++) {
+        wpre[w] = cnt;
+        cnt += s_wcnt[w][d];
     }
-#pragma unroll
-    for (uint32_t d = 0; d < kBins; d++) s_cnt[d][tid] = c[d];
-    __syncthreads();
-    // Per digit, exclusive scan across threads (one wave per digit group).
     {
-        const uint32_t wave = tid >> 6, lane = tid & 63;
-        for (uint32_t d = wave; d < kBins; d += kSortThreads / 64) {
-            uint32_t carry = 0;
-            for (uint32_t b0 = 0; b0 < kSortThreads; b0 += 64) {
-                const uint32_t v = s_cnt[d][b0 + lane];
-                uint32_t incl = v;
-                for (int o = 1; o < 64; o <<= 1) {
-                    uint32_t y = __shfl_up(incl, o, 64);
-                    if (lane >= (uint32_t)o) incl += y;
-                }
-                s_cnt[d][b0 + lane] = carry + incl - v;
-                carry += __shfl(incl, 63, 64);
+        uint32_t incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        __shared__ uint32_t s_wsum[kSortWaves];
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        uint32_t off = 0;
+        for (uint32_t w = 0; w < wave; w++) off += s_wsum[w];
+        s_start[d] = off + incl - cnt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t w = 0; w < kSortWaves; w++) s_wcnt[w][d] = wpre[w]; // becomes the wave's offset
+    // Decoupled look-back over the table's earlier tiles, one digit per thread.
+    uint32_t *st = status + (size_t)p * ntiles * kRadix;
+    uint32_t excl = 0;
+    if (lt == 0) {
+        lb_store(&st[(size_t)t * kRadix + d], kFlagPrefix | cnt);
+    } else {
+        lb_store(&st[(size_t)t * kRadix + d], kFlagAggregate | cnt);
+        uint32_t pred = t - 1;
+        for (uint32_t spins = 0;;) {
+            const uint32_t v = lb_load(&st[(size_t)pred * kRadix + d]);
+            if ((v & ~kCountMask) == 0) { // not published yet
+                if (++spins > (1u << 26)) break; // bounded (a broken invariant, not a hang)
+                __builtin_amdgcn_s_sleep(1);
+                continue;
             }
-            if (lane == 0) s_tot[d] = carry;
+            excl += v & kCountMask;
+            if ((v & ~kCountMask) == kFlagPrefix || pred == S.tile_base) break;
+            pred--;
+        }
+        lb_store(&st[(size_t)t * kRadix + d], kFlagPrefix | (excl + cnt));
+    }
+    s_excl[d] = excl;
+    __syncthreads();
+    // Items into LDS at their tile-local sorted position.
+#pragma unroll
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const uint32_t e = wave * (64 * kSortRounds) + r * 64 + lane;
+        if (e < m) {
+            const uint32_t pos = s_start[dig[r]] + s_wcnt[wave][dig[r]] + rank[r];
+#pragma unroll
+            for (uint32_t l = 0; l < KL; l++) s_key[l][pos] = k[r][l];
+            s_idx[pos] = ix[r];
         }
     }
     __syncthreads();
-    if (tid < kBins) s_gbase[tid] = hist[hist_slot(S, tid, lt)];
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (uint32_t d = 0; d < kBins; d++) {
-            s_dstart[d] = acc;
-            acc += s_tot[d];
-        }
-    }
-    __syncthreads();
-    // Rank every item inside the tile in digit order (stable: thread order,
-    // then item order within the thread) ...
-    uint32_t run[kBins];
+    // Out in that order: each digit's run lands contiguously.
+    const uint32_t *bin = bins + ((size_t)sg * kMaxPasses + p) * kRadix;
+    for (uint32_t j = tid; j < m; j += kSortThreads) {
+        const uint32_t dj = (uint32_t)(s_key[0][j] >> shift) & 255u;
+        const uint32_t dst = bin[dj] + s_excl[dj] + (j - s_start[dj]);
 #pragma unroll
-    for (uint32_t d = 0; d < kBins; d++) run[d] = s_dstart[d] + s_cnt[d][tid];
-#pragma unroll
-    for (uint32_t k = 0; k < kSortPer; k++) {
-        if (dig[k] < kBins) {
-            uint32_t loc = 0;
-#pragma unroll
-            for (uint32_t d = 0; d < kBins; d++)
-                if (dig[k] == d) loc = run[d]++;
-            s_perm[loc] = (uint16_t)(tid * kSortPer + k);
-        }
-    }
-    __syncthreads();
-    // ... then write the tile out in that order: consecutive threads write
-    // consecutive destinations inside each digit's run (coalesced).
-    for (uint32_t i = tid; i < m; i += kSortThreads) {
-        const uint32_t e = s_perm[i];
-        const uint32_t d = (uint32_t)(s_key[0][e] >> shift) & (kBins - 1);
-        const uint32_t dst = s_gbase[d] + (i - s_dstart[d]);
-#pragma unroll
-        for (int l = 0; l < KL; l++) gst<uint64_t>(keys_out + (size_t)(limb + l) * N + dst, s_key[l][e]);
-        gst<uint32_t>(idx_out + dst, s_idx[e]);
+        for (uint32_t l = 0; l < KL; l++)
+            if (l < live) gst<uint64_t>(kdst + (size_t)(limb + l) * N + dst, s_key[l][j]);
+        gst<uint32_t>(idst + dst, s_idx[j]);
     }
 }
 
-// values[i] = scratch[idx[i]] (segment-local; scratch holds the unsorted
-// table), 16 bytes per lane; sorted tables are left alone.
+// values[i] = copy[idx[i]] (table-local), 16 bytes per lane; sorted tables
+// are left alone.
 __global__ __launch_bounds__(256) void k_sort_gather(const SortSeg *segs, const uint32_t *tile_seg,
-                                                     const uint32_t *idx) {
+                                                     const SortPlan *plan, const uint32_t *idx0,
+                                                     const uint32_t *idx1) {
     const SortSeg S = segs[tile_seg[blockIdx.x]];
     if (!S.unsorted) return;
+    const uint32_t *idx = plan->final_buf ? idx1 : idx0;
     const uint32_t lt = blockIdx.x - S.tile_base;
     const uint32_t first = lt * kSortTile;
     const uint32_t m = (S.n - first) < kSortTile ? (S.n - first) : kSortTile;
@@ -342,145 +363,133 @@ __global__ __launch_bounds__(256) void k_sort_gather(const SortSeg *segs, const 
         const uint32_t e = c / cpv, part = c % cpv;
         const uint32_t src = gld<uint32_t>(idx + S.item_base + first + e) - S.item_base;
         gst<u32x4>(S.values + (size_t)(first + e) * S.vs + 16 * part,
-                   gld<u32x4>(S.scratch + (size_t)src * S.vs + 16 * part));
+                   gld<u32x4>(S.copy + (size_t)src * S.vs + 16 * part));
     }
 }
 
-static uint32_t key_limbs(uint32_t kind) {
-    return kind == kKeyTimestamp ? 1 : kind == kKeyCompositeU128 ? 3 : 2;
-}
+static uint32_t key_limbs(uint32_t kind) { return kind == kKeyTimestamp ? 1 : kind == kKeyCompositeU128 ? 3 : 2; }
 
 static uint64_t tiles_of(uint32_t n) { return (n + kSortTile - 1) / kSortTile; }
+static uint64_t align256(uint64_t x) { return (x + 255) / 256 * 256; }
 
-uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count) {
-    uint64_t N = 0, tiles = 0, vals = 0;
+// Scratch layout (sort_scratch_bytes must match launch_sort_batch).
+struct SortScratch {
+    uint64_t plan, segs, tile_seg, keys, idx, hist, bins, status, counters, copies, total;
+};
+
+static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
+    uint64_t N = 0, tiles = 0, vals = 0, nseg = 0, kl = 1;
     for (uint32_t j = 0; j < count; j++) {
         if (items[j].n < 2) continue;
         N += items[j].n;
         tiles += tiles_of(items[j].n);
-        vals += ((uint64_t)items[j].n * items[j].value_size + 255) / 256 * 256;
+        vals += align256((uint64_t)items[j].n * items[j].value_size);
+        nseg++;
+        kl = kl > key_limbs(items[j].key_kind) ? kl : key_limbs(items[j].key_kind);
     }
-    return sizeof(SortProbe) * kProbeBuckets           // probes
-           + ((uint64_t)sizeof(SortSeg) * count + 255) / 256 * 256
-           + (4 * tiles + 255) / 256 * 256              // tile -> segment
-           + 2 * ((N * 3 * 8) + (N * 4 + 255) / 256 * 256) // two item buffers
-           + (4 * kBins * tiles + 255) / 256 * 256      // histogram
-           + (4 * (kBins * tiles / kScanChunk + 1) + 255) / 256 * 256 // scan chunk sums
-           + vals;                                      // gathered values
+    SortScratch s;
+    uint64_t o = 0;
+    s.plan = o;
+    o += align256(sizeof(SortPlan));
+    s.segs = o;
+    o += align256(sizeof(SortSeg) * count);
+    s.tile_seg = o;
+    o += align256(4 * tiles);
+    s.keys = o;
+    o += 2 * align256(8 * N * kl);
+    s.idx = o;
+    o += 2 * align256(4 * N);
+    s.hist = o;
+    o += align256(4ull * nseg * kMaxPasses * kRadix);
+    s.bins = o;
+    o += align256(4ull * nseg * kMaxPasses * kRadix);
+    s.status = o;
+    o += align256(4ull * 8 * kl * tiles * kRadix);
+    s.counters = o;
+    o += align256(4ull * kMaxPasses);
+    s.copies = o;
+    o += vals;
+    s.total = o;
+    return s;
 }
 
-int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *stream) {
-    if (scratch_bytes < sort_scratch_bytes(items, count)) return -1;
+uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count) { return scratch_layout(items, count).total; }
+
+// Everything is enqueued on `stream`; the host never waits. The plan, table
+// descriptors and tile map go through the caller's pinned staging (`host`,
+// at least sort_host_bytes) which must stay untouched until the stream has
+// passed this batch.
+uint64_t sort_host_bytes(const SortItem *items, uint32_t count) {
+    const SortScratch s = scratch_layout(items, count);
+    return s.keys; // plan + segs + tile map
+}
+
+int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *host,
+                      void *stream) {
+    const SortScratch L = scratch_layout(items, count);
+    if (scratch_bytes < L.total) return -1;
     hipStream_t s = (hipStream_t)stream;
-    // Host plan: segments (n >= 2), tile bases, widest key.
-    std::vector<SortSeg> segs;
-    std::vector<uint32_t> tile_seg;
-    uint32_t N = 0, kl = 1;
+    uint8_t *base = (uint8_t *)scratch, *hbase = (uint8_t *)host;
+    SortPlan *hplan = (SortPlan *)(hbase + L.plan);
+    SortSeg *hsegs = (SortSeg *)(hbase + L.segs);
+    uint32_t *htile = (uint32_t *)(hbase + L.tile_seg);
+    uint32_t N = 0, kl = 1, nseg = 0, ntiles = 0;
+    uint64_t copy_off = L.copies;
     for (uint32_t j = 0; j < count; j++) {
         const SortItem &it = items[j];
         if (it.n < 2) continue;
         SortSeg g{};
         g.values = (uint8_t *)it.values;
+        g.copy = base + copy_off;
+        copy_off += align256((uint64_t)it.n * it.value_size);
         g.n = it.n;
         g.vs = it.value_size;
         g.ts_off = it.timestamp_offset;
         g.kind = it.key_kind;
         g.item_base = N;
-        g.tile_base = (uint32_t)tile_seg.size();
+        g.tile_base = ntiles;
         g.tiles = (uint32_t)tiles_of(it.n);
-        for (uint32_t t = 0; t < g.tiles; t++) tile_seg.push_back((uint32_t)segs.size());
+        for (uint32_t t = 0; t < g.tiles; t++) htile[ntiles + t] = nseg;
+        ntiles += g.tiles;
         N += it.n;
         kl = kl > key_limbs(it.key_kind) ? kl : key_limbs(it.key_kind);
-        segs.push_back(g);
+        hsegs[nseg++] = g;
     }
-    if (segs.empty()) return 0;
-    const uint32_t nseg = (uint32_t)segs.size(), ntiles = (uint32_t)tile_seg.size();
-    uint8_t *p = (uint8_t *)scratch;
-    SortProbe *probe = (SortProbe *)p;
-    p += sizeof(SortProbe) * kProbeBuckets;
-    SortSeg *d_segs = (SortSeg *)p;
-    p += ((uint64_t)sizeof(SortSeg) * count + 255) / 256 * 256;
-    uint32_t *d_tile_seg = (uint32_t *)p;
-    p += (4ull * ntiles + 255) / 256 * 256;
-    uint64_t *keys[2];
-    uint32_t *idx[2];
-    for (int b = 0; b < 2; b++) {
-        keys[b] = (uint64_t *)p;
-        p += (uint64_t)N * 3 * 8;
-        idx[b] = (uint32_t *)p;
-        p += ((uint64_t)N * 4 + 255) / 256 * 256;
-    }
-    uint32_t *hist = (uint32_t *)p;
-    p += ((uint64_t)4 * kBins * ntiles + 255) / 256 * 256;
-    uint32_t *chunk_sums = (uint32_t *)p;
-    p += ((uint64_t)4 * (kBins * ntiles / kScanChunk + 1) + 255) / 256 * 256;
-    for (SortSeg &g : segs) {
-        g.scratch = p;
-        p += ((uint64_t)g.n * g.vs + 255) / 256 * 256;
-    }
-
-    // The plan is staged through static host memory owned by the caller's
-    // stream order: copy it synchronously with the probe read below.
-    std::vector<SortProbe> init(kProbeBuckets);
-    for (SortProbe &pr : init)
-        for (int l = 0; l < 4; l++) pr.or_[l] = 0, pr.and_[l] = ~0ull;
-    if (hipMemcpyAsync(probe, init.data(), sizeof(SortProbe) * kProbeBuckets, hipMemcpyHostToDevice, s) !=
-            hipSuccess ||
-        hipMemcpyAsync(d_segs, segs.data(), sizeof(SortSeg) * nseg, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(d_tile_seg, tile_seg.data(), 4ull * ntiles, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (!nseg) return 0;
+    memset(hplan, 0, sizeof(SortPlan));
+    for (uint32_t l = 0; l < kMaxLimbs; l++) hplan->key_and[l] = ~0ull;
+    hplan->kl = kl;
+    SortPlan *plan = (SortPlan *)(base + L.plan);
+    SortSeg *d_segs = (SortSeg *)(base + L.segs);
+    uint32_t *d_tile = (uint32_t *)(base + L.tile_seg);
+    uint64_t *keys0 = (uint64_t *)(base + L.keys), *keys1 = (uint64_t *)(base + L.keys + align256(8ull * N * kl));
+    uint32_t *idx0 = (uint32_t *)(base + L.idx), *idx1 = (uint32_t *)(base + L.idx + align256(4ull * N));
+    uint32_t *hist = (uint32_t *)(base + L.hist), *bins = (uint32_t *)(base + L.bins);
+    uint32_t *status = (uint32_t *)(base + L.status), *counters = (uint32_t *)(base + L.counters);
+    // Histograms, look-back words and tile counters start at zero.
+    if (hipMemcpyAsync(base, hbase, L.keys, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(hist, 0, L.copies - L.hist, s) != hipSuccess)
         return -1;
-    hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg, kl, N, keys[0], idx[0],
-                       probe);
-    // The digit plan needs the probe on the host (one small synchronous read
-    // per batch, not per memtable).
-    std::vector<SortProbe> buckets(kProbeBuckets);
-    std::vector<SortSeg> hsegs(nseg);
-    if (hipMemcpyAsync(buckets.data(), probe, sizeof(SortProbe) * kProbeBuckets, hipMemcpyDeviceToHost, s) !=
-            hipSuccess ||
-        hipMemcpyAsync(hsegs.data(), d_segs, sizeof(SortSeg) * nseg, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return -1;
-    SortProbe host = buckets[0];
-    for (const SortProbe &pr : buckets)
-        for (int l = 0; l < 4; l++) host.or_[l] |= pr.or_[l], host.and_[l] &= pr.and_[l];
-    bool any = false;
-    for (const SortSeg &g : hsegs) any |= g.unsorted != 0;
-    if (!any) return 0; // table_memory.zig:141: already sorted, no-op
-    int cur = 0;
-    // LSD passes carry only the limbs still to be sorted on: limbs below the
-    // current one are final, limbs above the highest varying one are constant.
-    uint32_t hi = 0;
-    for (uint32_t limb = 0; limb < kl; limb++)
-        if (host.or_[limb] ^ host.and_[limb]) hi = limb + 1;
-    for (uint32_t limb = 0; limb < hi; limb++) {
-        const uint64_t varies = host.or_[limb] ^ host.and_[limb];
-        const uint32_t live = hi - limb; // limbs [limb, hi) move with the items
-        for (uint32_t shift = 0; shift < 64; shift += kDigitBits) {
-            if (((varies >> shift) & (kBins - 1)) == 0) continue; // constant digit: order unchanged
-            hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg, keys[cur],
-                               N, limb, shift, hist);
-            const uint32_t m = kBins * ntiles, chunks = (m + kScanChunk - 1) / kScanChunk;
-            hipLaunchKernelGGL(k_scan_reduce, dim3(chunks), dim3(256), 0, s, hist, m, chunk_sums);
-            hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, chunk_sums, chunks);
-            hipLaunchKernelGGL(k_scan_apply, dim3(chunks), dim3(256), 0, s, hist, m, chunk_sums);
-            switch (live) {
-            case 1:
-                hipLaunchKernelGGL(k_sort_scatter<1>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
-                                   keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
-                break;
-            case 2:
-                hipLaunchKernelGGL(k_sort_scatter<2>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
-                                   keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
-                break;
-            default:
-                hipLaunchKernelGGL(k_sort_scatter<3>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile_seg,
-                                   keys[cur], idx[cur], keys[cur ^ 1], idx[cur ^ 1], N, limb, shift, hist);
-                break;
-            }
-            cur ^= 1;
+    hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, kl, N, keys0, idx0,
+                       plan, hist);
+    hipLaunchKernelGGL(k_sort_plan, dim3(nseg), dim3(kRadix), 0, s, d_segs, plan, hist, bins);
+    for (uint32_t p = 0; p < 8 * kl; p++) {
+        switch (kl - (p >> 3)) { // limbs still moving in this pass
+        case 1:
+            hipLaunchKernelGGL(k_sort_pass<1>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, plan, p, ntiles,
+                               N, keys0, keys1, idx0, idx1, bins, status, counters);
+            break;
+        case 2:
+            hipLaunchKernelGGL(k_sort_pass<2>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, plan, p, ntiles,
+                               N, keys0, keys1, idx0, idx1, bins, status, counters);
+            break;
+        default:
+            hipLaunchKernelGGL(k_sort_pass<3>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, plan, p, ntiles,
+                               N, keys0, keys1, idx0, idx1, bins, status, counters);
+            break;
         }
     }
-    hipLaunchKernelGGL(k_sort_gather, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile_seg, idx[cur]);
+    hipLaunchKernelGGL(k_sort_gather, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile, plan, idx0, idx1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -215,8 +215,12 @@ struct SortItem {
     void *values;
     uint32_t n, value_size, timestamp_offset, key_kind;
 };
-int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *stream);
+// Enqueues the whole sort of a batch of memtables (no host wait); `host` is
+// pinned staging of sort_host_bytes() that must outlive the enqueued copy.
+int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *host,
+                      void *stream);
 uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count);
+uint64_t sort_host_bytes(const SortItem *items, uint32_t count);
 size_t kway_scan_tmp_bytes(uint32_t n);
 int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
                 uint32_t tiles, uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan,
