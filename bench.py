@@ -31,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from tigerbeetle_amd import Engine, Job, configs  # noqa: E402
+from tigerbeetle_amd import Engine, Grid, Job, benchmark_load, configs, forest  # noqa: E402
 from tigerbeetle_amd.shard import plan_shards, reduce_step  # noqa: E402
 
 METRIC = "compacted input MB/s per GPU and per node (1/2/4/8) + % HBM roofline"
@@ -122,6 +122,102 @@ class Workload:
         return b
 
 
+class ReplayWorkload:
+    """BASELINE config 1 (`tigerbeetle benchmark` default: 10k accounts, 10M
+    transfers in batches of 8,190; tigerbeetle_amd/benchmark_load.py).
+
+    Setup (untimed, but timed and reported as the PCIe-inclusive replay):
+    every op is generated on the host, its puts stream into device memtables
+    (tbc_memtable_put: pinned staging + H2D), and the Forest schedule
+    (forest.py: Tree.compact / Manifest / FreeSet restated) runs every bar-end
+    sort and half-bar compaction batch on the GPU grid, recording them with
+    a device copy of each memtable before its sort. A step re-executes that
+    whole record with its inputs resident in HBM: per bar the memtables are
+    re-landed (D2D), sorted (tbc_sort_values_batch), and the two half-bars'
+    batches run (tbc_compaction_submit); all enqueued without host waits,
+    completed batches are then released."""
+
+    def __init__(self, eng: Engine, transfer_count: int, bs: int):
+        self.bs = bs
+        self.grid = Grid(eng, 24_000)
+        self.executor = forest.GridExecutor(eng, self.grid, record=True)
+        self.forest = forest.Forest(self.executor, self.grid.block_count, cluster=0)
+        load = benchmark_load.BenchmarkLoad(transfer_count=transfer_count)
+        t0 = time.perf_counter()
+        self.forest.run(load.ops(), progress=lambda op: op % 256 == 0 and print(
+            f"config 1 record: op {op}", file=sys.stderr, flush=True))
+        eng.synchronize()
+        self.record_s = time.perf_counter() - t0
+        self.puts_bytes = self.executor.puts_bytes
+        self.jobs = [js for kind, *rest in self.executor.record if kind == "batch" for js in rest[0]]
+        R = 0
+        for j in self.jobs:
+            vs = j.tree.value_size
+            R += sum(n for _, n in j.segments_a) * vs if j.a_immutable else sum(t[2] for t in j.tables_a) * vs
+            R += sum(t[2] for t in j.tables_b) * vs
+        self.input_bytes = R
+        W = 0
+        for _, cs in self.forest.history:
+            for _, c in cs:
+                if not c.move:
+                    r = c.result
+                    W += r.value_count * c.tree.value_size + 256 * r.data_block_count + \
+                        r.table_count * c.tree.layout(bs)["index_size"]
+        self.output_bytes = W
+        self.sort_bytes = sum(2 * n * forest.trees.BY_NAME[name].value_size
+                              for bar in self.forest.swaps for name, n, srt in bar if not srt)
+        self.batches = sum(1 for kind, *_ in self.executor.record if kind == "batch")
+        self.sorts = sum(1 for kind, *_ in self.executor.record if kind == "sort")
+        self.moves = sum(1 for _, cs in self.forest.history for _, c in cs if c.move)
+
+    def step(self, eng: Engine, ktimes: dict | None = None):
+        live = []
+        for kind, *rest in self.executor.record:
+            if kind == "sort":
+                jobs, landings = rest
+                for dst, src, n in landings:
+                    eng.copy_device_async(dst, src, n)
+                eng.sort_values_batch(jobs)
+            else:
+                live.append(eng.submit(rest[0]))
+        for b in live:
+            b.wait()
+            if ktimes is not None:
+                for k, v in b.kernel_times().items():
+                    ktimes[k] = ktimes.get(k, 0.0) + v
+            b.release()
+
+
+def cpu_baseline_config1(bars: int = 11, bs: int = 1 << 20) -> dict:
+    """The oracle on the identical per-tree inputs of config 1's first bars:
+    the same Forest schedule with the oracle as executor (bar-end sorts and
+    every compaction), timed inside the oracle calls only."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle
+    from oracle_executor import OracleExecutor
+    oracle.build()
+    ex = OracleExecutor(oracle, bs)
+    f = forest.Forest(ex, 24_000, cluster=0)
+    f.run(benchmark_load.BenchmarkLoad(transfer_count=bars * 32 * benchmark_load.BATCH).ops())
+    return {"value": round(ex.input_bytes / ex.busy / 1e6, 1), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"config 1's first {bars} bars ({bars * 32 * benchmark_load.BATCH} transfers: "
+                      f"{len(f.history)} half-bars, {ex.input_bytes / 1e6:.0f} MB of compaction input, "
+                      f"{ex.busy:.1f} s in the oracle's sorts and compactions) through oracle/tbc_oracle.c "
+                      f"(single thread) on {cpu_model()}"}
+
+
+def cpu_model() -> str:
+    import platform
+    cpu = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return cpu
+
+
 def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 << 20) -> dict:
     """The oracle (single-threaded C restatement, AES-NI AEGIS) on a bounded
     sample of the same workload: whole jobs (memtable sort included for
@@ -188,16 +284,83 @@ def pmc_traffic(kernel: str):
     return None, None
 
 
+# LDS T-table AES: one AES round of one 16-byte block = 16 ds_read_b32
+# lookups (4 per column) = 64 LDS bytes; ds_read_b32 moves 128 B/clk/CU
+# (MI355X_MICROARCH.md §LDS) -> 2 rounds/clk/CU x 256 CUs x 2.4 GHz.
+AES_ROUNDS_PEAK = 2 * 256 * 2.4e9
+
+
+def aes_roofline(body_bytes: int, data_blocks: int, kernel_us: float, kernel: str) -> dict:
+    """AEGIS-128L of the data blocks as AES rounds/s against the LDS
+    T-table bound: per block body/32 absorbs + 7 finalisation updates, plus
+    the 240-byte header (8 + 7 updates); 8 AES rounds per update."""
+    updates = body_bytes / 32 + data_blocks * (7 + 15)
+    rounds = 8 * updates
+    achieved = rounds / (kernel_us * 1e-6)
+    out = {"bound": "lds", "kernel": kernel, "achieved": round(achieved / 1e9, 2), "peak": round(AES_ROUNDS_PEAK / 1e9, 1),
+           "unit": "G AES rounds/s", "frac": round(achieved / AES_ROUNDS_PEAK, 4), "aes_rounds": int(rounds)}
+    sq = pmc_sq(kernel)
+    if sq:
+        out["pmc"] = sq
+    return out
+
+
+def pmc_sq(kernel: str):
+    """VALU / LDS instruction counts of `kernel` from the SQ PMC pass of a
+    profile taken with this very libtbc.so (profiles/*/traffic.json)."""
+    import glob
+    import hashlib
+    from tigerbeetle_amd import abi
+    try:
+        md5 = hashlib.md5(open(abi.LIB_PATH, "rb").read()).hexdigest()
+    except OSError:
+        return None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+        d = json.load(open(f))
+        k = d.get("kernels", {}).get(KERNEL_SYMBOL.get(kernel, kernel), {})
+        if d.get("lib_md5") == md5 and k.get("sq"):
+            return dict(k["sq"], source=os.path.relpath(f, ROOT))
+    return None
+
+
+def measure_pcie(eng: Engine, blocks_in: int, blocks_out: int, bs: int, cap: int = 4096) -> dict:
+    """H2D / D2H timed apart from the device step. The job
+    set's input blocks are staged from host memory into a GPU grid as blocks
+    read from storage (tbc_grid_put_blocks: host copy into pinned staging +
+    H2D), and its output blocks copied back (tbc_grid_get_blocks); at most
+    `cap` blocks are moved and the time scaled linearly (stated)."""
+    n_in, n_out = min(blocks_in, cap), min(blocks_out, cap)
+    grid = Grid(eng, max(n_in, n_out))
+    host = np.random.default_rng(1).integers(0, 256, size=(max(n_in, n_out), bs), dtype=np.uint8)
+    addrs = np.arange(1, max(n_in, n_out) + 1, dtype=np.uint64)
+    eng.synchronize()
+    t0 = time.perf_counter()
+    grid.put_blocks(addrs[:n_in], host[:n_in])
+    eng.synchronize()
+    h2d = (time.perf_counter() - t0) * blocks_in / n_in
+    t0 = time.perf_counter()
+    grid.get_blocks(addrs[:n_out])
+    d2h = (time.perf_counter() - t0) * blocks_out / n_out
+    grid.close()
+    return {"h2d": {"blocks": blocks_in, "bytes": blocks_in * bs, "ms": round(h2d * 1e3, 2),
+                    "GBps": round(blocks_in * bs / h2d / 1e9, 2)},
+            "d2h": {"blocks": blocks_out, "bytes": blocks_out * bs, "ms": round(d2h * 1e3, 2),
+                    "GBps": round(blocks_out * bs / d2h / 1e9, 2)},
+            "sample_blocks": [n_in, n_out]}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(configs.GENERATORS))
+    ap.add_argument("--config", type=int, default=2, choices=[1] + sorted(configs.GENERATORS))
+    ap.add_argument("--transfers", type=int, default=benchmark_load.TRANSFER_COUNT,
+                    help="config 1: transfers of the benchmark load (default: its 10M)")
     ap.add_argument("--jobs", type=int, default=None, help="jobs per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    njobs = args.jobs or configs.DEFAULT_JOBS[args.config]
+    njobs = args.jobs or configs.DEFAULT_JOBS.get(args.config, 1)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -217,6 +380,8 @@ def main() -> None:
 
     bs = 1 << 20
     eng = Engine(device=local, block_size=bs, profile=True, arena_bytes=2 << 30)
+    if args.config == 1:
+        return main_config1(args, eng, rank, world, local, dist, backend, bs)
     # Weak scaling: njobs jobs per GPU; the global job set is sharded by
     # input bytes (LPT, shard.py), no data-path collective.
     plan = plan_shards([configs.job_bytes(args.config, j) for j in range(njobs * world)], world)
@@ -289,6 +454,9 @@ def main() -> None:
     achieved = alg_bytes.get(dominant, R) / (kt_us * 1e-6) / 1e9
     job_bytes = R + W_data + W_index + wl.sort_bytes  # R + W (+ S)
     traffic, traffic_src = pmc_traffic(dominant)
+    blocks_in = sum(len(j.segments_a) if not j.a_immutable else 0 for j in wl.jobs) + \
+        sum(len(j.segments_b) for j in wl.jobs)
+    pcie = measure_pcie(eng, blocks_in, data_blocks + tables, bs) if world == 1 else None
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -313,6 +481,12 @@ def main() -> None:
                          "frac": round(job_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},
     }
+    if "data_blocks" in per_step:
+        line["compute_roofline"] = aes_roofline(out_values, data_blocks, per_step["data_blocks"], "data_blocks")
+    if pcie:
+        pcie["pcie_inclusive_MBps"] = round(wl.input_bytes / (step_s + (pcie["h2d"]["ms"] + pcie["d2h"]["ms"]) * 1e-3)
+                                            / 1e6, 1)
+        line["pcie"] = pcie
     if "assemble" not in per_step and "data_blocks" in per_step:
         # Latency regime: every data block's AEGIS-128L chain is in flight at
         # once, so the data-block kernel is bound by the chain of the longest
@@ -329,6 +503,96 @@ def main() -> None:
         line["cpu_baseline"] = cpu_baseline(args.config, njobs)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def main_config1(args, eng, rank, world, local, dist, backend, bs) -> None:
+    """BASELINE configs[0]: the `tigerbeetle benchmark` default load, replayed
+    (ReplayWorkload). Every rank is a replica compacting its own copy of the
+    forest, as every TigerBeetle replica does ("replicas only": no collective;
+    weak scaling)."""
+    wl = ReplayWorkload(eng, args.transfers, bs)
+    for _ in range(args.warmup):
+        wl.step(eng)
+
+    def barrier():
+        eng.synchronize()
+        if dist:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    import gc
+    gc.collect()
+    gc.disable()
+    ktimes: dict = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step(eng, ktimes)
+    barrier()
+    dt = time.perf_counter() - t0
+    gc.enable()
+    total_bytes, t_max = reduce_step(dist, wl.input_bytes, dt,
+                                     device=f"cuda:{local}" if dist and backend == "nccl" else None)
+    step_s = t_max / args.steps
+    per_step = {k: v / args.steps for k, v in ktimes.items()}
+    job_bytes = wl.input_bytes + wl.output_bytes + wl.sort_bytes
+    dominant = max(per_step, key=per_step.get) if per_step else None
+    line = {
+        "metric": METRIC,
+        "value": round(total_bytes / step_s / 1e6, 1),
+        "unit": "MB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: the tigerbeetle benchmark default load regenerated (tigerbeetle_amd/benchmark_load.py, "
+                "restated Zig DefaultPrng seed 42; deviations in host/benchmark_load.c)",
+        "config": {"workload": f"tigerbeetle benchmark default: {benchmark_load.ACCOUNT_COUNT} accounts, "
+                               f"{args.transfers} transfers in batches of {benchmark_load.BATCH}; every bar-end "
+                               f"memtable sort and half-bar compaction of the forest replayed on the GPU grid",
+                   "baseline_config": 1, "bars": len(wl.forest.swaps), "batches": wl.batches,
+                   "compactions": len(wl.jobs), "moves": wl.moves, "sort_batches": wl.sorts,
+                   "input_bytes_per_gpu": wl.input_bytes, "block_size": bs,
+                   "parallelism": f"replicas x{world}"},
+        "job_roofline": {"bytes": job_bytes, "achieved": round(job_bytes / step_s / 1e9, 1), "unit": "GB/s",
+                         "frac": round(job_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "terms": {"R": wl.input_bytes, "W": wl.output_bytes, "S": wl.sort_bytes}},
+        "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},
+        "pcie_inclusive": {"what": "the recording pass: host generation of every op, memtable puts streamed "
+                                   "H2D (tbc_memtable_put), all sorts and compactions",
+                           "seconds": round(wl.record_s, 3), "puts_bytes": wl.puts_bytes,
+                           "MBps": round(wl.input_bytes / wl.record_s / 1e6, 1)},
+    }
+    if dominant:
+        out_values = sum(c.result.value_count * c.tree.value_size for _, cs in wl.forest.history
+                         for _, c in cs if not c.move)
+        data_blocks = sum(c.result.data_block_count for _, cs in wl.forest.history for _, c in cs if not c.move)
+        W_data = out_values + 256 * data_blocks
+        alg = {"merge": wl.input_bytes, "data_blocks": out_values + W_data, "assemble": 2 * out_values,
+               "index_blocks": wl.output_bytes - W_data + 64 * data_blocks}
+        a_bytes = alg.get(dominant, wl.input_bytes)
+        achieved = a_bytes / (per_step[dominant] * 1e-6) / 1e9
+        traffic, traffic_src = pmc_traffic(dominant)
+        if "data_blocks" in per_step:
+            line["compute_roofline"] = aes_roofline(out_values, data_blocks, per_step["data_blocks"], "data_blocks")
+        line["roofline"] = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                            "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_step": a_bytes,
+                            "note": "the kernel's time summed over the replay's batches (hipEvents on the "
+                                    "engine stream); its AEGIS chains bound it, not HBM (DESIGN.md §4)"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_config1()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    wl.grid.close()
     eng.close()
     if dist:
         dist.destroy_process_group()

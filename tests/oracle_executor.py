@@ -45,13 +45,18 @@ class OracleExecutor:
         self.mutable.setdefault(name, []).append(np.ascontiguousarray(values))
 
     def swap(self, names):
+        """Every memtable becomes immutable (one run of values); the ones
+        named are sorted (TableMemory.sort, table_memory.zig:140-150)."""
         for name in set(self.mutable) | set(self.immutable):
-            self.mutable[name], self.immutable[name] = [], self.mutable.get(name, [])
+            vals = self.mutable.get(name, [])
+            self.mutable[name] = []
+            self.immutable[name] = [np.concatenate(vals)] if vals else []
         for name in names:
             spec = trees.BY_NAME[name]
-            vals = np.concatenate(self.immutable[name])
+            if not self.immutable[name]:
+                continue
             t0 = time.perf_counter()
-            self.immutable[name] = [self.oracle.sort_values(self._tree(spec), vals)]
+            self.immutable[name] = [self.oracle.sort_values(self._tree(spec), self.immutable[name][0])]
             self.busy += time.perf_counter() - t0
 
     def flushed(self, name):

@@ -143,13 +143,22 @@ class Tree:
         self.levels = [Level() for _ in range(LSM_LEVELS)]
         self.mutable_count = 0
         self.mutable_keys = [None, None]      # (min, max) of the mutable table's keys
+        self.mutable_sorted = True            # puts arrived in key order (table_memory.zig:83-87)
         self.immutable_count = 0
         self.immutable_keys = [None, None]
+        self.immutable_sorted = True
         self.immutable_flushed = True
         self.compactions: list = []
 
     # -- TableMemory ------------------------------------------------------
-    def put_keys(self, n: int, key_min: int, key_max: int) -> None:
+    def put_keys(self, n: int, key_min: int, key_max: int, in_order: bool = True, first: int | None = None) -> None:
+        """TableMemory.put of a batch: count, key range, and whether the
+        table is still sorted (the batch in order and not below the last key)."""
+        if self.mutable_keys[1] is not None and (not in_order or (first if first is not None else key_min) <
+                                                 self.mutable_keys[1]):
+            self.mutable_sorted = False
+        if not in_order:
+            self.mutable_sorted = False
         self.mutable_count += n
         lo, hi = self.mutable_keys
         self.mutable_keys = [key_min if lo is None else min(lo, key_min), key_max if hi is None else max(hi, key_max)]
@@ -159,8 +168,9 @@ class Tree:
         """tree.zig:979-999; returns whether the new immutable table has values."""
         assert self.immutable_flushed
         self.immutable_count, self.immutable_keys = self.mutable_count, self.mutable_keys
+        self.immutable_sorted = self.mutable_sorted
         self.immutable_flushed = self.immutable_count == 0
-        self.mutable_count, self.mutable_keys = 0, [None, None]
+        self.mutable_count, self.mutable_keys, self.mutable_sorted = 0, [None, None], True
         return self.immutable_count > 0
 
     # -- Manifest ---------------------------------------------------------
@@ -254,9 +264,12 @@ class Forest:
         self.cluster = cluster
         self.pending = None       # (batch handle, [Compaction]) of the running half-bar
         self.history: list = []   # per half-bar: (op, [Compaction]) once applied
+        self.swaps: list = []     # per bar end: [(tree, values, sorted)] made immutable
 
-    def put(self, name: str, values: np.ndarray, key_min: int, key_max: int) -> None:
-        self.trees[name].put_keys(len(values), key_min, key_max)
+    def put(self, name: str, values: np.ndarray) -> None:
+        spec = self.trees[name].spec
+        first, key_min, key_max, in_order = key_summary(values, spec)
+        self.trees[name].put_keys(len(values), key_min, key_max, in_order, first)
         self.executor.put(name, values)
 
     def compact(self, op: int) -> None:
@@ -291,24 +304,27 @@ class Forest:
             self.pending = None
         if beat == BAR - 1:
             swapped = [name for name in self.ORDER if self.trees[name].swap_mutable_and_immutable()]
-            self.executor.swap(swapped)
+            self.swaps.append([(name, self.trees[name].immutable_count, self.trees[name].immutable_sorted)
+                               for name in swapped])
+            # TableMemory.sort skips a table whose puts arrived in key order
+            # (table_memory.zig:110-150): only the others are sorted.
+            self.executor.swap([name for name in swapped if not self.trees[name].immutable_sorted])
 
     def run(self, load_ops, progress=None) -> None:
         """Commit every op of a workload: its puts, then Forest.compact(op)."""
         for op in load_ops:
             for name, values in op.puts.items():
-                spec = self.trees[name].spec
-                keys = key_range(values, spec)
-                self.put(name, values, keys[0], keys[1])
+                self.put(name, values)
             self.compact(op.op)
             if progress:
                 progress(op.op)
 
 
-def key_range(values: np.ndarray, spec: trees.TreeSpec) -> tuple:
-    """(min, max) of key_from_value over a put batch, as integers."""
+def key_summary(values: np.ndarray, spec: trees.TreeSpec) -> tuple:
+    """(first key, min key, max key, keys non-decreasing) of a put batch,
+    keys as integers (key_from_value: composite_key.zig:48-50, groove.zig)."""
     from . import workloads
-    limbs = workloads.keys_of(values, spec)
+    limbs = workloads.keys_of(values, spec)  # least significant limb first
 
     def extreme(pick):
         idx = np.arange(len(limbs[0]))
@@ -317,7 +333,15 @@ def key_range(values: np.ndarray, spec: trees.TreeSpec) -> tuple:
             idx = idx[v == pick(v)]
         return sum(int(l[idx[0]]) << (64 * i) for i, l in enumerate(limbs))
 
-    return extreme(np.min), extreme(np.max)
+    # consecutive keys in order: compare limbs from the most significant one
+    decided = np.zeros(max(0, len(limbs[0]) - 1), dtype=bool)
+    ok = np.ones_like(decided)
+    for l in reversed(limbs):
+        lt, gt = l[:-1] < l[1:], l[:-1] > l[1:]
+        ok &= ~(gt & ~decided)
+        decided |= lt | gt
+    first = sum(int(l[0]) << (64 * i) for i, l in enumerate(limbs))
+    return first, extreme(np.min), extreme(np.max), bool(ok.all())
 
 
 class GridExecutor:
@@ -350,6 +374,7 @@ class GridExecutor:
         self.puts_bytes += values.nbytes
 
     def swap(self, names: list) -> None:
+        """Every memtable becomes immutable; the ones named are sorted."""
         for name in list(self.mutable):
             self.mutable[name], self.immutable[name] = self.immutable[name], self.mutable[name]
             self.mutable[name].reset()

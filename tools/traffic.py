@@ -41,6 +41,10 @@ def counters(root: str, counter: str) -> dict:
     return {k: sum(v) / len(v) for k, v in per.items()}
 
 
+SQ_COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
+               "SQ_INSTS_SALU", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU"]
+
+
 def main() -> None:
     src, dst = sys.argv[1], sys.argv[2]
     os.makedirs(dst, exist_ok=True)
@@ -51,6 +55,11 @@ def main() -> None:
     fetch = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(src, "write"), "WRITE_SIZE")
     md5 = open(os.path.join(src, "lib.md5")).read().split()[0]
+    sq = {}
+    if glob.glob(os.path.join(src, "sq", "**", "*counter_collection.csv"), recursive=True):
+        for c in SQ_COUNTERS:
+            for k, v in counters(os.path.join(src, "sq"), c).items():
+                sq.setdefault(k, {})[c] = v
     out = {"lib_md5": md5, "note": "bytes per launch; fetch = 2 x FETCH_SIZE KiB (gfx950 correction), "
                                    "write = WRITE_SIZE KiB", "kernels": {}}
     for k in sorted(avg_ns):
@@ -59,6 +68,18 @@ def main() -> None:
         out["kernels"][k] = {"avg_ns": avg_ns[k], "fetch_bytes": round(f), "write_bytes": round(w),
                              "traffic_bytes": round(f + w),
                              "traffic_gbs": round((f + w) / avg_ns[k], 1) if avg_ns[k] else None}
+        if k in sq:
+            s = dict(sq[k])
+            # Rates against the chip: a wave64 VALU instruction holds a SIMD-32 for 2 cycles
+            # (1,024 SIMDs); LDS instructions per CU-cycle (256 CUs). Busy cycles are per-SE
+            # sums (SQ counters count quad-cycles for WAVE/WAIT/ACTIVE: MI355X_MICROARCH.md).
+            ns = avg_ns[k]
+            if ns:
+                s["valu_instr_per_ns"] = round(s.get("SQ_INSTS_VALU", 0) / ns, 2)
+                s["valu_issue_frac"] = round(s.get("SQ_INSTS_VALU", 0) * 2 / (1024 * 2.4 * ns), 4)
+                s["lds_instr_per_ns"] = round(s.get("SQ_INSTS_LDS", 0) / ns, 2)
+                s["lds_instr_frac"] = round(s.get("SQ_INSTS_LDS", 0) * 2 / (256 * 2.4 * ns), 4)
+            out["kernels"][k]["sq"] = s
     json.dump(out, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
