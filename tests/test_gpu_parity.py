@@ -168,6 +168,40 @@ def test_sort_values_already_sorted_is_noop(engine):
     assert np.array_equal(buf.download(vals.nbytes).reshape(5000, 32), vals)
 
 
+def test_sort_values_low_limbs_in_order(engine, oracle_lib):
+    """Tables already in order on their low key limbs, as a secondary index
+    put in timestamp order is: the sort skips those limbs' passes
+    (sort.hip k_sort_plan) and must still equal the oracle's stable sort.
+    Cases: timestamps ascending (skip 1 limb); (field lo, timestamp) in order
+    with the high field random and repeated keys (skip 2); an id whose low
+    limb ascends (skip 1); and a composite u64 index with tombstones."""
+    rng = np.random.default_rng(15)
+    n = 50_001
+    tables, wants = [], []
+
+    def add(name, limbs, tomb=None):
+        spec = trees.BY_NAME[name]
+        vals = workloads.values_from_keys(spec, limbs, np.zeros(n, bool) if tomb is None else tomb, rng)
+        t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                            spec.value_count_max, 1 << 20)
+        wants.append(oracle_lib.sort_values(t, vals))
+        tables.append((spec, engine.upload(vals, pad=16), n))
+
+    ts = np.arange(1, n + 1, dtype=np.uint64) * np.uint64(3)
+    add("transfers.debit_account_id", [ts, rng.integers(1, 10_001, n, dtype=np.uint64), np.zeros(n, np.uint64)])
+    lo = np.sort(rng.integers(0, 500, n, dtype=np.uint64))
+    ts2 = rng.integers(1, 40, n, dtype=np.uint64)
+    order = np.lexsort((ts2, lo))  # (lo, ts) ascending, duplicates kept
+    add("transfers.credit_account_id", [ts2[order], lo[order], rng.integers(0, 3, n, dtype=np.uint64)])
+    add("transfers.id", [np.arange(n, dtype=np.uint64), rng.integers(0, 1 << 40, n, dtype=np.uint64)])
+    add("accounts.user_data_64", [ts, rng.integers(0, 1 << 62, n, dtype=np.uint64)], rng.random(n) < 0.1)
+    engine.sort_values_batch(tables)
+    engine.synchronize()
+    for (spec, buf, _), want in zip(tables, wants):
+        got = buf.download(n * spec.value_size).reshape(n, spec.value_size)
+        assert np.array_equal(got, want), spec.name
+
+
 def test_immutable_compaction_after_device_sort(engine, oracle_lib):
     """Bar end: sort the mutable table on the device, then compact it as the
     immutable table A (tree.zig:979-999 -> compaction.zig:483-559)."""

@@ -109,6 +109,11 @@ struct tbc_engine {
     // tables' copies): grown on demand like the masks.
     uint8_t *sort_scratch = nullptr;
     uint64_t sort_scratch_size = 0;
+    // Its look-back words: zeroed when allocated, then tagged with a fresh
+    // epoch per pass launch (sort.hip), so no pass clears them.
+    uint64_t *sort_status = nullptr;
+    uint64_t sort_status_words = 0;
+    uint32_t sort_epoch = 1;
 };
 
 struct tbc_grid {
@@ -304,6 +309,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     hipFree(e->dev.base);
     if (e->masks) hipFree(e->masks);
     if (e->sort_scratch) hipFree(e->sort_scratch);
+    if (e->sort_status) hipFree(e->sort_status);
     if (e->side) hipStreamDestroy(e->side);
     hipStreamDestroy(e->stream);
     delete e;
@@ -589,6 +595,20 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
         }
         e->sort_scratch_size = want;
     }
+    const uint64_t words = sort_status_words(items.data(), count);
+    if (words > e->sort_status_words) {
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (e->sort_status) hipFree(e->sort_status);
+        e->sort_status = nullptr;
+        e->sort_status_words = 0;
+        const uint64_t want = align_up(words + words / 8, 1ull << 20);
+        if (hipMalloc((void **)&e->sort_status, 8 * want) != hipSuccess) {
+            e->sort_status = nullptr;
+            return TBC_ERR_OUT_OF_MEMORY;
+        }
+        if (hipMemsetAsync(e->sort_status, 0, 8 * want, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        e->sort_status_words = want;
+    }
     // The descriptors go through a pinned staging slot, reusable once the
     // stream has passed this sort.
     Staging &st = e->staging;
@@ -596,7 +616,8 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     st.next = (st.next + 1) % Staging::kSlots;
     if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
     uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
-    int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, host, e->stream);
+    int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, e->sort_status,
+                               e->sort_status_words, &e->sort_epoch, host, e->stream);
     if (hipEventRecord(st.ev[slot], e->stream) != hipSuccess) rc = -1;
     st.used[slot] = true;
     return rc == 0 ? TBC_OK : TBC_ERR_DEVICE;

@@ -6,24 +6,34 @@
 // keeps the LAST of a run of equal keys (compaction.zig:519-522).
 //
 // A batch of memtables (every tree's at the bar end) is sorted by one
-// enqueued launch sequence that never waits on the host:
+// enqueued launch sequence that never waits on the host. Items are sorted
+// as (packed key, index) pairs by a stable LSD radix sort with 8-bit digits:
 //
-//   k_sort_extract  per tile of 2,048 items: key limbs (limb-major) and item
-//                   indices, a copy of the values (the gather's source),
-//                   OR/AND of the keys, per-table sortedness, and the 8-bit
-//                   digit histograms of every pass, per table;
-//   k_sort_plan     per table: which passes move anything (a digit that is
-//                   constant over the batch cannot reorder), each pass's
-//                   source buffer, and every digit's start in its table;
-//   k_sort_pass x P one launch per potential pass (P = 8 per key limb); an
-//                   inactive pass returns at once. Onesweep: each tile ranks
+//   k_sort_extract  per tile of 2,048 items: a copy of the values (the
+//                   gather's source), OR/AND of every key limb, and whether
+//                   the table is out of order at all;
+//   k_sort_layout   per table: the key bytes that vary over the table, in
+//                   significance order; the rest cannot decide any order, so
+//                   the packed key (those bytes only, 8 per limb) orders the
+//                   table exactly as its key does (config 3's composite u128
+//                   keys: 24 key bytes, 6 varying -> one 64-bit limb);
+//   k_sort_pack     per tile: packed keys + indices, the digit histograms of
+//                   every packed byte, and which low-order prefixes of the
+//                   packed key the table is already in order on;
+//   k_sort_plan     per table: LSD passes run from the least significant
+//                   byte up, so the bytes of a prefix the table is already
+//                   in order on (a secondary index put in timestamp order)
+//                   cannot change the stable order and are skipped; each
+//                   remaining pass's source buffer; every digit's start;
+//   k_sort_pass x P one launch per potential pass (P = 8 per key limb of the
+//                   batch's widest key), persistent workgroups; a pass no
+//                   table needs returns at once. Onesweep: each tile ranks
 //                   its items by digit (wave match ballots + per-wave counts:
 //                   stable), publishes its digit counts, looks back over the
 //                   tiles before it in its table for their prefix (decoupled
-//                   look-back, one 32-bit flag|count word per tile and digit),
-//                   and writes the tile out through LDS so each digit's run
-//                   is contiguous;
-//   k_sort_gather   values[i] = copy[idx[i]] for tables that were unsorted.
+//                   look-back), and writes the tile out through LDS so each
+//                   digit's run is contiguous; a table's last pass moves
+//                   the values themselves (values[i] = copy[idx[i]]).
 //
 // Tiles never straddle tables, so a table's passes are independent of the
 // others' (a segmented sort with no table digit). Tables whose puts arrived
@@ -45,25 +55,31 @@ constexpr uint32_t kRadix = 256;
 constexpr uint32_t kMaxLimbs = 3;
 constexpr uint32_t kMaxPasses = 8 * kMaxLimbs;
 
-// Look-back words: flag in the top two bits, count below (counts < 2^30).
-constexpr uint32_t kFlagAggregate = 1u << 30;
-constexpr uint32_t kFlagPrefix = 2u << 30;
-constexpr uint32_t kCountMask = (1u << 30) - 1;
+// Look-back words (64-bit): the pass launch's epoch in the top half (words
+// of earlier launches read as "not published", so the buffer is zeroed once,
+// never per pass), the flag in bits 31:30, the count below (< 2^30).
+constexpr uint64_t kFlagAggregate = 1ull << 30;
+constexpr uint64_t kFlagPrefix = 2ull << 30;
+constexpr uint64_t kCountMask = (1ull << 30) - 1;
 
 struct SortSeg {
+    uint64_t key_or[kMaxLimbs], key_and[kMaxLimbs]; // over the table (extract)
     uint8_t *values;
     uint8_t *copy; // n * vs bytes: the table as put, the gather's source
     uint32_t n, vs, ts_off, kind;
-    uint32_t item_base, tile_base, tiles, unsorted;
+    uint32_t kl; // key limbs of the table's key kind
+    uint32_t item_base, tile_base, tiles;
+    uint32_t unsorted;  // some adjacent pair is out of key order (extract)
+    uint32_t nbytes;    // varying key bytes = packed key bytes (layout)
+    uint32_t viol;      // bit b: out of order on packed bytes [0, b] (pack)
+    uint32_t active;    // bit p: pass p moves this table's items (plan)
+    uint32_t src_bits;  // bit p: pass p reads buffer 1
+    uint32_t final_buf; // buffer the last pass would have written
+    uint8_t byte_src[kMaxPasses]; // packed byte j = key byte byte_src[j] (limb * 8 + byte)
 };
 
-struct SortPlan {
-    uint64_t key_or[kMaxLimbs], key_and[kMaxLimbs];
-    uint32_t active[kMaxPasses]; // pass moves items
-    uint32_t src[kMaxPasses];    // ping-pong buffer the pass reads
-    uint32_t final_buf;          // buffer holding the sorted indices
-    uint32_t kl;                 // key limbs of the batch
-    uint32_t any_unsorted;
+struct SortBatch {
+    uint32_t active; // passes some table needs
 };
 
 __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t ts_off, uint64_t k[3]) {
@@ -76,23 +92,28 @@ __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t
     }
 }
 
-// hist layout: [segment][pass][digit] u32.
+// hist / bins layout: [segment][pass][digit] u32.
 __device__ __forceinline__ uint32_t *seg_hist(uint32_t *hist, uint32_t s) { return hist + (size_t)s * kMaxPasses * kRadix; }
+
+// The key and the next item's key (the next lane's; lane 63 loads its
+// neighbour, which may sit in the next tile) of every lane of a row.
+__device__ __forceinline__ void row_keys(const SortSeg &S, uint32_t li, bool in, uint64_t k[3], uint64_t kn[3]) {
+    k[0] = k[1] = k[2] = 0;
+    if (in) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
+    for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
+    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
+}
 
 // --------------------------------------------------------------------------
 // Extract: one workgroup per tile.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, const uint32_t *tile_seg, uint32_t kl,
-                                                               uint32_t N, uint64_t *keys, uint32_t *idx,
-                                                               SortPlan *plan, uint32_t *hist) {
-    __shared__ uint32_t s_hist[kMaxPasses * kRadix];
+__global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, const uint32_t *tile_seg) {
     __shared__ uint64_t s_or[kMaxLimbs][kSortWaves], s_and[kMaxLimbs][kSortWaves];
     __shared__ uint32_t s_uns;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t sg = tile_seg[blockIdx.x];
     const SortSeg S = segs[sg];
     const uint32_t lt = blockIdx.x - S.tile_base;
-    for (uint32_t i = tid; i < 8 * kl * kRadix; i += kSortThreads) s_hist[i] = 0;
     if (tid == 0) s_uns = 0;
     __syncthreads();
     uint64_t o[kMaxLimbs] = {0, 0, 0}, a[kMaxLimbs] = {~0ull, ~0ull, ~0ull};
@@ -101,31 +122,20 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
         if (lt * kSortTile + r * kSortThreads >= S.n) break; // wave-uniform (whole row past the end)
         const bool in = li < S.n;
-        const uint32_t i = S.item_base + li;
-        uint64_t k[3] = {0, 0, 0}, kn[3];
-        if (in) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
-        // The next item's key comes from the next lane; lane 63 reads its neighbour.
-        for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
-        if (lane == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
+        uint64_t k[3], kn[3];
+        row_keys(S, li, in, k, kn);
         if (!in) continue;
         for (uint32_t q = 0; q < S.vs; q += 16)
             gst<u32x4>(S.copy + (size_t)li * S.vs + q, gld<u32x4>(S.values + (size_t)li * S.vs + q));
-        for (uint32_t l = 0; l < kl; l++) {
-            keys[(size_t)l * N + i] = k[l];
+        for (uint32_t l = 0; l < S.kl; l++) {
             o[l] |= k[l];
             a[l] &= k[l];
-            for (uint32_t b = 0; b < 8; b++) atomicAdd(&s_hist[(8 * l + b) * kRadix + ((k[l] >> (8 * b)) & 255)], 1u);
         }
-        idx[i] = i;
         if (li + 1 < S.n) {
-            bool gt = false, decided = false;
-            for (int l = (int)kl - 1; l >= 0 && !decided; l--) {
-                if (k[l] != kn[l]) {
-                    gt = k[l] > kn[l];
-                    decided = true;
-                }
-            }
-            uns |= gt ? 1u : 0u;
+            int cmp = 0;
+            for (uint32_t l = 0; l < S.kl; l++)
+                if (k[l] != kn[l]) cmp = k[l] > kn[l] ? 1 : -1;
+            uns |= cmp > 0 ? 1u : 0u;
         }
     }
     for (uint32_t l = 0; l < kMaxLimbs; l++) {
@@ -140,49 +150,140 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     }
     if (uns) atomicOr(&s_uns, 1u);
     __syncthreads();
-    uint32_t *h = seg_hist(hist, sg);
-    for (uint32_t i = tid; i < 8 * kl * kRadix; i += kSortThreads)
-        if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
-    if (tid < kl) {
+    if (tid < S.kl) {
         uint64_t oo = 0, aa = ~0ull;
         for (uint32_t w = 0; w < kSortWaves; w++) {
             oo |= s_or[tid][w];
             aa &= s_and[tid][w];
         }
-        atomicOr((unsigned long long *)&plan->key_or[tid], (unsigned long long)oo);
-        atomicAnd((unsigned long long *)&plan->key_and[tid], (unsigned long long)aa);
+        atomicOr((unsigned long long *)&segs[sg].key_or[tid], (unsigned long long)oo);
+        atomicAnd((unsigned long long *)&segs[sg].key_and[tid], (unsigned long long)aa);
     }
-    if (tid == 0 && s_uns) {
-        atomicOr(&segs[sg].unsorted, 1u);
-        atomicOr(&plan->any_unsorted, 1u);
+    if (tid == 0 && s_uns) atomicOr(&segs[sg].unsorted, 1u);
+}
+
+// Layout: one thread per table — its varying key bytes, least significant first.
+__global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs, uint32_t nseg) {
+    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= nseg) return;
+    SortSeg &S = segs[s];
+    uint32_t nb = 0;
+    if (S.unsorted)
+        for (uint32_t l = 0; l < S.kl; l++)
+            for (uint32_t b = 0; b < 8; b++)
+                if (((S.key_or[l] ^ S.key_and[l]) >> (8 * b)) & 255) S.byte_src[nb++] = (uint8_t)(8 * l + b);
+    S.nbytes = nb;
+}
+
+__device__ __forceinline__ void pack_key(const uint8_t *map, uint32_t nb, const uint64_t k[3], uint64_t pk[3]) {
+    pk[0] = pk[1] = pk[2] = 0;
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t src = map[j];
+        pk[j >> 3] |= ((k[src >> 3] >> (8 * (src & 7))) & 255ull) << (8 * (j & 7));
     }
 }
 
-// --------------------------------------------------------------------------
-// Plan: one workgroup per table (block 0 also fills the batch-wide plan).
-// bins[segment][pass][digit] = the digit's first item in the global item
-// space (table base + exclusive prefix of the table's histogram).
-// --------------------------------------------------------------------------
-__global__ __launch_bounds__(kRadix) void k_sort_plan(const SortSeg *segs, SortPlan *plan, const uint32_t *hist,
+// One wave's 64 digits into an LDS histogram row: a digit shared by the
+// whole row (a slowly varying key byte) is one add; otherwise the lanes
+// with equal digits (8 ballots) add once through their first lane.
+__device__ __forceinline__ void hist_add(uint32_t *row, uint32_t d, bool in) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t act = __ballot(in);
+    if (!act) return;
+    const uint32_t first = __builtin_ctzll(act);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)first);
+    if (!__ballot(in && d != d0)) {
+        if (lane == first) atomicAdd(&row[d0], (uint32_t)__builtin_popcountll(act));
+        return;
+    }
+    uint64_t peers = act;
+#pragma unroll
+    for (uint32_t b = 0; b < 8; b++) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    if (in && !(peers & ((1ull << lane) - 1))) atomicAdd(&row[d], (uint32_t)__builtin_popcountll(peers));
+}
+
+// Pack: one workgroup per tile of an unsorted table.
+__global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const uint32_t *tile_seg, uint32_t N,
+                                                            uint64_t *keys, uint32_t *idx, uint32_t *hist) {
+    __shared__ uint32_t s_hist[kMaxPasses][kRadix];
+    __shared__ uint32_t s_viol;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t sg = tile_seg[blockIdx.x];
+    const SortSeg S = segs[sg];
+    const uint32_t nb = S.nbytes;
+    if (!nb) return; // uniform: a sorted table
+    __shared__ uint8_t s_map[kMaxPasses]; // the byte map is read per item: LDS, not scratch
+    const uint32_t pl = (nb + 7) >> 3;
+    for (uint32_t j = 0; j < nb; j++) s_hist[j][tid] = 0;
+    if (tid < kMaxPasses) s_map[tid] = segs[sg].byte_src[tid];
+    if (tid == 0) s_viol = 0;
+    __syncthreads();
+    const uint32_t lt = blockIdx.x - S.tile_base;
+    uint32_t viol = 0;
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
+        if (lt * kSortTile + r * kSortThreads >= S.n) break; // uniform
+        const bool in = li < S.n;
+        uint64_t k[3], kn[3], pk[3], pn[3];
+        row_keys(S, li, in, k, kn);
+        pack_key(s_map, nb, k, pk);
+        const uint32_t i = S.item_base + li;
+        if (in) {
+            for (uint32_t l = 0; l < pl; l++) keys[(size_t)l * N + i] = pk[l];
+            idx[i] = i;
+        }
+        for (uint32_t j = 0; j < nb; j++) hist_add(s_hist[j], (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u, in);
+        if (in && li + 1 < S.n) {
+            pack_key(s_map, nb, kn, pn);
+            int cmp = 0; // order of (item, next) on packed bytes [0, j]
+            for (uint32_t j = 0; j < nb; j++) {
+                const uint32_t x = (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u;
+                const uint32_t y = (uint32_t)(pn[j >> 3] >> (8 * (j & 7))) & 255u;
+                if (x != y) cmp = x > y ? 1 : -1;
+                if (cmp > 0) viol |= 1u << j;
+            }
+        }
+    }
+    if (viol) atomicOr(&s_viol, viol);
+    __syncthreads();
+    uint32_t *h = seg_hist(hist, sg);
+    for (uint32_t j = 0; j < nb; j++)
+        if (s_hist[j][tid]) atomicAdd(&h[j * kRadix + tid], s_hist[j][tid]);
+    if (tid == 0 && s_viol) atomicOr(&segs[sg].viol, s_viol);
+}
+
+// Plan: one workgroup per table. Passes [skip, nbytes) run, where the table
+// is already in order on packed bytes [0, skip) (the largest such prefix);
+// then the digit starts of those passes.
+__global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *batch, const uint32_t *hist,
                                                       uint32_t *bins) {
     const uint32_t s = blockIdx.x, d = threadIdx.x, lane = d & 63, wave = d >> 6;
     __shared__ uint32_t wsum[kRadix / 64];
-    const uint32_t kl = plan->kl;
-    if (s == 0 && d == 0) {
-        uint32_t buf = 0;
-        for (uint32_t p = 0; p < kMaxPasses; p++) {
-            const uint32_t l = p >> 3;
-            const bool act = l < kl && plan->any_unsorted &&
-                             (((plan->key_or[l] ^ plan->key_and[l]) >> (8 * (p & 7))) & 255) != 0;
-            plan->active[p] = act ? 1u : 0u;
-            plan->src[p] = buf;
-            if (act) buf ^= 1u;
-        }
-        plan->final_buf = buf;
+    SortSeg &S = segs[s];
+    const uint32_t nb = S.nbytes;
+    uint32_t skip = 0;
+    for (uint32_t j = 1; j < nb; j++)
+        if (!((S.viol >> (j - 1)) & 1u)) skip = j;
+    uint32_t active = 0, src = 0, buf = 0;
+    for (uint32_t p = skip; p < nb; p++) {
+        active |= 1u << p;
+        src |= buf << p;
+        buf ^= 1u;
+    }
+    __syncthreads(); // every thread has read viol before thread 0 writes the plan
+    if (d == 0) {
+        S.active = active;
+        S.src_bits = src;
+        S.final_buf = buf;
+        if (active) atomicOr(&batch->active, active);
     }
     const uint32_t *h = hist + (size_t)s * kMaxPasses * kRadix;
     uint32_t *out = bins + (size_t)s * kMaxPasses * kRadix;
-    for (uint32_t p = 0; p < 8 * kl; p++) {
+    for (uint32_t m = active; m; m &= m - 1) {
+        const uint32_t p = __builtin_ctz(m);
         const uint32_t c = h[p * kRadix + d];
         uint32_t incl = c;
         for (int o = 1; o < 64; o <<= 1) {
@@ -193,177 +294,222 @@ __global__ __launch_bounds__(kRadix) void k_sort_plan(const SortSeg *segs, SortP
         __syncthreads();
         uint32_t off = 0;
         for (uint32_t w = 0; w < wave; w++) off += wsum[w];
-        out[p * kRadix + d] = segs[s].item_base + off + incl - c;
+        out[p * kRadix + d] = S.item_base + off + incl - c;
         __syncthreads();
     }
 }
 
 // --------------------------------------------------------------------------
-// One onesweep pass (digit = byte `p & 7` of limb `p >> 3`).
+// One onesweep pass (digit = packed byte p: byte p & 7 of packed limb p >> 3).
 // --------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lb_load(const uint32_t *p) {
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <uint32_t KL>
-__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const uint32_t *tile_seg,
-                                                            const SortPlan *plan, uint32_t p, uint32_t ntiles,
+// Persistent workgroups take tiles in arrival order (dynamic ids): every
+// tile one looks back on was taken by a workgroup that is running or done.
+// The tile is reordered through LDS one key limb at a time (16 KiB), so the
+// workgroup's LDS does not grow with the key width (5 workgroups per CU).
+// A table's last pass moves the values themselves (values[dst] =
+// copy[index]) instead of keys and indices: the gather is fused into it.
+__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
+                                                            const uint32_t *tile_seg, uint32_t p, uint32_t ntiles,
                                                             uint32_t N, uint64_t *keys0, uint64_t *keys1,
                                                             uint32_t *idx0, uint32_t *idx1, const uint32_t *bins,
-                                                            uint32_t *status, uint32_t *tile_counter) {
-    if (!plan->active[p]) return; // uniform: a constant digit cannot reorder anything
+                                                            uint64_t *status, uint32_t epoch,
+                                                            uint32_t *tile_counter) {
+    constexpr uint32_t R = kSortRounds;
     __shared__ uint32_t s_tile;
     __shared__ uint32_t s_wcnt[kSortWaves][kRadix]; // per wave: running, then total counts
     __shared__ uint32_t s_start[kRadix];            // local start of each digit in the tile
     __shared__ uint32_t s_excl[kRadix];             // items of the digit in the table's earlier tiles
-    __shared__ uint64_t s_key[KL][kSortTile];
+    __shared__ uint32_t s_wsum[kSortWaves];
+    __shared__ uint64_t s_key[kSortTile];           // one limb at a time
     __shared__ uint32_t s_idx[kSortTile];
+    __shared__ uint8_t s_dig[kSortTile];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // Dynamic tile ids in arrival order: every tile a workgroup looks back on
-    // was taken by a workgroup that is running or done (forward progress).
-    if (tid == 0) s_tile = atomicAdd(&tile_counter[p], 1u);
-    for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t t = s_tile;
-    if (t >= ntiles) return;
-    const uint32_t sg = tile_seg[t];
-    const SortSeg S = segs[sg];
-    if (!S.unsorted) return; // tables put in order are left as they are
-    const uint32_t lt = t - S.tile_base;
-    const uint32_t base = S.item_base + lt * kSortTile;
-    const uint32_t m = (S.n - lt * kSortTile) < kSortTile ? (S.n - lt * kSortTile) : kSortTile;
+    if (!((batch->active >> p) & 1u)) return; // uniform: no table needs this pass
     const uint32_t limb = p >> 3, shift = 8 * (p & 7);
-    const uint32_t live = plan->kl - limb; // limbs [limb, kl) still move with the items
-    const uint64_t *ksrc = plan->src[p] ? keys1 : keys0;
-    uint64_t *kdst = plan->src[p] ? keys0 : keys1;
-    const uint32_t *isrc = plan->src[p] ? idx1 : idx0;
-    uint32_t *idst = plan->src[p] ? idx0 : idx1;
-
-    // Wave w owns items [512 w, 512 w + 512) of the tile, 64 per round in
-    // lane order: stable rank = (earlier waves) + (earlier rounds of this
-    // wave, counted in s_wcnt) + (earlier lanes with the same digit).
+    const uint64_t ep = (uint64_t)epoch << 32;
     const uint64_t lt_mask = (1ull << lane) - 1;
-    uint32_t rank[kSortRounds], dig[kSortRounds];
-    uint64_t k[kSortRounds][KL];
-    uint32_t ix[kSortRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < kSortRounds; r++) {
-        const uint32_t e = wave * (64 * kSortRounds) + r * 64 + lane;
-        const bool in = e < m;
-#pragma unroll
-        for (uint32_t l = 0; l < KL; l++)
-            k[r][l] = in && l < live ? gld<uint64_t>(ksrc + (size_t)(limb + l) * N + base + e) : 0ull;
-        ix[r] = in ? gld<uint32_t>(isrc + base + e) : 0u;
-        const uint32_t d = in ? (uint32_t)(k[r][0] >> shift) & 255u : 0u;
-        dig[r] = d;
-        uint64_t peers = __ballot(in);
-#pragma unroll
-        for (uint32_t b = 0; b < 8; b++) {
-            const uint64_t bal = __ballot((d >> b) & 1u);
-            peers &= ((d >> b) & 1u) ? bal : ~bal;
-        }
-        const uint32_t before = __builtin_popcountll(peers & lt_mask);
-        const uint32_t prior = in ? s_wcnt[wave][d] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (in && before == 0) s_wcnt[wave][d] = prior + (uint32_t)__builtin_popcountll(peers);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        rank[r] = prior + before;
-    }
-    __syncthreads();
-    // Per digit (thread d): counts of the tile, exclusive prefix over waves,
-    // and the tile-local start (exclusive scan over digits).
-    const uint32_t d = tid;
-    uint32_t cnt = 0, wpre[kSortWaves];
-#pragma unroll
-    for (uint32_t w = 0; w < kSortWaves; w++) {
-        wpre[w] = cnt;
-        cnt += s_wcnt[w][d];
-    }
-    {
-        uint32_t incl = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= (uint32_t)o) incl += y;
-        }
-        __shared__ uint32_t s_wsum[kSortWaves];
-        if (lane == 63) s_wsum[wave] = incl;
+    for (;;) {
+        __syncthreads(); // the previous tile's LDS readers are done
+        if (tid == 0) s_tile = atomicAdd(&tile_counter[p], 1u);
+        for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
         __syncthreads();
-        uint32_t off = 0;
-        for (uint32_t w = 0; w < wave; w++) off += s_wsum[w];
-        s_start[d] = off + incl - cnt;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t w = 0; w < kSortWaves; w++) s_wcnt[w][d] = wpre[w]; // becomes the wave's offset
-    // Decoupled look-back over the table's earlier tiles, one digit per thread.
-    uint32_t *st = status + (size_t)p * ntiles * kRadix;
-    uint32_t excl = 0;
-    if (lt == 0) {
-        lb_store(&st[(size_t)t * kRadix + d], kFlagPrefix | cnt);
-    } else {
-        lb_store(&st[(size_t)t * kRadix + d], kFlagAggregate | cnt);
-        uint32_t pred = t - 1;
-        for (uint32_t spins = 0;;) {
-            const uint32_t v = lb_load(&st[(size_t)pred * kRadix + d]);
-            if ((v & ~kCountMask) == 0) { // not published yet
-                if (++spins > (1u << 26)) break; // bounded (a broken invariant, not a hang)
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += v & kCountMask;
-            if ((v & ~kCountMask) == kFlagPrefix || pred == S.tile_base) break;
-            pred--;
-        }
-        lb_store(&st[(size_t)t * kRadix + d], kFlagPrefix | (excl + cnt));
-    }
-    s_excl[d] = excl;
-    __syncthreads();
-    // Items into LDS at their tile-local sorted position.
-#pragma unroll
-    for (uint32_t r = 0; r < kSortRounds; r++) {
-        const uint32_t e = wave * (64 * kSortRounds) + r * 64 + lane;
-        if (e < m) {
-            const uint32_t pos = s_start[dig[r]] + s_wcnt[wave][dig[r]] + rank[r];
-#pragma unroll
-            for (uint32_t l = 0; l < KL; l++) s_key[l][pos] = k[r][l];
-            s_idx[pos] = ix[r];
-        }
-    }
-    __syncthreads();
-    // Out in that order: each digit's run lands contiguously.
-    const uint32_t *bin = bins + ((size_t)sg * kMaxPasses + p) * kRadix;
-    for (uint32_t j = tid; j < m; j += kSortThreads) {
-        const uint32_t dj = (uint32_t)(s_key[0][j] >> shift) & 255u;
-        const uint32_t dst = bin[dj] + s_excl[dj] + (j - s_start[dj]);
-#pragma unroll
-        for (uint32_t l = 0; l < KL; l++)
-            if (l < live) gst<uint64_t>(kdst + (size_t)(limb + l) * N + dst, s_key[l][j]);
-        gst<uint32_t>(idst + dst, s_idx[j]);
-    }
-}
+        const uint32_t t = s_tile;
+        if (t >= ntiles) return;
+        const uint32_t sg = tile_seg[t];
+        const SortSeg &S = segs[sg];
+        const uint32_t active = S.active;
+        if (!((active >> p) & 1u)) continue; // uniform: sorted table, skipped prefix
+        const bool last = (active >> p) == 1u;
+        const uint32_t lt = t - S.tile_base;
+        const uint32_t base = S.item_base + lt * kSortTile;
+        const uint32_t m = (S.n - lt * kSortTile) < kSortTile ? (S.n - lt * kSortTile) : kSortTile;
+        const uint32_t live = ((S.nbytes + 7) >> 3) - limb; // packed limbs [limb, ..) still move
+        const bool from1 = (S.src_bits >> p) & 1u;
+        const uint64_t *ksrc = from1 ? keys1 : keys0;
+        uint64_t *kdst = from1 ? keys0 : keys1;
+        const uint32_t *isrc = from1 ? idx1 : idx0;
+        uint32_t *idst = from1 ? idx0 : idx1;
 
-// values[i] = copy[idx[i]] (table-local), 16 bytes per lane; sorted tables
-// are left alone.
-__global__ __launch_bounds__(256) void k_sort_gather(const SortSeg *segs, const uint32_t *tile_seg,
-                                                     const SortPlan *plan, const uint32_t *idx0,
-                                                     const uint32_t *idx1) {
-    const SortSeg S = segs[tile_seg[blockIdx.x]];
-    if (!S.unsorted) return;
-    const uint32_t *idx = plan->final_buf ? idx1 : idx0;
-    const uint32_t lt = blockIdx.x - S.tile_base;
-    const uint32_t first = lt * kSortTile;
-    const uint32_t m = (S.n - first) < kSortTile ? (S.n - first) : kSortTile;
-    const uint32_t cpv = S.vs >> 4;
-    for (uint32_t c = threadIdx.x; c < m * cpv; c += 256) {
-        const uint32_t e = c / cpv, part = c % cpv;
-        const uint32_t src = gld<uint32_t>(idx + S.item_base + first + e) - S.item_base;
-        gst<u32x4>(S.values + (size_t)(first + e) * S.vs + 16 * part,
-                   gld<u32x4>(S.copy + (size_t)src * S.vs + 16 * part));
+        // Wave w owns items [512 w, 512 w + 512) of the tile, 64 per round in
+        // lane order: stable rank = (earlier waves) + (earlier rounds of this
+        // wave, counted in s_wcnt) + (earlier lanes with the same digit).
+        uint32_t rank[R], dig[R], ix[R];
+        uint64_t k[R][kMaxLimbs];
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = wave * (64 * R) + r * 64 + lane;
+            const bool in = e < m;
+#pragma unroll
+            for (uint32_t l = 0; l < kMaxLimbs; l++)
+                k[r][l] = in && l < live ? gld<uint64_t>(ksrc + (size_t)(limb + l) * N + base + e) : 0ull;
+            ix[r] = in ? gld<uint32_t>(isrc + base + e) : 0u;
+            const uint32_t d = in ? (uint32_t)(k[r][0] >> shift) & 255u : 0u;
+            dig[r] = d;
+            uint64_t peers = __ballot(in);
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) {
+                const uint64_t bal = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? bal : ~bal;
+            }
+            const uint32_t before = __builtin_popcountll(peers & lt_mask);
+            const uint32_t prior = in ? s_wcnt[wave][d] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (in && before == 0) s_wcnt[wave][d] = prior + (uint32_t)__builtin_popcountll(peers);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            rank[r] = prior + before;
+        }
+        __syncthreads();
+        // Per digit (thread d): counts of the tile, exclusive prefix over
+        // waves, and the tile-local start (exclusive scan over digits).
+        const uint32_t d = tid;
+        uint32_t cnt = 0, wpre[kSortWaves];
+#pragma unroll
+        for (uint32_t w = 0; w < kSortWaves; w++) {
+            wpre[w] = cnt;
+            cnt += s_wcnt[w][d];
+        }
+        {
+            uint32_t incl = cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            if (lane == 63) s_wsum[wave] = incl;
+            __syncthreads();
+            uint32_t off = 0;
+            for (uint32_t w = 0; w < wave; w++) off += s_wsum[w];
+            s_start[d] = off + incl - cnt;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t w = 0; w < kSortWaves; w++) s_wcnt[w][d] = wpre[w]; // becomes the wave's offset
+        // Decoupled look-back over the table's earlier tiles, one digit per thread.
+        uint32_t excl = 0;
+        if (lt == 0) {
+            lb_store(&status[(size_t)t * kRadix + d], ep | kFlagPrefix | cnt);
+        } else {
+            lb_store(&status[(size_t)t * kRadix + d], ep | kFlagAggregate | cnt);
+            // Tiles in flight together all publish their aggregates at about
+            // the same time, so a walk can be long: read a window of kLook
+            // predecessors per round trip, nearest first.
+            constexpr uint32_t kLook = 8;
+            uint32_t pred = t - 1;
+            for (uint32_t spins = 0;;) {
+                uint64_t v[kLook];
+#pragma unroll
+                for (uint32_t w = 0; w < kLook; w++)
+                    v[w] = pred >= S.tile_base + w ? lb_load(&status[(size_t)(pred - w) * kRadix + d]) : 0ull;
+                bool done = false, stall = false;
+#pragma unroll
+                for (uint32_t w = 0; w < kLook; w++) {
+                    if (done || stall) continue;
+                    if ((v[w] >> 32) != epoch || !(v[w] & (3ull << 30))) { // not published by this pass yet
+                        stall = true;
+                        pred -= w;
+                        continue;
+                    }
+                    excl += (uint32_t)(v[w] & kCountMask);
+                    if ((v[w] & (3ull << 30)) == kFlagPrefix || pred - w == S.tile_base) done = true;
+                }
+                if (done) break;
+                if (stall) {
+                    if (++spins > (1u << 24)) break; // bounded (a broken invariant, not a hang)
+                    __builtin_amdgcn_s_sleep(1);
+                } else {
+                    pred -= kLook;
+                }
+            }
+            lb_store(&status[(size_t)t * kRadix + d], ep | kFlagPrefix | (excl + cnt));
+        }
+        s_excl[d] = excl;
+        __syncthreads();
+        // Tile-local sorted position of every item; indices and digits into LDS.
+        uint32_t pos[R];
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = wave * (64 * R) + r * 64 + lane;
+            pos[r] = s_start[dig[r]] + s_wcnt[wave][dig[r]] + rank[r];
+            if (e < m) {
+                s_idx[pos[r]] = ix[r];
+                s_dig[pos[r]] = (uint8_t)dig[r];
+            }
+        }
+        __syncthreads();
+        // Destination of sorted position j = tid + 256 q: each digit's run
+        // lands contiguously.
+        const uint32_t *bin = bins + ((size_t)sg * kMaxPasses + p) * kRadix;
+        uint32_t dst[R];
+#pragma unroll
+        for (uint32_t q = 0; q < R; q++) {
+            const uint32_t j = tid + kSortThreads * q;
+            const uint32_t dj = j < m ? s_dig[j] : 0u;
+            dst[q] = bin[dj] + s_excl[dj] + (j - s_start[dj]);
+        }
+        if (last) {
+            // values[dst] = copy[index]: 16 bytes per lane, a lane group per value.
+            const uint32_t cpv = S.vs >> 4, vpr = kSortThreads / cpv; // values per row of the workgroup
+            for (uint32_t j0 = 0; j0 < m; j0 += vpr) {
+                const uint32_t j = j0 + tid / cpv, part = tid % cpv;
+                if (j < m) {
+                    const uint32_t dj = s_dig[j];
+                    const uint32_t to = bin[dj] + s_excl[dj] + (j - s_start[dj]) - S.item_base;
+                    const uint32_t from = s_idx[j] - S.item_base;
+                    gst<u32x4>(S.values + (size_t)to * S.vs + 16 * part,
+                               gld<u32x4>(S.copy + (size_t)from * S.vs + 16 * part));
+                }
+            }
+            continue;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < R; q++) {
+            const uint32_t j = tid + kSortThreads * q;
+            if (j < m) gst<uint32_t>(idst + dst[q], s_idx[j]);
+        }
+#pragma unroll
+        for (uint32_t l = 0; l < kMaxLimbs; l++) { // unrolled: k[r][l] stays in registers
+            if (l >= live) break;
+            __syncthreads(); // the previous limb's readers are done
+#pragma unroll
+            for (uint32_t r = 0; r < R; r++) {
+                const uint32_t e = wave * (64 * R) + r * 64 + lane;
+                if (e < m) s_key[pos[r]] = k[r][l];
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < R; q++) {
+                const uint32_t j = tid + kSortThreads * q;
+                if (j < m) gst<uint64_t>(kdst + (size_t)(limb + l) * N + dst[q], s_key[j]);
+            }
+        }
     }
 }
 
@@ -372,9 +518,11 @@ static uint32_t key_limbs(uint32_t kind) { return kind == kKeyTimestamp ? 1 : ki
 static uint64_t tiles_of(uint32_t n) { return (n + kSortTile - 1) / kSortTile; }
 static uint64_t align256(uint64_t x) { return (x + 255) / 256 * 256; }
 
-// Scratch layout (sort_scratch_bytes must match launch_sort_batch).
+// Scratch layout (sort_scratch_bytes must match launch_sort_batch). The
+// look-back words live in their own buffer (sort_status_words): epochs are
+// only unique there.
 struct SortScratch {
-    uint64_t plan, segs, tile_seg, keys, idx, hist, bins, status, counters, copies, total;
+    uint64_t segs, tile_seg, hist, counters, batch, bins, keys, idx, copies, total;
 };
 
 static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
@@ -389,24 +537,22 @@ static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
     }
     SortScratch s;
     uint64_t o = 0;
-    s.plan = o;
-    o += align256(sizeof(SortPlan));
     s.segs = o;
     o += align256(sizeof(SortSeg) * count);
     s.tile_seg = o;
     o += align256(4 * tiles);
+    s.hist = o; // zeroed per batch: hist, counters, batch
+    o += align256(4ull * nseg * kMaxPasses * kRadix);
+    s.counters = o;
+    o += align256(4ull * kMaxPasses);
+    s.batch = o;
+    o += align256(sizeof(SortBatch));
+    s.bins = o;
+    o += align256(4ull * nseg * kMaxPasses * kRadix);
     s.keys = o;
     o += 2 * align256(8 * N * kl);
     s.idx = o;
     o += 2 * align256(4 * N);
-    s.hist = o;
-    o += align256(4ull * nseg * kMaxPasses * kRadix);
-    s.bins = o;
-    o += align256(4ull * nseg * kMaxPasses * kRadix);
-    s.status = o;
-    o += align256(4ull * 8 * kl * tiles * kRadix);
-    s.counters = o;
-    o += align256(4ull * kMaxPasses);
     s.copies = o;
     o += vals;
     s.total = o;
@@ -415,30 +561,39 @@ static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
 
 uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count) { return scratch_layout(items, count).total; }
 
-// Everything is enqueued on `stream`; the host never waits. The plan, table
-// descriptors and tile map go through the caller's pinned staging (`host`,
-// at least sort_host_bytes) which must stay untouched until the stream has
-// passed this batch.
-uint64_t sort_host_bytes(const SortItem *items, uint32_t count) {
-    const SortScratch s = scratch_layout(items, count);
-    return s.keys; // plan + segs + tile map
+uint64_t sort_status_words(const SortItem *items, uint32_t count) {
+    uint64_t tiles = 0;
+    for (uint32_t j = 0; j < count; j++)
+        if (items[j].n >= 2) tiles += tiles_of(items[j].n);
+    return tiles * kRadix;
 }
 
-int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *host,
-                      void *stream) {
+// Everything is enqueued on `stream`; the host never waits. The table
+// descriptors and tile map go through the caller's pinned staging (`host`,
+// at least sort_host_bytes) which must stay untouched until the stream has
+// passed this batch. `status` (sort_status_words, zeroed once when
+// allocated) is reused by every pass: each pass launch takes a fresh epoch.
+uint64_t sort_host_bytes(const SortItem *items, uint32_t count) {
+    const SortScratch s = scratch_layout(items, count);
+    return s.hist; // segs + tile map
+}
+
+int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, uint64_t *status,
+                      uint64_t status_words, uint32_t *epoch, void *host, void *stream) {
     const SortScratch L = scratch_layout(items, count);
-    if (scratch_bytes < L.total) return -1;
+    if (scratch_bytes < L.total || status_words < sort_status_words(items, count)) return -1;
     hipStream_t s = (hipStream_t)stream;
     uint8_t *base = (uint8_t *)scratch, *hbase = (uint8_t *)host;
-    SortPlan *hplan = (SortPlan *)(hbase + L.plan);
     SortSeg *hsegs = (SortSeg *)(hbase + L.segs);
     uint32_t *htile = (uint32_t *)(hbase + L.tile_seg);
-    uint32_t N = 0, kl = 1, nseg = 0, ntiles = 0;
+    uint32_t N = 0, nseg = 0, ntiles = 0;
+    uint32_t max_kl = 0;
     uint64_t copy_off = L.copies;
     for (uint32_t j = 0; j < count; j++) {
         const SortItem &it = items[j];
         if (it.n < 2) continue;
         SortSeg g{};
+        for (uint32_t l = 0; l < kMaxLimbs; l++) g.key_and[l] = ~0ull;
         g.values = (uint8_t *)it.values;
         g.copy = base + copy_off;
         copy_off += align256((uint64_t)it.n * it.value_size);
@@ -446,50 +601,39 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         g.vs = it.value_size;
         g.ts_off = it.timestamp_offset;
         g.kind = it.key_kind;
+        g.kl = key_limbs(it.key_kind);
         g.item_base = N;
         g.tile_base = ntiles;
         g.tiles = (uint32_t)tiles_of(it.n);
         for (uint32_t t = 0; t < g.tiles; t++) htile[ntiles + t] = nseg;
         ntiles += g.tiles;
         N += it.n;
-        kl = kl > key_limbs(it.key_kind) ? kl : key_limbs(it.key_kind);
+        max_kl = max_kl > g.kl ? max_kl : g.kl;
         hsegs[nseg++] = g;
     }
     if (!nseg) return 0;
-    memset(hplan, 0, sizeof(SortPlan));
-    for (uint32_t l = 0; l < kMaxLimbs; l++) hplan->key_and[l] = ~0ull;
-    hplan->kl = kl;
-    SortPlan *plan = (SortPlan *)(base + L.plan);
     SortSeg *d_segs = (SortSeg *)(base + L.segs);
     uint32_t *d_tile = (uint32_t *)(base + L.tile_seg);
-    uint64_t *keys0 = (uint64_t *)(base + L.keys), *keys1 = (uint64_t *)(base + L.keys + align256(8ull * N * kl));
+    const uint64_t klw = align256(8ull * N * max_kl);
+    uint64_t *keys0 = (uint64_t *)(base + L.keys), *keys1 = (uint64_t *)(base + L.keys + klw);
     uint32_t *idx0 = (uint32_t *)(base + L.idx), *idx1 = (uint32_t *)(base + L.idx + align256(4ull * N));
     uint32_t *hist = (uint32_t *)(base + L.hist), *bins = (uint32_t *)(base + L.bins);
-    uint32_t *status = (uint32_t *)(base + L.status), *counters = (uint32_t *)(base + L.counters);
-    // Histograms, look-back words and tile counters start at zero.
-    if (hipMemcpyAsync(base, hbase, L.keys, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(hist, 0, L.copies - L.hist, s) != hipSuccess)
+    uint32_t *counters = (uint32_t *)(base + L.counters);
+    SortBatch *d_batch = (SortBatch *)(base + L.batch);
+    if (hipMemcpyAsync(base, hbase, L.hist, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(hist, 0, L.bins - L.hist, s) != hipSuccess)
         return -1;
-    hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, kl, N, keys0, idx0,
-                       plan, hist);
-    hipLaunchKernelGGL(k_sort_plan, dim3(nseg), dim3(kRadix), 0, s, d_segs, plan, hist, bins);
-    for (uint32_t p = 0; p < 8 * kl; p++) {
-        switch (kl - (p >> 3)) { // limbs still moving in this pass
-        case 1:
-            hipLaunchKernelGGL(k_sort_pass<1>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, plan, p, ntiles,
-                               N, keys0, keys1, idx0, idx1, bins, status, counters);
-            break;
-        case 2:
-            hipLaunchKernelGGL(k_sort_pass<2>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, plan, p, ntiles,
-                               N, keys0, keys1, idx0, idx1, bins, status, counters);
-            break;
-        default:
-            hipLaunchKernelGGL(k_sort_pass<3>, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, plan, p, ntiles,
-                               N, keys0, keys1, idx0, idx1, bins, status, counters);
-            break;
-        }
+    hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile);
+    hipLaunchKernelGGL(k_sort_layout, dim3((nseg + 63) / 64), dim3(64), 0, s, d_segs, nseg);
+    hipLaunchKernelGGL(k_sort_pack, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, N, keys0, idx0, hist);
+    hipLaunchKernelGGL(k_sort_plan, dim3(nseg), dim3(kRadix), 0, s, d_segs, d_batch, hist, bins);
+    // Persistent: five workgroups per CU fit the LDS.
+    const uint32_t pgrid = ntiles < 1280 ? ntiles : 1280;
+    for (uint32_t p = 0; p < 8 * max_kl; p++) {
+        if (*epoch == 0) *epoch = 1; // 0 is the zeroed buffer's
+        hipLaunchKernelGGL(k_sort_pass, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, p, ntiles, N,
+                           keys0, keys1, idx0, idx1, bins, status, (*epoch)++, counters);
     }
-    hipLaunchKernelGGL(k_sort_gather, dim3(ntiles), dim3(256), 0, s, d_segs, d_tile, plan, idx0, idx1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

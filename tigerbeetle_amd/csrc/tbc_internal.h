@@ -217,9 +217,10 @@ struct SortItem {
 };
 // Enqueues the whole sort of a batch of memtables (no host wait); `host` is
 // pinned staging of sort_host_bytes() that must outlive the enqueued copy.
-int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, void *host,
-                      void *stream);
+int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, uint64_t *status,
+                      uint64_t status_words, uint32_t *epoch, void *host, void *stream);
 uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count);
+uint64_t sort_status_words(const SortItem *items, uint32_t count);
 uint64_t sort_host_bytes(const SortItem *items, uint32_t count);
 size_t kway_scan_tmp_bytes(uint32_t n);
 int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
