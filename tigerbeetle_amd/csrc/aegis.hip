@@ -811,7 +811,7 @@ constexpr uint32_t kMaxChainOnlyWaves = 16;
 // Above this many chain waves (2 per SIMD) the two-pass path wins.
 constexpr uint32_t kFusedMaxChainWaves = 2048;
 
-template <bool Fused>
+template <bool Fused, class ChainStep = StepBpermute>
 __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
                                                       const JobResultDev *res, const uint64_t *status,
                                                       const uint64_t *masks, const uint32_t *block_tile,
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
         if (__hip_atomic_load(ready + j.dblock_base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
             gst<uint32_t>(const_cast<uint32_t *>(&res[j.job_index].invariant), 0xdeafu);
         GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
-        body_tag = aegis_mac32<GlobalMsg, StepBpermute>(sT, body);
+        body_tag = aegis_mac32<GlobalMsg, ChainStep>(sT, body);
     }
 
     HeaderFields h;
@@ -1131,6 +1131,26 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
     }
 }
 
+// Pipelined batches (tbc_compaction_submit, grid mode): the data block
+// addresses of every output table's index block (TableIndex.data_addresses,
+// schema.zig:80-260), written with the bodies so that a later batch can
+// resolve these tables before this batch's chains have sealed them. The seal
+// (k_index_blocks) rewrites the same values with the rest of the block.
+__global__ __launch_bounds__(256) void k_index_layout(const JobDesc *jobs, int njobs, uint32_t total,
+                                                      const JobResultDev *res) {
+    const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= total) return;
+    const int ji = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
+    const JobDesc &j = jobs[ji];
+    const uint32_t k = m - j.dblock_base;
+    const uint32_t db = res[j.job_index].data_block_count;
+    if (k >= db) return;
+    const uint32_t t = k / j.dbcm;
+    const uint32_t k_last = ((t + 1) * j.dbcm < db ? (t + 1) * j.dbcm : db) - 1;
+    uint8_t *idx = block_ptr(j, index_block_slot(t, k_last));
+    gst<uint64_t>(idx + j.idx_addresses_off + 8 * (k - t * j.dbcm), gld<uint64_t>(j.addresses + data_block_slot(k, j.dbcm)));
+}
+
 // One workgroup per CU (the tables take 128 KiB of LDS): spread the waves
 // over all 256 CUs, at most 16 waves per workgroup.
 static uint32_t waves_per_block(uint32_t waves) {
@@ -1218,6 +1238,59 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         hipLaunchKernelGGL(k_data_blocks<false>, dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs, njobs,
                            total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
                            c, (const uint32_t *)d_ready);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (mark) mark(mark_ctx, "data_blocks");
+    if (total_tables) {
+        hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (mark) mark(mark_ctx, "index_blocks");
+    return 0;
+}
+
+// Pipelined batch, front (engine stream, in order with every later batch's
+// front): every body assembled, and the output index blocks' data addresses.
+int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks,
+                        uint32_t *d_ready, const JobResultDev *d_results, const uint64_t *d_status,
+                        const uint64_t *d_masks, const SplitDesc *d_splits, void *stream,
+                        void (*mark)(void *, const char *), void *mark_ctx) {
+    hipStream_t s = (hipStream_t)stream;
+    if (total_dblocks) {
+        const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+        hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                           d_masks, d_splits, d_ready, d_results);
+        if (hipGetLastError() != hipSuccess) return -1;
+        hipLaunchKernelGGL(k_index_layout, dim3((total_dblocks + 255) / 256), dim3(256), 0, s, d_jobs, njobs,
+                           total_dblocks, d_results);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (mark) mark(mark_ctx, "assemble");
+    return 0;
+}
+
+// Pipelined batch, tail (one of the engine's tail streams, after the front):
+// the chains and headers of every data block, then the index blocks. Tails
+// of consecutive batches run concurrently, so their chains share the chip.
+int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
+                       JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
+                       const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
+                       void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t waves = (total_dblocks + 1) / 2;
+    if (total_dblocks) {
+        if (waves <= 1024) { // latency regime: one chain per SIMD, round keys by VALU lane moves
+            const uint32_t c = waves_per_block(waves);
+            hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                               d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                               d_block_tile, d_splits, c, d_ready);
+        } else {
+            const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
+            const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
+            hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                               d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                               d_block_tile, d_splits, c, d_ready);
+        }
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "data_blocks");

@@ -96,7 +96,15 @@ struct tbc_engine {
     uint32_t block_size = 0;
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr; // grid input validation beside the compaction (joined before results)
+    // Tail streams of pipelined (grid) batches: a batch's chains, index
+    // blocks, input checks and results run on one of them, after its front
+    // (merge + bodies) on `stream`; the next batch's front does not wait
+    // for them, so consecutive batches' AEGIS chains share the chip. Main +
+    // tails = 4 streams, HIP's hardware queues per process.
+    static constexpr int kTails = 3;
+    hipStream_t tail[kTails] = {};
+    hipEvent_t tail_ev[kTails] = {}; // the last batch finished on each tail
+    int next_tail = 0;
     Arena dev, host;
     Staging staging;
     std::vector<hipEvent_t> event_pool;
@@ -211,7 +219,8 @@ struct tbc_batch {
     std::vector<uint32_t> info_base; // per original job index
     std::vector<uint32_t> status;    // host-side validation status per job
     hipEvent_t done = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;          // side-stream validation (grid inputs)
+    hipEvent_t fork = nullptr;                          // end of the front (pipelined batches)
+    hipStream_t mark_stream = nullptr;                  // where mark_cb records
     hipEvent_t marks[kMaxMarks] = {};
     const char *mark_names[kMaxMarks] = {};
     int nmarks = 0;
@@ -242,10 +251,19 @@ static void debug_stage(hipStream_t s, const char *name) {
 
 static void mark_cb(void *ctx, const char *name) {
     tbc_batch *b = (tbc_batch *)ctx;
-    debug_stage(b->engine->stream, name);
+    hipStream_t s = b->mark_stream ? b->mark_stream : b->engine->stream;
+    debug_stage(s, name);
     if (!(b->engine->flags & TBC_CONFIG_PROFILE) || b->nmarks >= kMaxMarks) return;
-    hipEventRecord(b->marks[b->nmarks], b->engine->stream);
+    hipEventRecord(b->marks[b->nmarks], s);
     b->mark_names[b->nmarks++] = name;
+}
+
+// Later work on the engine stream that touches grid blocks (staging blocks in
+// or out, synchronous checks) waits for every batch tail enqueued so far.
+static bool join_tails(tbc_engine *e) {
+    for (int t = 0; t < tbc_engine::kTails; t++)
+        if (hipStreamWaitEvent(e->stream, e->tail_ev[t], 0) != hipSuccess) return false;
+    return true;
 }
 
 extern "C" {
@@ -283,8 +301,11 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
         delete e;
         return TBC_ERR_OUT_OF_MEMORY;
     }
-    bool ok = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
+    bool ok = true;
+    for (int t = 0; ok && t < tbc_engine::kTails; t++)
+        ok = hipStreamCreateWithFlags(&e->tail[t], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
     for (int s = 0; ok && s < Staging::kSlots; s++)
         ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
@@ -300,7 +321,8 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (!e) return;
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
-    if (e->side) hipStreamSynchronize(e->side);
+    for (int t = 0; t < tbc_engine::kTails; t++)
+        if (e->tail[t]) hipStreamSynchronize(e->tail[t]);
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
     for (int s = 0; s < Staging::kSlots; s++)
         if (e->staging.ev[s]) hipEventDestroy(e->staging.ev[s]);
@@ -310,7 +332,10 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (e->masks) hipFree(e->masks);
     if (e->sort_scratch) hipFree(e->sort_scratch);
     if (e->sort_status) hipFree(e->sort_status);
-    if (e->side) hipStreamDestroy(e->side);
+    for (int t = 0; t < tbc_engine::kTails; t++) {
+        if (e->tail_ev[t]) hipEventDestroy(e->tail_ev[t]);
+        if (e->tail[t]) hipStreamDestroy(e->tail[t]);
+    }
     hipStreamDestroy(e->stream);
     delete e;
 }
@@ -341,8 +366,7 @@ tbc_status tbc_grid_init(tbc_engine *e, uint64_t block_count, tbc_grid **out) {
 void tbc_grid_deinit(tbc_grid *g) {
     if (!g) return;
     hipSetDevice(g->engine->device);
-    hipStreamSynchronize(g->engine->stream);
-    hipStreamSynchronize(g->engine->side);
+    tbc_synchronize(g->engine);
     hipFree(g->verified);
     hipFree(g->base);
     delete g;
@@ -360,6 +384,7 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
         if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
+    if (!join_tails(e)) return TBC_ERR_DEVICE; // no running batch reads a block being replaced
     for (uint32_t i = 0; i < count; i++) {
         if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size) ||
             hipMemsetAsync(g->verified + addresses[i] - 1, 0, 1, e->stream) != hipSuccess) // validate before trusting
@@ -374,6 +399,7 @@ tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *con
         if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
+    if (!join_tails(e)) return TBC_ERR_DEVICE; // blocks still being sealed by a batch tail
     for (uint32_t i = 0; i < count; i++)
         if (!stage_d2h(e, blocks[i], g->base + (addresses[i] - 1) * e->block_size, e->block_size))
             return TBC_ERR_DEVICE;
@@ -494,7 +520,9 @@ tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes
 tbc_status tbc_synchronize(tbc_engine *e) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
+    for (int t = 0; t < tbc_engine::kTails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
+    return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const uint64_t *lengths, uint32_t count,
@@ -504,6 +532,7 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
     for (uint32_t i = 0; i < count; i++)
         if (lengths[i] > 0xffffffffull || (lengths[i] && !messages[i])) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
+    if (!join_tails(e)) return TBC_ERR_DEVICE; // the messages may be blocks a batch tail still writes
     const uint64_t dt = e->dev.top, ht = e->host.top;
     uint8_t *d = e->dev.alloc(16ull * count + 16ull * count);
     uint8_t *h = e->host.alloc(16ull * count + 16ull * count);
@@ -540,6 +569,7 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
     for (uint32_t i = 0; i < count; i++)
         if (!blocks[i] || ((uintptr_t)blocks[i] & 15)) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
+    if (!join_tails(e)) return TBC_ERR_DEVICE; // the messages may be blocks a batch tail still writes
     const uint64_t in_bytes = 32ull * count, out_off = align_up(in_bytes, 256);
     const uint64_t dt = e->dev.top, ht = e->host.top;
     uint8_t *d = e->dev.alloc(out_off + count);
@@ -970,44 +1000,58 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     // Tile status, block tiles and results start zeroed (contiguous).
     ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");
-    // Grid inputs: the data blocks found through the index blocks, the header
-    // checks of every input block in stream order (cheap), and the blocks
-    // staged from storage validated (AEGIS, latency-bound) on the side
-    // stream concurrently with the compaction; joined before the results.
-    if (ok && grid_mode && n_checks) {
-        ok = launch_grid_resolve(d_resolve, (uint32_t)resolve.size(), (uint64_t *)(uintptr_t)dev_seg,
-                                 d_checks, grid0->base, grid0->block_count, e->block_size, d_res,
-                                 s) == 0 &&
-             launch_grid_checks(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
-                                d_res, e->block_size, s) == 0;
+    if (grid_mode) {
+        // Pipelined: the front (input data blocks found through their index
+        // blocks, merge, bodies, index block addresses) on the engine stream;
+        // the tail (chains, index blocks, input checks, results) on a tail
+        // stream. The input checks read blocks earlier batches wrote, so they
+        // wait for every earlier tail; nothing else of the tail does.
+        if (ok && !resolve.empty())
+            ok = launch_grid_resolve(d_resolve, (uint32_t)resolve.size(), (uint64_t *)(uintptr_t)dev_seg, d_checks,
+                                     grid0->base, grid0->block_count, e->block_size, d_res, s) == 0;
+        if (ok && count)
+            ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+        if (ok && count)
+            ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
+                                     e->masks, d_splits, s, mark_cb, b) == 0;
+        const int ti = e->next_tail;
+        e->next_tail = (e->next_tail + 1) % tbc_engine::kTails;
+        hipStream_t T = e->tail[ti];
         b->fork = take_event(e);
-        b->join = take_event(e);
-        ok = ok && b->fork && b->join && hipEventRecord(b->fork, s) == hipSuccess &&
-             hipStreamWaitEvent(e->side, b->fork, 0) == hipSuccess &&
-             launch_grid_validate(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
-                                  d_res, e->block_size, e->side) == 0 &&
-             hipEventRecord(b->join, e->side) == hipSuccess;
-    }
-    if (grid_mode && n_checks) {
-        debug_stage(e->side, "grid_validate(side)");
+        ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
+        b->mark_stream = T;
+        mark_cb(b, "tail_wait");
+        if (ok && count)
+            ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
+                                    e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
+        // Outputs written by the engine are trusted like the reference's grid
+        // cache entries (grid.zig:802-841).
+        if (ok) ok = launch_grid_mark((const JobDesc *)d_in, (int)count, grid0->verified, T) == 0;
+        for (int o = 0; ok && o < tbc_engine::kTails; o++)
+            if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
+        if (ok && n_checks)
+            ok = launch_grid_expect(d_resolve, (uint32_t)resolve.size(), d_checks, T) == 0 &&
+                 launch_grid_validate(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in,
+                                      (int)count, d_res, e->block_size, T) == 0 &&
+                 launch_grid_checks(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
+                                    d_res, e->block_size, T) == 0;
         mark_cb(b, "grid_check");
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+    } else {
+        if (ok && count)
+            ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+        if (ok && count)
+            ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos,
+                               d_status, e->masks, d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0,
+                               maybe_sparse, s, mark_cb, b) == 0;
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     }
-    if (ok && count)
-        ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile,
-                          d_order, d_res, s, mark_cb, b) == 0;
-    if (ok && count)
-        ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
-                           d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0, maybe_sparse, s, mark_cb,
-                           b) == 0;
-    // Outputs written by the engine are trusted like the reference's grid
-    // cache entries (grid.zig:802-841).
-    if (ok && grid_mode) ok = launch_grid_mark((const JobDesc *)d_in, (int)count, grid0->verified, s) == 0;
-    if (ok && b->join) ok = hipStreamWaitEvent(s, b->join, 0) == hipSuccess;
-    ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
-    ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     if (!ok) {
-        hipStreamSynchronize(s);
-        hipStreamSynchronize(e->side);
+        tbc_synchronize(e);
         tbc_batch_release(b);
         return TBC_ERR_DEVICE;
     }
@@ -1104,7 +1148,6 @@ void tbc_batch_release(tbc_batch *b) {
         if (b->marks[m]) e->event_pool.push_back(b->marks[m]);
     if (b->done) e->event_pool.push_back(b->done);
     if (b->fork) e->event_pool.push_back(b->fork);
-    if (b->join) e->event_pool.push_back(b->join);
     if (b->h_results) {
         // LIFO release restores the arena tops; otherwise reclaim when idle.
         if (e->dev.live) e->dev.live--;

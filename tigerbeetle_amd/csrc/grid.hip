@@ -11,6 +11,8 @@
 //   k_grid_resolve  finds every input data block through its table's index
 //                   block (address, checksum) and fills the merge's segment
 //                   table — the host only knows TableInfos, as Compaction does;
+//   k_grid_expect   reads their expected checksums from the index blocks
+//                   once the batches that wrote them have sealed them;
 //   k_grid_check    applies read_block_from_cache's checks plus the header
 //                   fields the iterators assert, to every input block (cheap);
 //   k_grid_validate (aegis.hip) runs read_block_validate on the blocks staged
@@ -41,8 +43,6 @@ __global__ __launch_bounds__(256) void k_grid_resolve(const ResolveItem *items, 
     const ResolveItem it = items[i];
     const uint8_t *idx = (const uint8_t *)(uintptr_t)it.index_ptr;
     uint64_t address = gld<uint64_t>(idx + it.addr_off + 8 * it.k);
-    const uint64_t ck_lo = gld<uint64_t>(idx + it.cks_off + 32 * it.k);
-    const uint64_t ck_hi = gld<uint64_t>(idx + it.cks_off + 32 * it.k + 8);
     uint64_t blk = (uint64_t)(uintptr_t)grid_base + (address - 1) * block_size;
     if (address == 0 || address > grid_blocks) {
         grid_error(&res[it.job].block_error, 7u);
@@ -53,13 +53,23 @@ __global__ __launch_bounds__(256) void k_grid_resolve(const ResolveItem *items, 
     InputCheck c;
     c.ptr = blk;
     c.address = address;
-    c.checksum[0] = ck_lo;
-    c.checksum[1] = ck_hi;
+    c.checksum[0] = c.checksum[1] = 0; // k_grid_expect (the index block may not be sealed yet)
     c.value_count = it.value_count;
     c.job = it.job;
     c.kind = 5; // BlockType.data
     c.pad = 0;
     checks[it.check] = c;
+}
+
+// The expected checksum of every input data block, TableIndex.data_checksums[k]:
+// read once the batches that wrote the index blocks have sealed them.
+__global__ __launch_bounds__(256) void k_grid_expect(const ResolveItem *items, uint32_t count, InputCheck *checks) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const ResolveItem it = items[i];
+    const uint8_t *idx = (const uint8_t *)(uintptr_t)it.index_ptr;
+    checks[it.check].checksum[0] = gld<uint64_t>(idx + it.cks_off + 32 * it.k);
+    checks[it.check].checksum[1] = gld<uint64_t>(idx + it.cks_off + 32 * it.k + 8);
 }
 
 // One thread per trusted input block (index and data; blocks staged from
@@ -98,6 +108,13 @@ int launch_grid_resolve(const ResolveItem *d_items, uint32_t count, uint64_t *d_
     if (!count) return 0;
     hipLaunchKernelGGL(k_grid_resolve, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_items, count,
                        d_seg_ptr, d_checks, grid_base, grid_blocks, block_size, d_results);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_grid_expect(const ResolveItem *d_items, uint32_t count, InputCheck *d_checks, void *stream) {
+    if (!count) return 0;
+    hipLaunchKernelGGL(k_grid_expect, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_items, count,
+                       d_checks);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

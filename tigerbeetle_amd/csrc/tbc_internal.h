@@ -204,6 +204,15 @@ int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uin
 int launch_grid_resolve(const ResolveItem *d_items, uint32_t count, uint64_t *d_seg_ptr, InputCheck *d_checks,
                         const uint8_t *grid_base, uint64_t grid_blocks, uint32_t block_size, JobResultDev *d_results,
                         void *stream);
+int launch_grid_expect(const ResolveItem *d_items, uint32_t count, InputCheck *d_checks, void *stream);
+int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks,
+                        uint32_t *d_ready, const JobResultDev *d_results, const uint64_t *d_status,
+                        const uint64_t *d_masks, const SplitDesc *d_splits, void *stream,
+                        void (*mark)(void *, const char *), void *mark_ctx);
+int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
+                       JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
+                       const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
+                       void *stream, void (*mark)(void *, const char *), void *mark_ctx);
 int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t *d_verified, const JobDesc *d_jobs,
                        int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
 int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_verified, const JobDesc *d_jobs,
