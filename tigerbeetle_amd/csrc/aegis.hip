@@ -1280,7 +1280,13 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
     const uint32_t waves = (total_dblocks + 1) / 2;
     if (total_dblocks) {
         if (waves <= 1024) { // latency regime: one chain per SIMD, round keys by VALU lane moves
-            const uint32_t c = waves_per_block(waves);
+            // A chain workgroup holds a whole CU's LDS (the tables), so
+            // concurrent tails share the chip by CUs: pack four chains per
+            // CU (one per SIMD), more once a batch alone would take over a
+            // third of the CUs.
+            uint32_t c = (waves + 85) / 86;
+            c = c < 4 ? 4 : (c > 16 ? 16 : (c + 3) & ~3u);
+            if (c > waves) c = waves;
             hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
                                d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
                                d_block_tile, d_splits, c, d_ready);
