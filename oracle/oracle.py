@@ -98,6 +98,8 @@ def lib():
         _lib.tbo_compact.argtypes = [ctypes.POINTER(Job)]
         _lib.tbo_compact.restype = ctypes.c_int
         _lib.tbo_key.argtypes = [ctypes.POINTER(Tree), ctypes.c_void_p, ctypes.c_void_p]
+        _lib.tbo_tombstone.argtypes = [ctypes.POINTER(Tree), ctypes.c_void_p]
+        _lib.tbo_tombstone_from_key.argtypes = [ctypes.POINTER(Tree), ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
 

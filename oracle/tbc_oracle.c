@@ -302,6 +302,20 @@ int tbo_tombstone(const tbo_tree *t, const uint8_t *v) {
     return (rd64(v + t->timestamp_offset) & TOMBSTONE_BIT) != 0;
 }
 
+/* tombstone_from_key (composite_key.zig:64-73): the value {field = key >> 64,
+ * timestamp = key | tombstone_bit, padding = 0} of a composite tree; returns
+ * TBO_ERR_INVALID if the key's timestamp already has the tombstone bit. */
+int tbo_tombstone_from_key(const tbo_tree *t, const uint64_t k[4], uint8_t *v) {
+    if (t->key_kind != TBO_KEY_COMPOSITE_U64 && t->key_kind != TBO_KEY_COMPOSITE_U128) return TBO_ERR_INVALID;
+    if (k[0] & TOMBSTONE_BIT) return TBO_ERR_INVALID;
+    memset(v, 0, t->value_size);
+    const uint64_t ts = k[0] | TOMBSTONE_BIT;
+    memcpy(v, &k[1], 8);
+    if (t->key_kind == TBO_KEY_COMPOSITE_U128) memcpy(v + 8, &k[2], 8);
+    memcpy(v + t->timestamp_offset, &ts, 8);
+    return TBO_OK;
+}
+
 static inline int key_cmp(const uint64_t a[4], const uint64_t b[4]) {
     for (int i = 3; i >= 0; i--) {
         if (a[i] < b[i]) return -1;

@@ -202,6 +202,29 @@ def test_sort_values_low_limbs_in_order(engine, oracle_lib):
         assert np.array_equal(got, want), spec.name
 
 
+@pytest.mark.parametrize("name", ["accounts.user_data_64", "transfers.debit_account_id"])
+def test_sort_composite_key_cases(engine, oracle_lib, name):
+    """composite_key.zig:88-124's cases on the device's key_from_value: the
+    sort orders (1,100) < (1,101) < (2,99), and a tombstone (1, 100|bit) has
+    the key of (1,100) (equal keys keep their put order)."""
+    spec = trees.BY_NAME[name]
+    bit = 1 << 63
+    cases = [(2, 99), (1, 101), (1, 100 | bit), (1, 100), (1, 101 | bit)]
+    vals = np.zeros((len(cases), spec.value_size), dtype=np.uint8)
+    for i, (field, ts) in enumerate(cases):
+        vals[i, :8].view(np.uint64)[0] = field
+        vals[i, spec.timestamp_offset:spec.timestamp_offset + 8].view(np.uint64)[0] = np.uint64(ts)
+    t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                        spec.value_count_max, 1 << 20)
+    want = oracle_lib.sort_values(t, vals)
+    order = [(int(w[:8].view(np.uint64)[0]), int(w[spec.timestamp_offset:spec.timestamp_offset + 8]
+                                                  .view(np.uint64)[0])) for w in want]
+    assert order == [(1, 100 | bit), (1, 100), (1, 101), (1, 101 | bit), (2, 99)]
+    buf = engine.upload(vals, pad=16)
+    engine.sort_values(spec, buf, len(cases))
+    assert np.array_equal(buf.download(vals.nbytes).reshape(vals.shape), want)
+
+
 def test_immutable_compaction_after_device_sort(engine, oracle_lib):
     """Bar end: sort the mutable table on the device, then compact it as the
     immutable table A (tree.zig:979-999 -> compaction.zig:483-559)."""

@@ -52,25 +52,38 @@ def test_checksum_simple_fuzzing(oracle_lib):
 
 @pytest.mark.parametrize("kind", [KEY_COMPOSITE_U64, KEY_COMPOSITE_U128])
 def test_composite_key(oracle_lib, kind):
-    # composite_key.zig:88-119 through the oracle's key_from_value.
+    # composite_key.zig:88-124 (composite_key_test, all four blocks) through
+    # the oracle's key_from_value / tombstone / tombstone_from_key.
+    import ctypes
     spec = next(t for t in trees.TREES if t.key_kind == kind)
     t = oracle_tree(oracle_lib, spec, trees.BLOCK_SIZE)
-    rng = np.random.default_rng(0)
+    L = oracle_lib.lib()
 
-    def key(field, ts):
-        limbs = [np.array([ts], dtype=np.uint64), np.array([field], dtype=np.uint64)]
-        if kind == KEY_COMPOSITE_U128:
-            limbs.append(np.array([0], dtype=np.uint64))
-        v = workloads.values_from_keys(spec, limbs, np.array([False]), rng)[0]
-        v.view(np.uint64)[spec.timestamp_offset // 8] = np.uint64(ts)
-        import ctypes
+    def value(field, ts):
+        v = np.zeros(spec.value_size, dtype=np.uint8)
+        v[:8].view(np.uint64)[0] = field
+        v[spec.timestamp_offset:spec.timestamp_offset + 8].view(np.uint64)[0] = np.uint64(ts)
+        return v
+
+    def key(v):
         out = (ctypes.c_uint64 * 4)()
-        oracle_lib.lib().tbo_key(ctypes.byref(t), v.ctypes.data, out)
+        L.tbo_key(ctypes.byref(t), v.ctypes.data, out)
         return sum(int(out[i]) << (64 * i) for i in range(4))
 
-    assert key(1, 100) < key(1, 101)
-    assert key(1, 100) < key(2, 99)
-    assert key(1, 100 | (1 << 63)) == key(1, 100)
+    bit = 1 << 63
+    assert key(value(1, 100)) < key(value(1, 101))                    # :89-93
+    assert key(value(1, 100)) < key(value(2, 99))                     # :95-99
+    assert key(value(1, 100 | bit)) == key(value(1, 100))             # :101-111
+    k = key(value(1, 100))                                            # :113-118
+    limbs = (ctypes.c_uint64 * 4)(*[(k >> (64 * i)) & ((1 << 64) - 1) for i in range(4)])
+    tomb = np.zeros(spec.value_size, dtype=np.uint8)
+    assert L.tbo_tombstone_from_key(ctypes.byref(t), limbs, tomb.ctypes.data) == 0
+    assert L.tbo_tombstone(ctypes.byref(t), tomb.ctypes.data) == 1
+    assert int(tomb[spec.timestamp_offset:spec.timestamp_offset + 8].view(np.uint64)[0]) == 100 | bit
+    assert int(tomb[:8].view(np.uint64)[0]) == 1 and key(tomb) == k
+    # tombstone_from_key asserts the key's timestamp has no tombstone bit (:67)
+    bad = (ctypes.c_uint64 * 4)(100 | bit, 1, 0, 0)
+    assert L.tbo_tombstone_from_key(ctypes.byref(t), bad, tomb.ctypes.data) != 0
 
 
 def test_tree_layouts_match_survey(oracle_lib):

@@ -684,6 +684,29 @@ __device__ __forceinline__ bool sparse_job(const JobDesc &j, const JobResultDev 
     return res[j.job_index].value_count * 4 < (uint64_t)(j.a.n + j.b.n);
 }
 
+// Copy `count` staged values (source and destination pointers in LDS), 16
+// bytes per lane: eight loads in flight per lane before their stores (a
+// load-store loop keeps one, and is latency-bound).
+__device__ __forceinline__ void copy_staged(const uint64_t *src, const uint64_t *dst, uint32_t count,
+                                            uint32_t cpv_log) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t total = count << cpv_log;
+    const uint32_t qmask = (1u << cpv_log) - 1;
+    for (uint32_t c0 = 0; c0 < total; c0 += 64 * 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t c = c0 + lane + 64 * u;
+            if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)src[c >> cpv_log] + 16 * (c & qmask));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t c = c0 + lane + 64 * u;
+            if (c < total) gst<u32x4>((uint8_t *)(uintptr_t)dst[c >> cpv_log] + 16 * (c & qmask), v[u]);
+        }
+    }
+}
+
 __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint32_t cnt, const uint64_t *status,
                                              const uint64_t *masks, const uint32_t *block_tile,
                                              const SplitDesc *splits, uint8_t *body, uint32_t *prog,
@@ -727,10 +750,7 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t c = lane; c < (pend << cpv_log); c += 64) {
-            const uint32_t e = c >> cpv_log, q = c & ((1u << cpv_log) - 1);
-            gst<u32x4>((uint8_t *)(uintptr_t)st_dst[e] + 16 * q, gld<u32x4>((const uint8_t *)(uintptr_t)st_src[e] + 16 * q));
-        }
+        copy_staged(st_src, st_dst, pend, cpv_log);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -991,12 +1011,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            for (uint32_t c = lane; c < (ns << cpv_log); c += 64) {
-                const uint32_t e = c >> cpv_log, q = c & ((1u << cpv_log) - 1);
-                const uint8_t *src = (const uint8_t *)(uintptr_t)s_src[wv][e];
-                uint8_t *dst = (uint8_t *)(uintptr_t)s_dst[wv][e];
-                gst<u32x4>(dst + 16 * q, gld<u32x4>(src + 16 * q));
-            }
+            copy_staged(s_src[wv], s_dst[wv], ns, cpv_log);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }

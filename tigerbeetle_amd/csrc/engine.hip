@@ -221,6 +221,10 @@ struct tbc_batch {
     hipEvent_t done = nullptr;
     hipEvent_t fork = nullptr;                          // end of the front (pipelined batches)
     hipStream_t mark_stream = nullptr;                  // where mark_cb records
+    // A batch split into job groups (tbc_compaction_submit): the groups'
+    // batches, and per job its group and index there.
+    std::vector<tbc_batch *> children;
+    std::vector<std::pair<uint32_t, uint32_t>> job_map;
     hipEvent_t marks[kMaxMarks] = {};
     const char *mark_names[kMaxMarks] = {};
     int nmarks = 0;
@@ -722,7 +726,8 @@ tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment
     return st;
 }
 
-tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
+static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, bool pipeline,
+                              tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     hipSetDevice(e->device);
@@ -1039,6 +1044,28 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         mark_cb(b, "grid_check");
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+    } else if (pipeline) {
+        // A group of a split batch: front (merge + bodies) on the engine
+        // stream, chains and index blocks on a tail stream, so the group's
+        // chains run beside the next group's merge and body assembly.
+        if (ok && count)
+            ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+        if (ok && count)
+            ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
+                                     e->masks, d_splits, s, mark_cb, b) == 0;
+        const int ti = e->next_tail;
+        e->next_tail = (e->next_tail + 1) % tbc_engine::kTails;
+        hipStream_t T = e->tail[ti];
+        b->fork = take_event(e);
+        ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
+        b->mark_stream = T;
+        mark_cb(b, "tail_wait");
+        if (ok && count)
+            ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
+                                    e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
     } else {
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
@@ -1059,6 +1086,67 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     return TBC_OK;
 }
 
+// Above this many chain waves a batch is in the throughput regime (aegis.hip
+// kFusedMaxChainWaves): it is split into job groups that pipeline (each
+// group's chains beside the next group's merge and bodies).
+constexpr uint64_t kGroupMinChainWaves = 2048;
+constexpr uint32_t kMaxGroups = 6;
+
+tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
+    if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
+    static const bool no_groups = getenv("TBC_NO_GROUPS") != nullptr; // A/B measurement only
+    uint32_t groups = 1;
+    std::vector<uint64_t> n(count, 0);
+    if (!no_groups && count >= 2 && !(jobs_in[0].flags & (TBC_COMPACTION_GRID | TBC_COMPACTION_VALUES_ONLY))) {
+        uint64_t waves = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            const tbc_compaction &c = jobs_in[i];
+            Layout L;
+            if (!compute_layout(&c.tree, e->block_size, &L) || (c.segment_count_a && !c.segments_a) ||
+                (c.segment_count_b && !c.segments_b))
+                return submit_impl(e, jobs_in, count, false, out); // reports the error
+            for (uint32_t k = 0; k < c.segment_count_a; k++) n[i] += c.segments_a[k].count;
+            for (uint32_t k = 0; k < c.segment_count_b; k++) n[i] += c.segments_b[k].count;
+            waves += (n[i] + L.vcm - 1) / L.vcm / 2;
+        }
+        static const uint32_t max_groups = getenv("TBC_GROUPS") ? (uint32_t)atoi(getenv("TBC_GROUPS")) : kMaxGroups;
+        if (waves > kGroupMinChainWaves && max_groups > 1) groups = std::min<uint32_t>(max_groups, count);
+    }
+    if (groups == 1) return submit_impl(e, jobs_in, count, false, out);
+    // Contiguous groups of about equal input (job order kept inside a group).
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < count; i++) total += n[i];
+    tbc_batch *parent = new (std::nothrow) tbc_batch();
+    if (!parent) return TBC_ERR_OUT_OF_MEMORY;
+    parent->engine = e;
+    parent->count = count;
+    parent->job_map.resize(count);
+    uint32_t first = 0;
+    uint64_t acc = 0;
+    for (uint32_t g = 0; g < groups && first < count; g++) {
+        uint32_t last = first + 1;
+        acc += n[first];
+        const uint64_t goal = total * (g + 1) / groups;
+        while (last < count && (count - last) > (groups - g - 1) && acc + n[last] / 2 <= goal) acc += n[last++];
+        if (g == groups - 1) {
+            while (last < count) acc += n[last++];
+        }
+        tbc_batch *child = nullptr;
+        const tbc_status st = submit_impl(e, jobs_in + first, last - first, true, &child);
+        if (st != TBC_OK) {
+            for (auto it = parent->children.rbegin(); it != parent->children.rend(); ++it) tbc_batch_release(*it);
+            delete parent;
+            return st;
+        }
+        for (uint32_t i = first; i < last; i++)
+            parent->job_map[i] = {(uint32_t)parent->children.size(), i - first};
+        parent->children.push_back(child);
+        first = last;
+    }
+    *out = parent;
+    return TBC_OK;
+}
+
 static tbc_status batch_finish(tbc_batch *b) {
     b->complete = true;
     b->result = TBC_OK;
@@ -1071,9 +1159,22 @@ static tbc_status batch_finish(tbc_batch *b) {
     return b->result;
 }
 
+static tbc_status parent_finish(tbc_batch *b, bool wait) {
+    tbc_status res = TBC_OK;
+    for (tbc_batch *c : b->children) {
+        const tbc_status st = wait ? tbc_batch_wait(c) : tbc_batch_poll(c);
+        if (st == TBC_PENDING) return TBC_PENDING;
+        if (st != TBC_OK && res == TBC_OK) res = st;
+    }
+    b->complete = true;
+    b->result = res;
+    return res;
+}
+
 tbc_status tbc_batch_poll(tbc_batch *b) {
     if (!b) return TBC_ERR_INVALID_ARGUMENT;
     if (b->complete) return b->result;
+    if (!b->children.empty()) return parent_finish(b, false);
     hipSetDevice(b->engine->device);
     hipError_t q = hipEventQuery(b->done);
     if (q == hipErrorNotReady) return TBC_PENDING;
@@ -1089,6 +1190,7 @@ tbc_status tbc_batch_poll(tbc_batch *b) {
 tbc_status tbc_batch_wait(tbc_batch *b) {
     if (!b) return TBC_ERR_INVALID_ARGUMENT;
     if (b->complete) return b->result;
+    if (!b->children.empty()) return parent_finish(b, true);
     hipSetDevice(b->engine->device);
     // Poll like the adapter's event loop would (tbc_batch_poll), instead of a
     // blocking hipEventSynchronize whose OS wake-up adds milliseconds of jitter.
@@ -1108,6 +1210,10 @@ tbc_status tbc_batch_result(tbc_batch *b, uint32_t index, tbc_compaction_result 
                             uint32_t table_info_capacity) {
     if (!b || !out || index >= b->count) return TBC_ERR_INVALID_ARGUMENT;
     if (!b->complete) return TBC_PENDING;
+    if (!b->children.empty()) {
+        const auto m = b->job_map[index];
+        return tbc_batch_result(b->children[m.first], m.second, out, table_infos, table_info_capacity);
+    }
     if (b->result == TBC_ERR_DEVICE) return TBC_ERR_DEVICE;
     const JobResultDev &r = b->h_results[index];
     out->value_count = r.value_count;
@@ -1127,6 +1233,33 @@ tbc_status tbc_batch_kernel_times(tbc_batch *b, const char **names, double *us, 
                                   uint32_t *out_count) {
     if (!b || !out_count) return TBC_ERR_INVALID_ARGUMENT;
     if (!b->complete) return TBC_PENDING;
+    if (!b->children.empty()) { // summed over the groups, by name
+        std::vector<const char *> nm;
+        std::vector<double> t;
+        for (tbc_batch *c : b->children) {
+            const char *cn[kMaxMarks];
+            double cu[kMaxMarks];
+            uint32_t k = 0;
+            const tbc_status st = tbc_batch_kernel_times(c, cn, cu, kMaxMarks, &k);
+            if (st != TBC_OK) return st;
+            for (uint32_t i = 0; i < k; i++) {
+                size_t j = 0;
+                while (j < nm.size() && strcmp(nm[j], cn[i]) != 0) j++;
+                if (j == nm.size()) {
+                    nm.push_back(cn[i]);
+                    t.push_back(0.0);
+                }
+                t[j] += cu[i];
+            }
+        }
+        uint32_t n = 0;
+        for (; n < nm.size() && n < capacity; n++) {
+            if (names) names[n] = nm[n];
+            if (us) us[n] = t[n];
+        }
+        *out_count = n;
+        return TBC_OK;
+    }
     uint32_t n = 0;
     for (int m = 1; m < b->nmarks && n < capacity; m++) {
         float ms = 0;
@@ -1141,6 +1274,11 @@ tbc_status tbc_batch_kernel_times(tbc_batch *b, const char **names, double *us, 
 
 void tbc_batch_release(tbc_batch *b) {
     if (!b) return;
+    if (!b->children.empty()) { // reverse order: the groups' arena regions are a stack
+        for (auto it = b->children.rbegin(); it != b->children.rend(); ++it) tbc_batch_release(*it);
+        delete b;
+        return;
+    }
     tbc_engine *e = b->engine;
     hipSetDevice(e->device);
     if (!b->complete && b->done) hipEventSynchronize(b->done);

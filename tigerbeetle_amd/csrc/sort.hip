@@ -125,8 +125,15 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
         uint64_t k[3], kn[3];
         row_keys(S, li, in, k, kn);
         if (!in) continue;
-        for (uint32_t q = 0; q < S.vs; q += 16)
-            gst<u32x4>(S.copy + (size_t)li * S.vs + q, gld<u32x4>(S.values + (size_t)li * S.vs + q));
+        for (uint32_t b = 0; b < S.vs; b += 128) { // up to 8 loads in flight before their stores
+            u32x4 v[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                if (b + 16 * q < S.vs) v[q] = gld<u32x4>(S.values + (size_t)li * S.vs + b + 16 * q);
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                if (b + 16 * q < S.vs) gst<u32x4>(S.copy + (size_t)li * S.vs + b + 16 * q, v[q]);
+        }
         for (uint32_t l = 0; l < S.kl; l++) {
             o[l] |= k[l];
             a[l] &= k[l];

@@ -11,13 +11,15 @@ export TMPDIR=/tmp
 TAG=${1:?usage: profile.sh TAG}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--steps 10 --warmup 3"
+CFG=${CONFIG:-2}
+ARGS="--config $CFG --steps 10 --warmup 3"
+SHORT="--config $CFG --steps 3 --warmup 1"
 timeout -k 10 240 python -u bench.py $ARGS > $OUT/bench.log 2>&1
 tail -1 $OUT/bench.log > $OUT/bench.json
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 -u bench.py $ARGS --no-cpu-baseline > $OUT/trace.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/fetch.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/write.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/sq -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/sq.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 -u bench.py $SHORT --no-cpu-baseline > $OUT/fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 -u bench.py $SHORT --no-cpu-baseline > $OUT/write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/sq -o run -- python3 -u bench.py $SHORT --no-cpu-baseline > $OUT/sq.log 2>&1
 md5sum tigerbeetle_amd/libtbc.so > $OUT/lib.md5
 echo PROFILE_OK
 # Kernel traces of the other BASELINE configs (no PMC passes).
