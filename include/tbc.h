@@ -277,8 +277,18 @@ tbc_status tbc_sort_values_batch(tbc_engine *engine, const tbc_sort_job *jobs, u
  * 16-byte aligned) sorted by key_from_value in the merge direction, possibly
  * with repeated keys; the merged values (one per key: the first of the
  * winning stream's run) are written to `out_values` (device, capacity = the
- * streams' total) and their number to *out_count. Synchronous. */
+ * streams' total). tbc_kway_merge_submit enqueues the merge and returns at
+ * once (the scan's iterator polls it like a grid read, src/lsm/scan_tree.zig);
+ * the merged count is read with tbc_kway_count once tbc_kway_poll returns
+ * TBC_OK. tbc_kway_merge is the blocking form (tests, tools). */
 #define TBC_KWAY_STREAMS_MAX 64u
+typedef struct tbc_kway tbc_kway;
+tbc_status tbc_kway_merge_submit(tbc_engine *engine, const tbc_tree *tree, const tbc_segment *streams,
+                                 uint32_t stream_count, uint32_t descending, void *out_values, tbc_kway **out_merge);
+tbc_status tbc_kway_poll(tbc_kway *merge);
+tbc_status tbc_kway_wait(tbc_kway *merge);
+tbc_status tbc_kway_count(const tbc_kway *merge, uint64_t *out_count);
+void tbc_kway_release(tbc_kway *merge);
 tbc_status tbc_kway_merge(tbc_engine *engine, const tbc_tree *tree, const tbc_segment *streams, uint32_t stream_count,
                           uint32_t descending, void *out_values, uint64_t *out_count);
 

@@ -77,3 +77,31 @@ def test_kway_empty(engine):
     spec = trees.BY_NAME["transfers.id"]
     assert len(_run(engine, spec, [], False)) == 0
     assert len(_run(engine, spec, [np.zeros((0, 32), np.uint8)] * 3, True)) == 0
+
+
+def test_kway_async_handles(engine):
+    """tbc_kway_merge_submit returns at once; two merges in flight, polled to
+    completion, give the blocking call's bytes and counts."""
+    spec = trees.BY_NAME["transfers.id"]
+    rng = np.random.default_rng(7)
+    limbs = workloads.unique_sorted_keys(spec, 50_000, rng)
+    streams = []
+    for _ in range(5):
+        idx = np.sort(rng.integers(0, 50_000, size=int(rng.integers(1000, 20_000))))
+        streams.append(workloads.values_from_keys(spec, [l[idx] for l in limbs], np.zeros(len(idx), bool), rng))
+    bufs = [engine.upload(s) for s in streams]
+    segs = [(b.ptr, len(s)) for b, s in zip(bufs, streams)]
+    total = sum(len(s) for s in streams)
+    outs = [engine.alloc(total * 32) for _ in range(2)]
+    hs = [engine.kway_merge_submit(spec, segs, outs[0]), engine.kway_merge_submit(spec, segs[::-1], outs[1])]
+    import time
+    deadline = time.time() + 30
+    while not all(h.poll() for h in hs):
+        assert time.time() < deadline
+    counts = [h.count() for h in hs]
+    for h in hs[::-1]:
+        h.release()
+    want0, want1 = _run(engine, spec, streams, False), _run(engine, spec, streams[::-1], False)
+    assert counts == [len(want0), len(want1)]
+    assert np.array_equal(outs[0].download(counts[0] * 32).reshape(-1, 32), want0)
+    assert np.array_equal(outs[1].download(counts[1] * 32).reshape(-1, 32), want1)

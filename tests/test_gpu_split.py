@@ -49,18 +49,25 @@ def _run_rank(name, rank, world, exchange):
     with Engine(device=0, block_size=bs) as eng:
         lay = eng.layout(spec)
         vcm, dbcm = lay.block_value_count_max, lay.data_block_count_max
+        # Splitters from the inputs' data-block first keys (index blocks),
+        # cuts from one boundary block per side; then this rank stages only
+        # its own range of A and of B (per-rank staging).
+        b_all = np.concatenate(ji.b_tables)
+        side_a = split.BlockedSide.from_values(workloads.keys_of(ji.a_values, spec), len(ji.a_values), vcm)
+        side_b = split.BlockedSide.from_values(workloads.keys_of(b_all, spec), len(b_all), vcm)
+        cuts = split.block_cuts(side_a, side_b, split.block_splitters(side_a, side_b, world))
+        (a0, b0), (a1, b1) = cuts[rank], cuts[rank + 1]
+        a_mine, b_mine = ji.a_values[a0:a1], b_all[b0:b1]
         if ji.a_immutable:
-            abuf = eng.upload(ji.a_values) if len(ji.a_values) else None
-            segs_a = [(abuf.ptr, len(ji.a_values))] if abuf else []
+            abuf = eng.upload(a_mine) if len(a_mine) else None
+            segs_a = [(abuf.ptr, len(a_mine))] if abuf else []
         else:
-            abuf, segs_a = stage_blocks(eng, [workloads.split_blocks(ji.a_values, vcm)], spec.value_size, bs)
-        bbuf, segs_b = stage_blocks(eng, [workloads.split_blocks(t, vcm) for t in ji.b_tables], spec.value_size, bs)
+            abuf, segs_a = stage_blocks(eng, [workloads.split_blocks(a_mine, vcm)], spec.value_size, bs)
+        bbuf, segs_b = stage_blocks(eng, [workloads.split_blocks(b_mine, vcm)], spec.value_size, bs)
+        assert split.staged_bytes(cuts, rank, spec.value_size) == a_mine.nbytes + b_mine.nbytes
         job = Job(spec, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48,
                   np.asarray(addrs, dtype=np.uint64), None)
-        b_all = np.concatenate(ji.b_tables)
-        cuts = split.split_points(workloads.keys_of(ji.a_values, spec), len(ji.a_values),
-                                  workloads.keys_of(b_all, spec), len(b_all), world)
-        res = split.compact_split(eng, job, cuts, exchange, rank)
+        res = split.compact_split(eng, job, cuts, exchange, rank, staged=True)
         whole = run_oracle(oracle, ji, bs, addrs)
         assert whole.status == 0
         t0, t1 = res.tables

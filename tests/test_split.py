@@ -90,6 +90,25 @@ def _cuts(spec, ji, world):
     return split.split_points(la, len(ji.a_values), lb, len(b), world)
 
 
+def _sides(spec, ji, reads=None):
+    """A and B as data blocks (first keys from the 'index blocks'); `reads`
+    collects every (side, block) whose keys are read."""
+    vcm = spec.layout(BS)["block_value_count_max"]
+    out = []
+    for name, vals in (("a", ji.a_values), ("b", _b_all(ji))):
+        side = split.BlockedSide.from_values(workloads.keys_of(vals, spec), len(vals), vcm)
+        if reads is not None:
+            inner = side.keys
+            side.keys = (lambda nm, f: (lambda j: (reads.append((nm, j)), f(j))[1]))(name, inner)
+        out.append(side)
+    return out
+
+
+def _block_cuts(spec, ji, world, reads=None):
+    a, b = _sides(spec, ji, reads)
+    return split.block_cuts(a, b, split.block_splitters(a, b, world))
+
+
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_split_points_never_split_a_key(case):
     spec, ji, _ = _inputs(case)
@@ -129,11 +148,40 @@ def test_plan_tables_edges():
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("world", [2, 3, 5, 8])
+def test_block_cuts_read_only_boundary_blocks(case, world):
+    """Per-rank staging: the cuts come from the data blocks' first keys plus
+    at most one block of A and one of B per splitter; no key straddles a
+    cut; every rank stages about its share (its range, whole-block slack)."""
+    spec, ji, _ = _inputs(case)
+    reads = []
+    cuts = _block_cuts(spec, ji, world, reads)
+    assert len(reads) <= 2 * (world - 1)
+    b = _b_all(ji)
+    ka = [tuple(int(l[i]) for l in reversed(workloads.keys_of(ji.a_values, spec))) for i in range(len(ji.a_values))]
+    kb = [tuple(int(l[i]) for l in reversed(workloads.keys_of(b, spec))) for i in range(len(b))]
+    for (a0, b0), (a1, b1) in zip(cuts, cuts[1:]):
+        assert a0 <= a1 and b0 <= b1
+    for p in range(1, world):
+        a_cut, b_cut = cuts[p]
+        left = ka[:a_cut] + kb[:b_cut]
+        right = ka[a_cut:] + kb[b_cut:]
+        if left and right:
+            assert max(left) < min(right)
+    n, vs = len(ji.a_values) + len(b), spec.value_size
+    vcm = spec.layout(BS)["block_value_count_max"]
+    assert sum(split.staged_bytes(cuts, p, vs) for p in range(world)) == n * vs
+    for p in range(world):
+        assert split.staged_bytes(cuts, p, vs) <= (n // world + 2 * vcm * (world > 1) + 2 * vcm) * vs
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
 @pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
-def test_split_job_equals_unsplit_job(oracle_lib, case, world):
+@pytest.mark.parametrize("method", ["merge_path", "blocks"])
+def test_split_job_equals_unsplit_job(oracle_lib, case, world, method):
     spec, ji, addrs = _inputs(case)
     whole = _compact(oracle_lib, spec, ji.a_values, ji.a_immutable, _b_all(ji), ji.drop_tombstones, addrs)
-    cuts = _cuts(spec, ji, world)
+    cuts = _cuts(spec, ji, world) if method == "merge_path" else _block_cuts(spec, ji, world)
     surv = [_rank_phase1(oracle_lib, spec, ji, cuts, p) for p in range(world)]
     lay = spec.layout(BS)
     plan = split.plan_tables([len(s) for s in surv], lay["block_value_count_max"], lay["data_block_count_max"])
@@ -166,8 +214,10 @@ def _worker(rank, world, port, case, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
     spec, ji, addrs = _inputs(case)
-    cuts = _cuts(spec, ji, world)                   # identical on every rank, no communication
-    mine = _rank_phase1(oracle, spec, ji, cuts, rank)
+    reads = []
+    cuts = _block_cuts(spec, ji, world, reads)      # identical on every rank, no communication
+    assert len(reads) <= 2 * (world - 1)            # index keys + boundary blocks only
+    mine = _rank_phase1(oracle, spec, ji, cuts, rank)  # stages only [cuts[rank], cuts[rank+1])
     ex = split.TorchExchange(dist)
     lay = spec.layout(BS)
     plan = split.plan_tables(ex.all_gather_counts(len(mine)), lay["block_value_count_max"],

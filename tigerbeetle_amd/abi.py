@@ -146,6 +146,12 @@ _SIGNATURES = {
     "tbc_sort_values_batch": (ctypes.c_int, [_P, ctypes.POINTER(SortJob), ctypes.c_uint32]),
     "tbc_kway_merge": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.POINTER(Segment), ctypes.c_uint32,
                                       ctypes.c_uint32, _P, ctypes.POINTER(ctypes.c_uint64)]),
+    "tbc_kway_merge_submit": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.POINTER(Segment), ctypes.c_uint32,
+                                             ctypes.c_uint32, _P, ctypes.POINTER(_P)]),
+    "tbc_kway_poll": (ctypes.c_int, [_P]),
+    "tbc_kway_wait": (ctypes.c_int, [_P]),
+    "tbc_kway_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    "tbc_kway_release": (None, [_P]),
     "tbc_compaction_submit": (ctypes.c_int, [_P, ctypes.POINTER(Compaction), ctypes.c_uint32,
                                              ctypes.POINTER(_P)]),
     "tbc_batch_poll": (ctypes.c_int, [_P]),

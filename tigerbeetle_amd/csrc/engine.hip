@@ -122,6 +122,10 @@ struct tbc_engine {
     uint64_t *sort_status = nullptr;
     uint64_t sort_status_words = 0;
     uint32_t sort_epoch = 1;
+    // k-way merge scratch (level outputs, splits, masks, counts, descriptors):
+    // merges run in stream order, so one growable buffer serves them all.
+    uint8_t *kway_scratch = nullptr;
+    uint64_t kway_scratch_size = 0;
 };
 
 struct tbc_grid {
@@ -232,6 +236,18 @@ struct tbc_batch {
     tbc_status result = TBC_PENDING;
 };
 
+struct tbc_kway {
+    tbc_engine *engine = nullptr;
+    hipEvent_t done = nullptr;
+    uint32_t *h_count = nullptr; // pinned: the merged value count
+    uint64_t dev_top = 0, host_top = 0;
+    bool arena = false;
+    bool host_only = false; // only the pinned arena (device scratch is the engine's)
+    bool complete = false;
+    tbc_status result = TBC_OK;
+    uint64_t count = 0;
+};
+
 // TBC_DEBUG_SYNC=1 (tools only): wait up to 5 s for every stage of a batch
 // and name the one that does not finish.
 static void debug_stage(hipStream_t s, const char *name) {
@@ -336,6 +352,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (e->masks) hipFree(e->masks);
     if (e->sort_scratch) hipFree(e->sort_scratch);
     if (e->sort_status) hipFree(e->sort_status);
+    if (e->kway_scratch) hipFree(e->kway_scratch);
     for (int t = 0; t < tbc_engine::kTails; t++) {
         if (e->tail_ev[t]) hipEventDestroy(e->tail_ev[t]);
         if (e->tail[t]) hipStreamDestroy(e->tail[t]);
@@ -676,53 +693,255 @@ tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, ui
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
-tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams, uint32_t stream_count,
-                          uint32_t descending, void *out_values, uint64_t *out_count) {
+// Host image of kway.hip's KPair (kway_pair_bytes() checks the size).
+struct KPairHost {
+    uint64_t a, b, na, nb, out, n_out;
+    uint32_t tile_base, split_base, tiles_cap, pad;
+};
+
+tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams,
+                                 uint32_t stream_count, uint32_t descending, void *out_values, tbc_kway **out) {
     Layout L;
-    if (!e || !tree || !out_count || (stream_count && !streams) || stream_count > TBC_KWAY_STREAMS_MAX ||
-        !compute_layout(tree, e->block_size, &L) || ((uintptr_t)out_values & 15))
+    if (!e || !tree || !out || (stream_count && !streams) || stream_count > TBC_KWAY_STREAMS_MAX ||
+        !compute_layout(tree, e->block_size, &L) || ((uintptr_t)out_values & 15) ||
+        kway_pair_bytes() != sizeof(KPairHost))
         return TBC_ERR_INVALID_ARGUMENT;
-    *out_count = 0;
+    *out = nullptr;
     uint64_t n = 0;
-    // value pointers, then u32 prefix counts of values and of 256-value tiles
-    std::vector<uint64_t> tab(2 * (size_t)stream_count + 2, 0);
-    uint32_t *pre = (uint32_t *)(tab.data() + stream_count), *tile_pre = pre + stream_count + 1;
-    uint32_t tiles = 0;
     for (uint32_t s = 0; s < stream_count; s++) {
         if (streams[s].count && (!streams[s].values || ((uintptr_t)streams[s].values & 15)))
             return TBC_ERR_INVALID_ARGUMENT;
-        tab[s] = (uint64_t)(uintptr_t)streams[s].values;
-        pre[s] = (uint32_t)n;
-        tile_pre[s] = tiles;
         n += streams[s].count;
-        tiles += (streams[s].count + 255) / 256;
     }
     if (n >= 0x7fffffffull) return TBC_ERR_INVALID_ARGUMENT;
-    pre[stream_count] = (uint32_t)n;
-    tile_pre[stream_count] = tiles;
-    if (!n) return TBC_OK;
-    if (!out_values) return TBC_ERR_INVALID_ARGUMENT;
+    if (n && !out_values) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    const uint64_t tab_bytes = align_up(8ull * tab.size(), 256), flag_bytes = align_up(4 * (n + 1), 256);
-    const size_t cub_bytes = kway_scan_tmp_bytes((uint32_t)n);
-    const uint64_t dt = e->dev.top;
-    uint8_t *d = e->dev.alloc(tab_bytes + 2 * flag_bytes + align_up(cub_bytes, 256) + 256);
-    if (!d) return TBC_ERR_OUT_OF_MEMORY;
-    uint32_t *flags = (uint32_t *)(d + tab_bytes), *scan = (uint32_t *)(d + tab_bytes + flag_bytes);
-    void *cub = d + tab_bytes + 2 * flag_bytes;
-    tbc_status st = TBC_OK;
-    if (hipMemcpyAsync(d, tab.data(), 8 * tab.size(), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
-        launch_kway(tree->key_kind, descending != 0, (const uint64_t *)d, (const uint32_t *)(d + 8ull * stream_count),
-                    (const uint32_t *)(d + 8ull * stream_count) + stream_count + 1, tiles, stream_count, (uint32_t)n, tree->value_size, tree->timestamp_offset, flags, scan, cub, cub_bytes,
-                    (uint8_t *)out_values, e->stream) != 0)
-        st = TBC_ERR_DEVICE;
-    uint32_t total = 0;
-    if (st == TBC_OK && (hipMemcpyAsync(&total, scan + n, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-                         hipStreamSynchronize(e->stream) != hipSuccess))
-        st = TBC_ERR_DEVICE;
-    if (st != TBC_OK) hipStreamSynchronize(e->stream);
-    e->dev.top = dt;
-    *out_count = total;
+    tbc_kway *k = new (std::nothrow) tbc_kway();
+    if (!k) return TBC_ERR_OUT_OF_MEMORY;
+    k->engine = e;
+    if (!n) { // nothing to merge: complete at once
+        k->complete = true;
+        *out = k;
+        return TBC_OK;
+    }
+    const uint32_t vs = tree->value_size, T = kway_pair_tile();
+    // The tree of levels: level 0 pairs streams (2q, 2q + 1), the higher one
+    // first on equal keys (an odd last stream pairs with nothing, which still
+    // collapses its runs); every next level pairs the previous outputs.
+    // Counts: [0, k) the input counts, then one output count per pair.
+    struct Node { uint64_t ptr; uint32_t count_slot; uint64_t cap; };
+    std::vector<Node> cur;
+    std::vector<uint32_t> counts(stream_count);
+    for (uint32_t s = 0; s < stream_count; s++) {
+        cur.push_back(Node{(uint64_t)(uintptr_t)streams[s].values, s, streams[s].count});
+        counts[s] = streams[s].count;
+    }
+    std::vector<std::vector<KPairHost>> levels;
+    uint32_t next_count = stream_count;
+    const uint32_t empty_slot = 2 * TBC_KWAY_STREAMS_MAX + 1; // always zero
+    uint64_t max_slots = 0, max_tiles = 0;
+    int level = 0;
+    // temp output offsets (bytes) inside ping-pong buffer level % 2; final level writes out_values
+    while (true) {
+        const bool last = cur.size() <= 2;
+        std::vector<KPairHost> pairs;
+        std::vector<Node> nxt;
+        uint64_t off = 0;
+        uint32_t tiles = 0, slots = 0;
+        for (size_t q = 0; q < cur.size(); q += 2) {
+            const Node lo = cur[q];
+            const bool has_hi = q + 1 < cur.size();
+            KPairHost P{};
+            const Node A = has_hi ? cur[q + 1] : lo; // the higher stream (or the only one)
+            P.a = A.ptr;
+            P.na = A.count_slot;                      // patched to device pointers below
+            P.b = has_hi ? lo.ptr : A.ptr;
+            P.nb = has_hi ? lo.count_slot : empty_slot;
+            const uint64_t cap = A.cap + (has_hi ? lo.cap : 0);
+            P.out = last ? (uint64_t)(uintptr_t)out_values : off; // temp: offset, patched below
+            P.n_out = next_count;
+            P.tile_base = tiles;
+            P.split_base = slots;
+            P.tiles_cap = (uint32_t)((cap + T - 1) / T);
+            tiles += P.tiles_cap;
+            slots += P.tiles_cap + 1;
+            nxt.push_back(Node{last ? (uint64_t)(uintptr_t)out_values : off, next_count, cap});
+            off += cap * vs;
+            next_count++;
+            pairs.push_back(P);
+        }
+        max_slots = std::max<uint64_t>(max_slots, slots);
+        max_tiles = std::max<uint64_t>(max_tiles, tiles);
+        levels.push_back(pairs);
+        level++;
+        if (last) break;
+        cur = nxt;
+        // mark the offsets of this level's outputs as temp (resolved when the buffers exist)
+        for (auto &nd : cur) nd.ptr |= (1ull << 63) | ((uint64_t)((level - 1) & 1) << 62);
+    }
+    // Device memory: temp ping-pong buffers (stream-ordered), scratch, counts, descriptors.
+    const uint64_t temp_bytes = align_up(n * vs, 256);
+    const uint64_t n_levels = levels.size();
+    uint8_t *temp[2] = {nullptr, nullptr};
+    const uint64_t scratch_bytes = align_up(4 * max_slots, 256) + align_up(8 * 2 * (T / 64) * max_tiles, 256) +
+                                   2 * align_up(4 * max_tiles, 256);
+    const uint64_t count_bytes = align_up(4 * (2 * TBC_KWAY_STREAMS_MAX + 2), 256);
+    uint64_t npairs_total = 0;
+    for (auto &lv : levels) npairs_total += lv.size();
+    const uint64_t desc_bytes = align_up(sizeof(KPairHost) * npairs_total, 256);
+    const uint64_t need = 2 * temp_bytes + scratch_bytes + count_bytes + desc_bytes;
+    if (need > e->kway_scratch_size) { // grows once per larger merge (a stream drain)
+        if (hipStreamSynchronize(e->stream) != hipSuccess) {
+            delete k;
+            return TBC_ERR_DEVICE;
+        }
+        if (e->kway_scratch) hipFree(e->kway_scratch);
+        e->kway_scratch = nullptr;
+        e->kway_scratch_size = 0;
+        const uint64_t want = align_up(need + need / 8, 1ull << 24);
+        if (hipMalloc((void **)&e->kway_scratch, want) != hipSuccess) {
+            e->kway_scratch = nullptr;
+            delete k;
+            return TBC_ERR_OUT_OF_MEMORY;
+        }
+        e->kway_scratch_size = want;
+    }
+    temp[0] = e->kway_scratch;
+    temp[1] = e->kway_scratch + temp_bytes;
+    uint8_t *scratch = e->kway_scratch + 2 * temp_bytes;
+    k->dev_top = e->dev.top;
+    k->host_top = e->host.top;
+    uint8_t *h = e->host.alloc(count_bytes + desc_bytes + 256);
+    if (!h) {
+        e->host.top = k->host_top;
+        delete k;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    e->host.live++;
+    k->arena = true;
+    k->host_only = true;
+    uint32_t *splits = (uint32_t *)scratch;
+    uint64_t *masks = (uint64_t *)(scratch + align_up(4 * max_slots, 256));
+    uint32_t *tile_cnt = (uint32_t *)((uint8_t *)masks + align_up(8 * 2 * (T / 64) * max_tiles, 256));
+    uint32_t *tile_off = (uint32_t *)((uint8_t *)tile_cnt + align_up(4 * max_tiles, 256));
+    uint32_t *d_counts = (uint32_t *)(scratch + scratch_bytes);
+    uint8_t *d_desc = scratch + scratch_bytes + count_bytes;
+    uint32_t *h_counts = (uint32_t *)h;
+    KPairHost *h_desc = (KPairHost *)(h + count_bytes);
+    memset(h_counts, 0, count_bytes);
+    for (uint32_t s = 0; s < stream_count; s++) h_counts[s] = counts[s];
+    auto resolve = [&](uint64_t ptr) -> uint64_t {
+        if (!(ptr >> 63)) return ptr;
+        const int buf = (int)((ptr >> 62) & 1);
+        return (uint64_t)(uintptr_t)temp[buf] + (ptr & ((1ull << 62) - 1));
+    };
+    uint64_t di = 0;
+    for (uint64_t lv = 0; lv < n_levels; lv++) {
+        for (auto &P : levels[lv]) {
+            KPairHost Q = P;
+            Q.a = resolve(P.a);
+            Q.b = resolve(P.b);
+            Q.na = (uint64_t)(uintptr_t)(d_counts + P.na);
+            Q.nb = (uint64_t)(uintptr_t)(d_counts + P.nb);
+            Q.n_out = (uint64_t)(uintptr_t)(d_counts + P.n_out);
+            if (lv + 1 < n_levels) Q.out = (uint64_t)(uintptr_t)temp[lv & 1] + P.out;
+            h_desc[di++] = Q;
+        }
+    }
+    k->h_count = h_counts + (2 * TBC_KWAY_STREAMS_MAX); // the final count lands here
+    const uint32_t final_slot = levels.back()[0].n_out;
+    k->done = take_event(e);
+    bool ok = k->done && hipMemcpyAsync(d_counts, h_counts, count_bytes + desc_bytes, hipMemcpyHostToDevice, e->stream) ==
+                        hipSuccess;
+    di = 0;
+    for (uint64_t lv = 0; ok && lv < n_levels; lv++) {
+        uint32_t slots = 0, tiles = 0;
+        for (auto &P : levels[lv]) {
+            slots += P.tiles_cap + 1;
+            tiles += P.tiles_cap;
+        }
+        ok = launch_kway_level(tree->key_kind, descending != 0, d_desc + sizeof(KPairHost) * di,
+                               (uint32_t)levels[lv].size(), slots, tiles, vs, tree->timestamp_offset, splits, masks,
+                               tile_cnt, tile_off, e->stream) == 0;
+        if (!ok) fprintf(stderr, "tbc: k-way level %u (%u pairs, %u tiles) failed to launch: %s\n", (unsigned)lv,
+                         (unsigned)levels[lv].size(), tiles, hipGetErrorString(hipGetLastError()));
+        debug_stage(e->stream, "kway level");
+        di += levels[lv].size();
+    }
+    ok = ok && hipMemcpyAsync(k->h_count, d_counts + final_slot, 4, hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+         hipEventRecord(k->done, e->stream) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "tbc: k-way merge enqueue failed: %s\n", hipGetErrorString(hipGetLastError()));
+        hipStreamSynchronize(e->stream);
+        tbc_kway_release(k);
+        return TBC_ERR_DEVICE;
+    }
+    *out = k;
+    return TBC_OK;
+}
+
+tbc_status tbc_kway_poll(tbc_kway *k) {
+    if (!k) return TBC_ERR_INVALID_ARGUMENT;
+    if (k->complete) return k->result;
+    hipSetDevice(k->engine->device);
+    const hipError_t q = hipEventQuery(k->done);
+    if (q == hipErrorNotReady) return TBC_PENDING;
+    if (q != hipSuccess) fprintf(stderr, "tbc: k-way merge failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
+    k->complete = true;
+    k->result = q == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    if (k->result == TBC_OK) k->count = *k->h_count;
+    return k->result;
+}
+
+tbc_status tbc_kway_wait(tbc_kway *k) {
+    if (!k) return TBC_ERR_INVALID_ARGUMENT;
+    if (k->complete) return k->result;
+    hipSetDevice(k->engine->device);
+    if (const hipError_t q = hipEventSynchronize(k->done); q != hipSuccess) {
+        fprintf(stderr, "tbc: k-way merge failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
+        k->complete = true;
+        k->result = TBC_ERR_DEVICE;
+        return k->result;
+    }
+    return tbc_kway_poll(k);
+}
+
+tbc_status tbc_kway_count(const tbc_kway *k, uint64_t *out_count) {
+    if (!k || !out_count) return TBC_ERR_INVALID_ARGUMENT;
+    if (!k->complete) return TBC_PENDING;
+    if (k->result != TBC_OK) return k->result;
+    *out_count = k->count;
+    return TBC_OK;
+}
+
+void tbc_kway_release(tbc_kway *k) {
+    if (!k) return;
+    tbc_engine *e = k->engine;
+    hipSetDevice(e->device);
+    if (!k->complete && k->done) hipEventSynchronize(k->done);
+    if (k->done) e->event_pool.push_back(k->done);
+    if (k->arena) { // same protocol as batches: LIFO restores the tops, idle reclaims
+        if (!k->host_only) {
+            if (e->dev.live) e->dev.live--;
+            if (e->dev.live == 0) e->dev.top = 0;
+            else e->dev.top = std::min(e->dev.top, std::max(k->dev_top, e->dev.top));
+        }
+        if (e->host.live) e->host.live--;
+        if (e->host.live == 0) e->host.top = 0;
+    }
+    delete k;
+}
+
+tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams, uint32_t stream_count,
+                          uint32_t descending, void *out_values, uint64_t *out_count) {
+    if (!out_count) return TBC_ERR_INVALID_ARGUMENT;
+    *out_count = 0;
+    tbc_kway *k = nullptr;
+    tbc_status st = tbc_kway_merge_submit(e, tree, streams, stream_count, descending, out_values, &k);
+    if (st != TBC_OK) return st;
+    st = tbc_kway_wait(k);
+    if (st == TBC_OK) st = tbc_kway_count(k, out_count);
+    tbc_kway_release(k);
     return st;
 }
 

@@ -5,263 +5,337 @@
 // with precedence wins (`ordered`, :197-203) and `pop` discards every later
 // value whose key equals the last one popped (:91-107). With the precedence
 // of the reference's own tests (stream_precedence(a, b) = a > b, :239-244:
-// higher streams win) the output is a pure function of each element:
+// higher streams win), take the merged order "key, then higher stream first,
+// then position in the stream": the reference emits exactly the values whose
+// key differs from the previous value's in that order.
 //
-//   value (s, i) is emitted  iff  it is the first of its key's run in stream s
-//                                 and no stream s' > s holds that key;
-//   its output position      =    sum over streams s' of the emitted values of
-//                                 s' whose key comes before it (direction order).
-//
-// Kernels: emit flags (binary searches in the higher streams) -> exclusive scan
-// of the flags (hipCUB) -> scatter (one binary search per stream), both
-// searching only a per-tile window of each other stream. Each
-// element is read once per kernel plus O(k log n) key probes; the scatter
-// moves each emitted value once (16-byte copies).
+// That rule composes: merging two already-merged groups of streams (the
+// higher group first on equal keys) and emitting on a key change gives the
+// merge of all their streams. So k streams are merged as a pairwise tree,
+// ceil(log2 k) levels, every pair of a level in the same launches:
+//   k_kpair_partition  merge-path split of every 2,048-position tile;
+//   k_kpair_tile       per tile: the keys of both sides in LDS, each thread
+//                      merges 8 positions and sets their side and emit bits,
+//                      and the tile's emitted count;
+//   k_kpair_scan       per pair: tile offsets, and the pair's output count
+//                      (on the device: the next level reads it there);
+//   k_kpair_scatter    the emitted values, 16 bytes per lane.
+// Each level reads every value once for keys and once for the copy and
+// writes its output once; nothing waits on the host (the final count is
+// copied back with the rest, tbc_kway_poll).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "keys.h"
 #include "tbc.h"
 
 namespace tbc {
 
-template <int KIND, bool DESC, int KL = KeyLimbs<KIND>::value>
-__device__ __forceinline__ bool before(const Key<KL> &a, const Key<KL> &b) {
-    return DESC ? key_lt(b, a) : key_lt(a, b);
-}
+constexpr uint32_t kPairTile = 2048;
+constexpr uint32_t kPairThreads = 256;
+constexpr uint32_t kPairPer = kPairTile / kPairThreads;      // 8 positions per thread
+constexpr uint32_t kPairWords = kPairTile / 64;              // mask words per kind per tile
 
-// First index j of stream [v, v + n) whose key is not before `k`.
-template <int KIND, bool DESC, int KL = KeyLimbs<KIND>::value>
-__device__ __forceinline__ uint32_t kway_lower_bound(const uint8_t *v, uint32_t n, uint32_t vs, uint32_t ts,
-                                                     const Key<KL> &k) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (before<KIND, DESC>(load_key<KIND>(v + (size_t)mid * vs, ts), k)) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-constexpr uint32_t kKwayTile = 256;
-
-// Workgroups take 256 consecutive values of ONE stream (tiles never straddle
-// streams). The lower bounds of any key of the tile in another stream t lie
-// between those of the tile's first and last keys, so lanes 0..k-1 search
-// those two once and every thread then searches only that window (usually a
-// few hundred values, cache-resident) instead of the whole stream.
-struct KwayTile {
-    uint32_t s, i0, n_s;
+// One 2-way merge of a level: A is the higher-precedence side (first on
+// equal keys), B the lower; counts live on the device (a previous level's
+// output counts).
+struct KPair {
+    const uint8_t *a, *b;
+    const uint32_t *na, *nb; // device counts
+    uint8_t *out;
+    uint32_t *n_out;         // device: emitted values
+    uint32_t tile_base;      // first tile of the pair (tiles_cap tiles)
+    uint32_t split_base;     // first split slot (tiles_cap + 1 slots)
+    uint32_t tiles_cap;      // tiles of the pair's capacity (its counts are an upper bound)
+    uint32_t pad;
 };
 
-__device__ __forceinline__ KwayTile kway_tile(const uint32_t *pre, const uint32_t *tile_pre, uint32_t k) {
-    KwayTile t{0, 0, 0};
-    while (t.s + 1 < k && gld<uint32_t>(tile_pre + t.s + 1) <= blockIdx.x) t.s++;
-    t.i0 = (blockIdx.x - gld<uint32_t>(tile_pre + t.s)) * kKwayTile;
-    t.n_s = gld<uint32_t>(pre + t.s + 1) - gld<uint32_t>(pre + t.s);
-    return t;
-}
-
-template <int KIND, bool DESC>
-__device__ __forceinline__ void kway_windows(const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t vs,
-                                             uint32_t ts, const KwayTile &tl, uint32_t *lo, uint32_t *hi) {
-    const uint32_t t = threadIdx.x;
-    if (t < k && t != tl.s) {
-        const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + tl.s);
-        const uint32_t last = min(tl.i0 + kKwayTile, tl.n_s) - 1;
-        const uint8_t *w = (const uint8_t *)gld<uint64_t>(ptr + t);
-        const uint32_t len = gld<uint32_t>(pre + t + 1) - gld<uint32_t>(pre + t);
-        lo[t] = kway_lower_bound<KIND, DESC>(w, len, vs, ts, load_key<KIND>(v + (size_t)tl.i0 * vs, ts));
-        hi[t] = kway_lower_bound<KIND, DESC>(w, len, vs, ts, load_key<KIND>(v + (size_t)last * vs, ts));
-    }
-    __syncthreads();
-}
-
-// lower bound of `key` in stream t, known to lie in [lo, hi].
 template <int KIND, bool DESC, int KL = KeyLimbs<KIND>::value>
-__device__ __forceinline__ uint32_t kway_window_search(const uint8_t *w, uint32_t lo, uint32_t hi, uint32_t vs,
-                                                       uint32_t ts, const Key<KL> &key) {
+__device__ __forceinline__ bool kbefore(const Key<KL> &x, const Key<KL> &y) {
+    return DESC ? key_lt(y, x) : key_lt(x, y);
+}
+template <int KIND, bool DESC, int KL = KeyLimbs<KIND>::value>
+__device__ __forceinline__ bool kle(const Key<KL> &x, const Key<KL> &y) {
+    return !kbefore<KIND, DESC>(y, x);
+}
+
+template <bool SPLITS>
+__device__ __forceinline__ uint32_t pair_of(const KPair *pairs, uint32_t npairs, uint32_t g) {
+    uint32_t lo = 0, hi = npairs - 1;
     while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (before<KIND, DESC>(load_key<KIND>(w + (size_t)mid * vs, ts), key)) lo = mid + 1;
-        else hi = mid;
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if ((SPLITS ? pairs[mid].split_base : pairs[mid].tile_base) <= g) lo = mid;
+        else hi = mid - 1;
     }
     return lo;
 }
 
-// Lower bounds of `key` in every stream u < KMAX (u != skip) at once: one
-// bisection step per stream per round, so a thread has up to k independent
-// probes in flight instead of k dependent searches (k <= KMAX only).
-constexpr int kKwayLockstep = 16;
-
-template <int KIND, bool DESC, int KMAX, int KL = KeyLimbs<KIND>::value>
-__device__ __forceinline__ void kway_lockstep(const uint64_t *ptr, uint32_t k, uint32_t vs, uint32_t ts,
-                                              const uint32_t *wlo, const uint32_t *whi, uint32_t rounds,
-                                              uint32_t from, uint32_t skip, const Key<KL> &key,
-                                              uint32_t (&j)[KMAX], const uint8_t *(&w)[KMAX]) {
-    uint32_t hi[KMAX];
-#pragma unroll
-    for (int u = 0; u < KMAX; u++) {
-        const bool on = (uint32_t)u < k && (uint32_t)u >= from && (uint32_t)u != skip;
-        j[u] = on ? wlo[u] : 0;
-        hi[u] = on ? whi[u] : 0;
-        w[u] = (uint32_t)u < k ? (const uint8_t *)gld<uint64_t>(ptr + u) : nullptr;
+// splits[tile_base + t] = number of A values among the first t * kPairTile
+// merged positions (A first on equal keys), for t = 0 .. tiles_cap.
+template <int KIND, bool DESC>
+__global__ __launch_bounds__(256) void k_kpair_partition(const KPair *pairs, uint32_t npairs, uint32_t total,
+                                                         uint32_t vs, uint32_t ts, uint32_t *splits) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const KPair P = pairs[pair_of<true>(pairs, npairs, g)];
+    const uint32_t t = g - P.split_base; // 0 .. tiles_cap
+    const uint32_t na = *P.na, nb = *P.nb, n = na + nb;
+    const uint32_t d = t * kPairTile < n ? t * kPairTile : n;
+    uint32_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (kle<KIND, DESC>(load_key<KIND>(P.a + (size_t)mid * vs, ts), load_key<KIND>(P.b + (size_t)(d - 1 - mid) * vs, ts)))
+            lo = mid + 1;
+        else
+            hi = mid;
     }
-    for (uint32_t r = 0; r < rounds; r++) {
-#pragma unroll
-        for (int u = 0; u < KMAX; u++) {
-            if (j[u] < hi[u]) {
-                const uint32_t mid = (j[u] + hi[u]) >> 1;
-                if (before<KIND, DESC>(load_key<KIND>(w[u] + (size_t)mid * vs, ts), key)) j[u] = mid + 1;
-                else hi[u] = mid;
-            }
-        }
-    }
+    splits[g] = lo;
 }
 
-__device__ __forceinline__ uint32_t bisect_rounds(uint32_t width) {
-    return 32 - __builtin_clz(width | 1); // ceil(log2(width + 1))
-}
+template <int KL> struct PairShared {
+    uint64_t key[KL][kPairTile + 2];
+    uint32_t wave_sums[kPairThreads / 64];
+};
 
-template <int KIND, bool DESC, int KMAX, int KL = KeyLimbs<KIND>::value>
-__device__ __forceinline__ bool kway_emit_lockstep(const uint64_t *ptr, const uint32_t *pre, uint32_t k, uint32_t vs,
-                                                   uint32_t ts, const uint32_t *lo, const uint32_t *hi, uint32_t s,
-                                                   const Key<KL> &key, bool emit) {
-    uint32_t j[KMAX];
-    const uint8_t *w[KMAX];
-    uint32_t rounds = 0;
-    for (uint32_t u = s + 1; u < k; u++) rounds = max(rounds, bisect_rounds(hi[u] - lo[u]));
-    kway_lockstep<KIND, DESC, KMAX>(ptr, k, vs, ts, lo, hi, rounds, s + 1, s, key, j, w);
-#pragma unroll
-    for (int u = 0; u < KMAX; u++) {
-        if ((uint32_t)u > s && (uint32_t)u < k) {
-            const uint32_t len = gld<uint32_t>(pre + u + 1) - gld<uint32_t>(pre + u);
-            if (j[u] < len && key_eq(load_key<KIND>(w[u] + (size_t)j[u] * vs, ts), key)) emit = false;
-        }
-    }
-    return emit;
-}
-
-template <int KIND, bool DESC, int KMAX, int KL = KeyLimbs<KIND>::value>
-__device__ __forceinline__ uint32_t kway_pos_lockstep(const uint64_t *ptr, const uint32_t *pre, uint32_t k,
-                                                      uint32_t vs, uint32_t ts, const uint32_t *lo,
-                                                      const uint32_t *hi, uint32_t s, uint32_t i, const Key<KL> &key,
-                                                      const uint32_t *scan) {
-    uint32_t j[KMAX];
-    const uint8_t *w[KMAX];
-    uint32_t rounds = 0;
-    for (uint32_t u = 0; u < k; u++)
-        if (u != s) rounds = max(rounds, bisect_rounds(hi[u] - lo[u]));
-    kway_lockstep<KIND, DESC, KMAX>(ptr, k, vs, ts, lo, hi, rounds, 0, s, key, j, w);
-    uint32_t pos = 0;
-#pragma unroll
-    for (int u = 0; u < KMAX; u++) {
-        if ((uint32_t)u < k) {
-            const uint32_t base = gld<uint32_t>(pre + u);
-            const uint32_t jj = (uint32_t)u == s ? i : j[u];
-            pos += gld<uint32_t>(scan + base + jj) - gld<uint32_t>(scan + base);
-        }
-    }
-    return pos;
-}
-
-template <int KIND, bool DESC, bool LS>
-__global__ __launch_bounds__(256) void k_kway_flags(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
-                                                    uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags) {
-    __shared__ uint32_t lo[TBC_KWAY_STREAMS_MAX], hi[TBC_KWAY_STREAMS_MAX];
-    const KwayTile tl = kway_tile(pre, tile_pre, k);
-    kway_windows<KIND, DESC>(ptr, pre, k, vs, ts, tl, lo, hi);
-    const uint32_t i = tl.i0 + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x == 0) gst<uint32_t>(flags + n, 0u); // the scan's total lands there
-    if (i >= tl.n_s) return;
-    const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + tl.s);
-    const auto key = load_key<KIND>(v + (size_t)i * vs, ts);
-    bool emit = i == 0 || !key_eq(load_key<KIND>(v + (size_t)(i - 1) * vs, ts), key);
-    if (LS) { // 9..16 streams (a separate instantiation: its registers do not cost the others occupancy)
-        gst<uint32_t>(flags + gld<uint32_t>(pre + tl.s) + i,
-                      kway_emit_lockstep<KIND, DESC, kKwayLockstep>(ptr, pre, k, vs, ts, lo, hi, tl.s, key, emit)
-                          ? 1u : 0u);
+template <int KIND, bool DESC>
+__global__ __launch_bounds__(kPairThreads) void k_kpair_tile(const KPair *pairs, uint32_t npairs, uint32_t vs,
+                                                             uint32_t ts, const uint32_t *splits, uint64_t *masks,
+                                                             uint32_t *tile_cnt) {
+    constexpr int KL = KeyLimbs<KIND>::value;
+    __shared__ PairShared<KL> sh;
+    const uint32_t g = blockIdx.x, tid = threadIdx.x;
+    const KPair P = pairs[pair_of<false>(pairs, npairs, g)];
+    const uint32_t t = g - P.tile_base;
+    const uint32_t na = *P.na, nb = *P.nb, n = na + nb;
+    const uint32_t d0 = t * kPairTile;
+    if (d0 >= n) { // beyond the pair's actual merge (its counts were only known on the device)
+        if (tid == 0) tile_cnt[g] = 0;
         return;
     }
-    for (uint32_t t = tl.s + 1; emit && t < k; t++) {
-        const uint32_t len = gld<uint32_t>(pre + t + 1) - gld<uint32_t>(pre + t);
-        const uint8_t *w = (const uint8_t *)gld<uint64_t>(ptr + t);
-        const uint32_t j = kway_window_search<KIND, DESC>(w, lo[t], hi[t], vs, ts, key);
-        if (j < len && key_eq(load_key<KIND>(w + (size_t)j * vs, ts), key)) emit = false;
+    const uint32_t d1 = d0 + kPairTile < n ? d0 + kPairTile : n;
+    const uint32_t sb = P.split_base + t; // split slot of this tile's first boundary
+    const uint32_t i0 = splits[sb], i1 = splits[sb + 1];
+    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t ea = i1 - i0, eb = j1 - j0;
+    // LDS: A[i0 .. i1) at [0, ea), B[j0 .. j1) at [ea, ea + eb), the previous merged key at kPairTile + 1.
+    for (uint32_t e = tid; e < ea + eb; e += kPairThreads) {
+        const uint8_t *v = e < ea ? P.a + (size_t)(i0 + e) * vs : P.b + (size_t)(j0 + e - ea) * vs;
+        const auto k = load_key<KIND>(v, ts);
+#pragma unroll
+        for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
     }
-    gst<uint32_t>(flags + gld<uint32_t>(pre + tl.s) + i, emit ? 1u : 0u);
-}
-
-template <int KIND, bool DESC, bool LS>
-__global__ __launch_bounds__(256) void k_kway_scatter(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
-                                                      uint32_t k, uint32_t vs, uint32_t ts, const uint32_t *flags,
-                                                      const uint32_t *scan, uint8_t *out) {
-    __shared__ uint32_t lo[TBC_KWAY_STREAMS_MAX], hi[TBC_KWAY_STREAMS_MAX];
-    const KwayTile tl = kway_tile(pre, tile_pre, k);
-    kway_windows<KIND, DESC>(ptr, pre, k, vs, ts, tl, lo, hi);
-    const uint32_t i = tl.i0 + threadIdx.x;
-    if (i >= tl.n_s || !gld<uint32_t>(flags + gld<uint32_t>(pre + tl.s) + i)) return;
-    const uint8_t *v = (const uint8_t *)gld<uint64_t>(ptr + tl.s) + (size_t)i * vs;
-    const auto key = load_key<KIND>(v, ts);
-    uint32_t pos = 0;
-    if (LS) {
-        pos = kway_pos_lockstep<KIND, DESC, kKwayLockstep>(ptr, pre, k, vs, ts, lo, hi, tl.s, i, key, scan);
+    if (tid == 0) {
+        // The merged predecessor of position d0 is the later of A[i0-1] and
+        // B[j0-1]; only its key matters: the larger one (in merge order).
+        Key<KL> pk;
+        bool have = false;
+        if (i0 > 0) pk = load_key<KIND>(P.a + (size_t)(i0 - 1) * vs, ts), have = true;
+        if (j0 > 0) {
+            const auto kb = load_key<KIND>(P.b + (size_t)(j0 - 1) * vs, ts);
+            if (!have || kbefore<KIND, DESC>(pk, kb)) pk = kb;
+            have = true;
+        }
+        const uint64_t flag = have ? 1u : 0u;
+#pragma unroll
+        for (int l = 0; l < KL; l++) sh.key[l][kPairTile + 1] = have ? pk.l[l] : 0;
+        sh.key[0][kPairTile] = flag; // slot kPairTile holds "has a predecessor"
+    }
+    __syncthreads();
+    auto key_at = [&](uint32_t e) {
+        Key<KL> k;
+#pragma unroll
+        for (int l = 0; l < KL; l++) k.l[l] = sh.key[l][e];
+        return k;
+    };
+    // This thread's positions [d, d + kPairPer) of the tile: merge-path search in LDS.
+    const uint32_t tot = ea + eb;
+    const uint32_t d = kPairPer * tid < tot ? kPairPer * tid : tot;
+    uint32_t a, b;
+    {
+        uint32_t lo = d > eb ? d - eb : 0, hi = d < ea ? d : ea;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (kle<KIND, DESC>(key_at(mid), key_at(ea + d - 1 - mid))) lo = mid + 1;
+            else hi = mid;
+        }
+        a = lo;
+        b = d - lo;
+    }
+    // Key of the merged position before d.
+    bool have_prev;
+    Key<KL> prev;
+    if (d == 0) {
+        have_prev = sh.key[0][kPairTile] != 0;
+        prev = key_at(kPairTile + 1);
     } else {
-    for (uint32_t t = 0; t < k; t++) {
-        const uint32_t base = gld<uint32_t>(pre + t);
-        const uint32_t j = t == tl.s ? i
-                                     : kway_window_search<KIND, DESC>((const uint8_t *)gld<uint64_t>(ptr + t), lo[t],
-                                                                      hi[t], vs, ts, key);
-        pos += gld<uint32_t>(scan + base + j) - gld<uint32_t>(scan + base);
+        have_prev = true;
+        if (a == 0) prev = key_at(ea + b - 1);
+        else if (b == 0) prev = key_at(a - 1);
+        else {
+            const auto ka = key_at(a - 1), kb = key_at(ea + b - 1);
+            prev = kbefore<KIND, DESC>(ka, kb) ? kb : ka;
+        }
     }
+    uint32_t ebits = 0, abits = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPairPer; k++) {
+        if (d + k >= tot) continue;
+        const bool take_a = a < ea && (b >= eb || kle<KIND, DESC>(key_at(a), key_at(ea + b)));
+        const auto kk = take_a ? key_at(a) : key_at(ea + b);
+        const bool emit = !have_prev || !key_eq(kk, prev);
+        ebits |= (emit ? 1u : 0u) << k;
+        abits |= (take_a ? 1u : 0u) << k;
+        if (take_a) a++;
+        else b++;
+        prev = kk;
+        have_prev = true;
     }
-    uint8_t *d = out + (size_t)pos * vs;
-    for (uint32_t o = 0; o < vs; o += 16) { // 16-byte moves (value sizes are multiples of 16)
-        const uint64_t a = gld<uint64_t>(v + o), b = gld<uint64_t>(v + o + 8);
-        gst<uint64_t>(d + o, a);
-        gst<uint64_t>(d + o + 8, b);
+    constexpr uint32_t kThreadsPerWord = 64 / kPairPer;
+    const uint32_t shb = kPairPer * (tid % kThreadsPerWord);
+    uint64_t ew = (uint64_t)ebits << shb, aw = (uint64_t)abits << shb;
+    for (uint32_t o = 1; o < kThreadsPerWord; o <<= 1) {
+        ew |= __shfl_xor(ew, o, 64);
+        aw |= __shfl_xor(aw, o, 64);
+    }
+    uint64_t *m = masks + (size_t)g * (2 * kPairWords);
+    if (tid % kThreadsPerWord == 0) {
+        m[tid / kThreadsPerWord] = ew;
+        m[kPairWords + tid / kThreadsPerWord] = aw;
+    }
+    uint32_t sum = __builtin_popcount(ebits);
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((tid & 63) == 0) sh.wave_sums[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0) tile_cnt[g] = sh.wave_sums[0] + sh.wave_sums[1] + sh.wave_sums[2] + sh.wave_sums[3];
+}
+
+// Per pair (one workgroup): exclusive scan of its tiles' counts into
+// tile_off, the pair's output count into *n_out.
+constexpr uint32_t kPairScanThreads = 1024;
+__global__ __launch_bounds__(kPairScanThreads) void k_kpair_scan(const KPair *pairs, const uint32_t *tile_cnt,
+                                                                 uint32_t *tile_off) {
+    __shared__ uint32_t wsum[kPairScanThreads / 64];
+    __shared__ uint32_t carry;
+    const KPair P = pairs[blockIdx.x];
+    const uint32_t first = P.tile_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < P.tiles_cap; base += kPairScanThreads) {
+        const uint32_t t = base + tid;
+        const uint32_t c = t < P.tiles_cap ? tile_cnt[first + t] : 0u;
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        if (lane == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        uint32_t off = carry;
+        for (uint32_t w = 0; w < (tid >> 6); w++) off += wsum[w];
+        if (t < P.tiles_cap) tile_off[first + t] = off + incl - c;
+        __syncthreads();
+        if (tid == kPairScanThreads - 1) carry = off + incl;
+        __syncthreads();
+    }
+    if (tid == 0) *P.n_out = carry;
+}
+
+__global__ __launch_bounds__(kPairThreads) void k_kpair_scatter(const KPair *pairs, uint32_t npairs, uint32_t vs,
+                                                                const uint32_t *splits, const uint64_t *masks,
+                                                                const uint32_t *tile_off) {
+    __shared__ uint32_t s_pre[3][kPairWords + 1]; // emitted, A taken, B taken before word w
+    __shared__ uint64_t s_src[4][64], s_dst[4][64];
+    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const KPair P = pairs[pair_of<false>(pairs, npairs, g)];
+    const uint32_t t = g - P.tile_base;
+    const uint32_t na = *P.na, nb = *P.nb, n = na + nb;
+    const uint32_t d0 = t * kPairTile;
+    if (d0 >= n) return;
+    const uint32_t i0 = splits[P.split_base + t], j0 = d0 - i0;
+    const uint64_t *m = masks + (size_t)g * (2 * kPairWords);
+    auto valid_of = [&](uint32_t w) -> uint64_t {
+        const uint32_t pos0 = d0 + 64 * w;
+        return pos0 >= n ? 0ull : (n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1));
+    };
+    if (tid < kPairWords) {
+        const uint64_t em = m[tid], am = m[kPairWords + tid];
+        s_pre[0][tid + 1] = __builtin_popcountll(em);
+        s_pre[1][tid + 1] = __builtin_popcountll(am);
+        s_pre[2][tid + 1] = __builtin_popcountll(valid_of(tid) & ~am);
+    }
+    __syncthreads();
+    if (tid < 3) {
+        uint32_t acc = 0;
+        s_pre[tid][0] = 0;
+        for (uint32_t w = 1; w <= kPairWords; w++) {
+            acc += s_pre[tid][w];
+            s_pre[tid][w] = acc;
+        }
+    }
+    __syncthreads();
+    const uint32_t out0 = tile_off[g];
+    const uint32_t cpv = vs >> 4;
+    const uint64_t lt = (1ull << lane) - 1;
+    for (uint32_t w = wv; w < kPairWords; w += 4) {
+        if (d0 + 64 * w >= n) break;
+        const uint64_t em = m[w], am = m[kPairWords + w];
+        const uint32_t ns = __builtin_popcountll(em);
+        if (ns == 0) continue;
+        const uint64_t valid = valid_of(w);
+        if ((em >> lane) & 1) {
+            const uint32_t r = __builtin_popcountll(em & lt);
+            const bool from_a = (am >> lane) & 1;
+            const uint8_t *src = from_a ? P.a + (size_t)(i0 + s_pre[1][w] + __builtin_popcountll(am & lt)) * vs
+                                        : P.b + (size_t)(j0 + s_pre[2][w] + __builtin_popcountll(valid & ~am & lt)) * vs;
+            s_src[wv][r] = (uint64_t)(uintptr_t)src;
+            s_dst[wv][r] = (uint64_t)(uintptr_t)(P.out + (size_t)(out0 + s_pre[0][w] + r) * vs);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t total = ns * cpv;
+        for (uint32_t c0 = 0; c0 < total; c0 += 64 * 4) {
+            u32x4 v[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++) {
+                const uint32_t c = c0 + lane + 64 * u;
+                if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[wv][c / cpv] + 16 * (c % cpv));
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++) {
+                const uint32_t c = c0 + lane + 64 * u;
+                if (c < total) gst<u32x4>((uint8_t *)(uintptr_t)s_dst[wv][c / cpv] + 16 * (c % cpv), v[u]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
 }
 
-template <int KIND, bool DESC, bool LS>
-static int launch_kway_t3(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre, uint32_t tiles, uint32_t k,
-                         uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan, void *cub_tmp,
-                         size_t cub_bytes, uint8_t *out, hipStream_t s) {
-    hipLaunchKernelGGL((k_kway_flags<KIND, DESC, LS>), dim3(tiles), dim3(kKwayTile), 0, s, ptr, pre, tile_pre, k, n, vs, ts,
-                       flags);
-    if (hipGetLastError() != hipSuccess) return -1;
-    if (hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, flags, scan, (int)n + 1, s) != hipSuccess) return -1;
-    hipLaunchKernelGGL((k_kway_scatter<KIND, DESC, LS>), dim3(tiles), dim3(kKwayTile), 0, s, ptr, pre, tile_pre, k, vs, ts,
-                       flags, scan, out);
+// Every level's launches for `npairs` pairs whose descriptors are on the
+// device; split slots: tiles_cap + 1 per pair; tiles: tiles_cap per pair.
+template <int KIND, bool DESC>
+static int launch_level_t(const KPair *d_pairs, uint32_t npairs, uint32_t slots, uint32_t tiles, uint32_t vs,
+                          uint32_t ts, uint32_t *splits, uint64_t *masks, uint32_t *tile_cnt, uint32_t *tile_off,
+                          hipStream_t s) {
+    hipLaunchKernelGGL((k_kpair_partition<KIND, DESC>), dim3((slots + 255) / 256), dim3(256), 0, s, d_pairs, npairs,
+                       slots, vs, ts, splits);
+    hipLaunchKernelGGL((k_kpair_tile<KIND, DESC>), dim3(tiles), dim3(kPairThreads), 0, s, d_pairs, npairs, vs, ts,
+                       (const uint32_t *)splits, masks, tile_cnt);
+    hipLaunchKernelGGL(k_kpair_scan, dim3(npairs), dim3(kPairScanThreads), 0, s, d_pairs, (const uint32_t *)tile_cnt,
+                       tile_off);
+    hipLaunchKernelGGL(k_kpair_scatter, dim3(tiles), dim3(kPairThreads), 0, s, d_pairs, npairs, vs,
+                       (const uint32_t *)splits, (const uint64_t *)masks, (const uint32_t *)tile_off);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int KIND, bool DESC>
-static int launch_kway_t(const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre, uint32_t tiles, uint32_t k,
-                         uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan, void *cub_tmp,
-                         size_t cub_bytes, uint8_t *out, hipStream_t s) {
-    // Few streams: dependent searches with early exit measured faster (8
-    // streams); 9..16 streams: lockstep bisection (16: 13.6 -> 8.3 ms).
-    if (k > 8 && k <= (uint32_t)kKwayLockstep)
-        return launch_kway_t3<KIND, DESC, true>(ptr, pre, tile_pre, tiles, k, n, vs, ts, flags, scan, cub_tmp,
-                                                cub_bytes, out, s);
-    return launch_kway_t3<KIND, DESC, false>(ptr, pre, tile_pre, tiles, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes,
-                                             out, s);
-}
-
-size_t kway_scan_tmp_bytes(uint32_t n) {
-    size_t bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n + 1);
-    return bytes;
-}
-
-int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
-                uint32_t tiles, uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan,
-                void *cub_tmp, size_t cub_bytes, uint8_t *out, void *stream) {
+int launch_kway_level(uint32_t key_kind, bool descending, const void *d_pairs, uint32_t npairs, uint32_t slots,
+                      uint32_t tiles, uint32_t vs, uint32_t ts, uint32_t *splits, uint64_t *masks, uint32_t *tile_cnt,
+                      uint32_t *tile_off, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-#define TBC_KWAY(KIND)                                                                                    \
-    return descending ? launch_kway_t<KIND, true>(ptr, pre, tile_pre, tiles, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes, out, s) \
-                      : launch_kway_t<KIND, false>(ptr, pre, tile_pre, tiles, k, n, vs, ts, flags, scan, cub_tmp, cub_bytes, out, s)
+    const KPair *P = (const KPair *)d_pairs;
+#define TBC_KWAY(KIND)                                                                                             \
+    return descending ? launch_level_t<KIND, true>(P, npairs, slots, tiles, vs, ts, splits, masks, tile_cnt, tile_off, s) \
+                      : launch_level_t<KIND, false>(P, npairs, slots, tiles, vs, ts, splits, masks, tile_cnt, tile_off, s)
     switch (key_kind) {
     case kKeyTimestamp: TBC_KWAY(kKeyTimestamp);
     case kKeyIdU128: TBC_KWAY(kKeyIdU128);
@@ -271,5 +345,8 @@ int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const u
     }
 #undef TBC_KWAY
 }
+
+uint32_t kway_pair_tile() { return kPairTile; }
+uint32_t kway_pair_bytes() { return sizeof(KPair); }
 
 } // namespace tbc

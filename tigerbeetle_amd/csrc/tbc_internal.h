@@ -231,8 +231,12 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
 uint64_t sort_scratch_bytes(const SortItem *items, uint32_t count);
 uint64_t sort_status_words(const SortItem *items, uint32_t count);
 uint64_t sort_host_bytes(const SortItem *items, uint32_t count);
-size_t kway_scan_tmp_bytes(uint32_t n);
-int launch_kway(uint32_t key_kind, bool descending, const uint64_t *ptr, const uint32_t *pre, const uint32_t *tile_pre,
-                uint32_t tiles, uint32_t k, uint32_t n, uint32_t vs, uint32_t ts, uint32_t *flags, uint32_t *scan,
-                void *cub_tmp, size_t cub_bytes, uint8_t *out, void *stream);
+// One level of the pairwise k-way merge tree (kway.hip): d_pairs holds
+// npairs KPair descriptors (kway_pair_bytes() each), slots = sum(tiles_cap + 1),
+// tiles = sum(tiles_cap) with tiles of kway_pair_tile() merged positions.
+int launch_kway_level(uint32_t key_kind, bool descending, const void *d_pairs, uint32_t npairs, uint32_t slots,
+                      uint32_t tiles, uint32_t vs, uint32_t ts, uint32_t *splits, uint64_t *masks, uint32_t *tile_cnt,
+                      uint32_t *tile_off, void *stream);
+uint32_t kway_pair_tile();
+uint32_t kway_pair_bytes();
 } // namespace tbc

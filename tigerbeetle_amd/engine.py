@@ -239,6 +239,33 @@ class Batch:
             pass
 
 
+class KwayMerge:
+    """A submitted k-way merge (tbc_kway_*)."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def poll(self) -> bool:
+        st = lib().tbc_kway_poll(self.handle)
+        if st == abi.TBC_PENDING:
+            return False
+        check(st, "tbc_kway_poll")
+        return True
+
+    def wait(self) -> None:
+        check(lib().tbc_kway_wait(self.handle), "tbc_kway_wait")
+
+    def count(self) -> int:
+        n = ctypes.c_uint64()
+        check(lib().tbc_kway_count(self.handle, ctypes.byref(n)), "tbc_kway_count")
+        return n.value
+
+    def release(self) -> None:
+        if self.handle:
+            lib().tbc_kway_release(self.handle)
+            self.handle = None
+
+
 class Engine:
     def __init__(self, device: int = 0, block_size: int = BLOCK_SIZE, arena_bytes: int = 0,
                  profile: bool = False):
@@ -348,6 +375,19 @@ class Engine:
         check(lib().tbc_kway_merge(self.handle, ctypes.byref(t), arr, len(streams), int(descending),
                                    out.ptr if out is not None else None, ctypes.byref(n_out)), "tbc_kway_merge")
         return n_out.value
+
+    def kway_merge_submit(self, tree: TreeSpec, streams: list, out: DeviceBuffer, descending: bool = False):
+        """tbc_kway_merge_submit: enqueue the merge and return a KwayMerge
+        handle at once (poll() / wait(), then count())."""
+        arr = (abi.Segment * max(1, len(streams)))()
+        for i, (p, n) in enumerate(streams):
+            arr[i].values, arr[i].count = p, n
+        t = tree.ctype()
+        h = ctypes.c_void_p()
+        check(lib().tbc_kway_merge_submit(self.handle, ctypes.byref(t), arr, len(streams), int(descending),
+                                          out.ptr if out is not None else None, ctypes.byref(h)),
+              "tbc_kway_merge_submit")
+        return KwayMerge(h)
 
     def prepare(self, jobs: list):
         """The tbc_compaction[] array of a job list (cached for a repeated list)."""

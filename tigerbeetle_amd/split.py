@@ -9,9 +9,16 @@ WHERE its survivors fall in the job's output: data blocks are cut every
 `block_value_count_max` survivors and tables every `data_block_count_max`
 blocks (compaction.zig:806-886), counted from the job's first survivor. So:
 
-1. `split_points`: P-1 splitter keys by merge-path co-ranking over A ∪ B
-   (A-first on equal keys, like the reference's merge), cuts moved back to the
-   start of the splitter's equal-key run. Every rank computes the same cuts.
+1. Splitters: P-1 keys, and the cuts (lower bounds of each splitter in A
+   and in B), identical on every rank without communication. Two ways:
+   `block_splitters` + `block_cuts` (what a rank on a node uses): the
+   splitters are data-block first keys (TableIndex.keys_min of the input
+   tables' index blocks, schema.zig:80-260) balanced by the blocks' value
+   counts, and each cut is a lower bound inside the one data block of A and
+   of each B table that can hold it, so a rank reads the index keys plus at
+   most two data blocks per input table, and stages only the blocks of its
+   own range (`rank_blocks`); or `split_points`, exact merge-path
+   co-ranking over A ∪ B, for a caller that holds every key anyway.
 2. Phase 1: each rank compacts its key range values-only (bodies in scratch
    data-block slots, no headers or checksums) and takes its survivor count c_p.
 3. Exchange (the only collective): all-gather of the counts c_p, then of each
@@ -86,6 +93,94 @@ def split_points(a_limbs: list, na: int, b_limbs: list, nb: int, world: int) -> 
         cuts.append((max(a_cut, pa), max(b_cut, pb)))
     cuts.append((na, nb))
     return cuts
+
+
+class BlockedSide:
+    """One input side (A, or B's tables concatenated) as its data blocks:
+    `first_keys[j]` = the key of block j's first value (from the index
+    block), `counts[j]` its values, and `keys(j)` the limb arrays of block j
+    (read on demand: only boundary blocks are ever asked for)."""
+
+    def __init__(self, first_keys: list, counts: list, keys):
+        self.first_keys, self.counts, self.keys = first_keys, [int(c) for c in counts], keys
+        self.starts = [0]
+        for c in self.counts:
+            self.starts.append(self.starts[-1] + c)
+
+    @property
+    def n(self) -> int:
+        return self.starts[-1]
+
+    def lower_bound(self, key: tuple) -> int:
+        """First global index whose key is not below `key`: inside the last
+        block whose first key is below it (one block read)."""
+        j = -1
+        for i, fk in enumerate(self.first_keys):  # index-block keys: host, tiny
+            if fk < key:
+                j = i
+            else:
+                break
+        if j < 0:
+            return 0
+        return self.starts[j] + lower_bound(self.keys(j), self.counts[j], key)
+
+    @classmethod
+    def from_values(cls, limbs: list, n: int, block_values: int) -> "BlockedSide":
+        """A side whose values are host arrays (tests and tools)."""
+        starts = list(range(0, n, block_values))
+        counts = [min(block_values, n - s) for s in starts]
+        first = [_key(limbs, s) for s in starts]
+        return cls(first, counts, lambda j: [l[starts[j]:starts[j] + counts[j]] for l in limbs])
+
+
+def block_splitters(a: BlockedSide, b: BlockedSide, world: int) -> list:
+    """P-1 splitter keys: data-block first keys of A ∪ B (index-block data
+    only), the p-th being the first whose blocks before it hold at least
+    p/world of the values. Identical on every rank."""
+    blocks = sorted([(k, c) for k, c in zip(a.first_keys, a.counts)] + [(k, c) for k, c in zip(b.first_keys, b.counts)])
+    total = a.n + b.n
+    out, acc, i = [], 0, 0
+    for p in range(1, world):
+        goal = p * total // world
+        while i < len(blocks) and acc + blocks[i][1] <= goal:
+            acc += blocks[i][1]
+            i += 1
+        # the block that would cross the goal starts the next range (or the end: nothing left)
+        out.append(blocks[i][0] if i < len(blocks) else None)
+    return out
+
+
+def block_cuts(a: BlockedSide, b: BlockedSide, splitters: list) -> list:
+    """[(a_cut, b_cut)] * (world + 1) from the splitter keys: each cut is the
+    splitter's lower bound in A and in B, so every value with that key (and
+    every equal key) falls to the same rank. Cuts never move backwards."""
+    cuts = [(0, 0)]
+    for s in splitters:
+        if s is None:
+            cuts.append((a.n, b.n))
+            continue
+        pa, pb = cuts[-1]
+        cuts.append((max(a.lower_bound(s), pa), max(b.lower_bound(s), pb)))
+    cuts.append((a.n, b.n))
+    return cuts
+
+
+def rank_blocks(side: BlockedSide, lo: int, hi: int) -> list:
+    """[(block, start, count)]: the parts of data blocks holding the side's
+    global values [lo, hi) — all a rank stages of that side."""
+    out = []
+    for j, c in enumerate(side.counts):
+        s = side.starts[j]
+        x, y = max(lo, s), min(hi, s + c)
+        if x < y:
+            out.append((j, x - s, y - x))
+    return out
+
+
+def staged_bytes(cuts: list, rank: int, value_size: int) -> int:
+    """Input bytes rank `rank` stages: its own range of A and B, nothing else."""
+    (a0, b0), (a1, b1) = cuts[rank], cuts[rank + 1]
+    return ((a1 - a0) + (b1 - b0)) * value_size
 
 
 def range_segments(counts: list, lo: int, hi: int) -> list:
@@ -246,9 +341,11 @@ class SplitResult:
     plan: TablePlan
 
 
-def compact_split(engine, job, cuts: list, exchange, rank: int) -> SplitResult:
-    """Run rank `rank`'s share of `job` (an engine.Job whose segments hold the
-    WHOLE job's inputs, on this GPU) split at `cuts` (split_points)."""
+def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = False) -> SplitResult:
+    """Run rank `rank`'s share of `job` split at `cuts` (block_cuts or
+    split_points). With staged=True the job's segments hold only this rank's
+    range [cuts[rank], cuts[rank+1]) of A and of B (what rank_blocks named,
+    staged on this GPU); otherwise the whole job's inputs, sliced here."""
     from .engine import Job
     tree, bs = job.tree, engine.block_size
     lay = engine.layout(tree)
@@ -258,7 +355,12 @@ def compact_split(engine, job, cuts: list, exchange, rank: int) -> SplitResult:
         return [(segs[s][0] + st * vs, n) for s, st, n in range_segments([n for _, n in segs], lo, hi)]
 
     (a_lo, b_lo), (a_hi, b_hi) = cuts[rank], cuts[rank + 1]
-    seg_a, seg_b = sub(job.segments_a, a_lo, a_hi), sub(job.segments_b, b_lo, b_hi)
+    if staged:
+        seg_a, seg_b = list(job.segments_a), list(job.segments_b)
+        assert sum(n for _, n in seg_a) == a_hi - a_lo and sum(n for _, n in seg_b) == b_hi - b_lo, \
+            "staged segments are not this rank's range"
+    else:
+        seg_a, seg_b = sub(job.segments_a, a_lo, a_hi), sub(job.segments_b, b_lo, b_hi)
     n = (a_hi - a_lo) + (b_hi - b_lo)
     db = -(-n // vcm)
     nblocks = db + -(-db // dbcm)
