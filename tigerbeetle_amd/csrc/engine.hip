@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <ctime>
 #include <new>
@@ -1412,9 +1413,16 @@ tbc_status tbc_batch_wait(tbc_batch *b) {
     if (!b->children.empty()) return parent_finish(b, true);
     hipSetDevice(b->engine->device);
     // Poll like the adapter's event loop would (tbc_batch_poll), instead of a
-    // blocking hipEventSynchronize whose OS wake-up adds milliseconds of jitter.
+    // blocking hipEventSynchronize whose OS wake-up adds milliseconds of
+    // jitter: spin for the first 200 us, then yield the core between polls
+    // (20 us sleeps), so a long batch does not hold a host core.
     hipError_t q;
+    const auto t0 = std::chrono::steady_clock::now();
     while ((q = hipEventQuery(b->done)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+            const timespec ts{0, 20000};
+            nanosleep(&ts, nullptr);
+        }
     }
     if (q != hipSuccess) {
         fprintf(stderr, "tbc: batch failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);

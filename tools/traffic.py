@@ -55,12 +55,17 @@ def main() -> None:
     fetch = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(src, "write"), "WRITE_SIZE")
     md5 = open(os.path.join(src, "lib.md5")).read().split()[0]
+    bench_cfg = None
+    try:
+        bench_cfg = json.loads(open(os.path.join(src, "bench.json")).read())["config"].get("baseline_config")
+    except (OSError, ValueError, KeyError):
+        pass
     sq = {}
     if glob.glob(os.path.join(src, "sq", "**", "*counter_collection.csv"), recursive=True):
         for c in SQ_COUNTERS:
             for k, v in counters(os.path.join(src, "sq"), c).items():
                 sq.setdefault(k, {})[c] = v
-    out = {"lib_md5": md5, "note": "bytes per launch; fetch = 2 x FETCH_SIZE KiB (gfx950 correction), "
+    out = {"lib_md5": md5, "baseline_config": bench_cfg, "note": "bytes per launch; fetch = 2 x FETCH_SIZE KiB (gfx950 correction), "
                                    "write = WRITE_SIZE KiB", "kernels": {}}
     for k in sorted(avg_ns):
         f = fetch.get(k, 0.0) * 1024 * 2
