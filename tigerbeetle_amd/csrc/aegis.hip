@@ -25,6 +25,8 @@
 // TableInfo.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "tbc_internal.h"
 
 namespace tbc {
@@ -636,44 +638,6 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
 // their value into place with 16-byte loads and stores. Progress (body bytes
 // final and visible) goes to *prog in 256-byte units, after the stores have
 // completed, for the chain waves of the workgroup (BodyMsg::ready).
-struct SegCursor {
-    const uint64_t *ptrs;
-    const uint32_t *pre;
-    uint32_t nseg, seg, lo, hi;
-    uint64_t base;
-    __device__ __forceinline__ void load() {
-        lo = gld<uint32_t>(pre + seg);
-        hi = gld<uint32_t>(pre + seg + 1);
-        base = gld<uint64_t>(ptrs + seg);
-    }
-    __device__ __forceinline__ void init(const Stream &s, uint32_t seg0) {
-        ptrs = s.seg_ptr;
-        pre = s.seg_pre;
-        nseg = s.nseg;
-        seg = nseg ? (seg0 < nseg ? seg0 : nseg - 1) : 0;
-        if (nseg) load();
-        else lo = hi = 0, base = 0;
-    }
-    // Move forward to the segment holding element `idx` (wave-uniform).
-    __device__ __forceinline__ void advance(uint32_t idx) {
-        while (seg + 1 < nseg && idx >= hi) {
-            seg++;
-            load();
-        }
-    }
-    // Address of element idx >= lo (per lane; usually inside the cursor's segment).
-    __device__ __forceinline__ const uint8_t *elem(uint32_t idx, uint32_t vs) const {
-        uint32_t s = seg, l = lo, h = hi;
-        uint64_t b = base;
-        while (idx >= h && s + 1 < nseg) {
-            s++;
-            l = h;
-            h = gld<uint32_t>(pre + s + 1);
-            b = gld<uint64_t>(ptrs + s);
-        }
-        return (const uint8_t *)(uintptr_t)b + (size_t)(idx - l) * vs;
-    }
-};
 
 // A job whose survivors are under a quarter of its merged positions (heavy
 // dedup, e.g. an object tree updated many times per key) leaves its survivors
@@ -684,28 +648,6 @@ __device__ __forceinline__ bool sparse_job(const JobDesc &j, const JobResultDev 
     return res[j.job_index].value_count * 4 < (uint64_t)(j.a.n + j.b.n);
 }
 
-// Copy `count` staged values (source and destination pointers in LDS), 16
-// bytes per lane: eight loads in flight per lane before their stores (a
-// load-store loop keeps one, and is latency-bound).
-__device__ __forceinline__ void copy_staged(const uint64_t *src, const uint64_t *dst, uint32_t count,
-                                            uint32_t cpv_log) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t total = count << cpv_log;
-    const uint32_t qmask = (1u << cpv_log) - 1;
-    for (uint32_t c0 = 0; c0 < total; c0 += 64 * 8) {
-        u32x4 v[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; u++) {
-            const uint32_t c = c0 + lane + 64 * u;
-            if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)src[c >> cpv_log] + 16 * (c & qmask));
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 8; u++) {
-            const uint32_t c = c0 + lane + 64 * u;
-            if (c < total) gst<u32x4>((uint8_t *)(uintptr_t)dst[c >> cpv_log] + 16 * (c & qmask), v[u]);
-        }
-    }
-}
 
 __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint32_t cnt, const uint64_t *status,
                                              const uint64_t *masks, const uint32_t *block_tile,
@@ -1205,13 +1147,13 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, bool maybe_sparse,
                   void *stream,
-                  void (*mark)(void *, const char *), void *mark_ctx) {
+                  void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
     if (values_only) {
         // Survivors only (TBC_COMPACTION_VALUES_ONLY): the bodies, no chains
         // and no index blocks.
-        if (total_dblocks) {
+        if (total_dblocks && !bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
             hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
                                d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
@@ -1220,7 +1162,9 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         if (mark) mark(mark_ctx, "assemble");
         return 0;
     }
-    if (total_dblocks && waves <= kFusedMaxChainWaves) {
+    static const uint32_t fused_max = getenv("TBC_FUSED_MAX_WAVES") ? (uint32_t)atoi(getenv("TBC_FUSED_MAX_WAVES"))
+                                                                    : kFusedMaxChainWaves; // A/B measurement only
+    if (total_dblocks && waves <= fused_max) {
         // Latency regime: every chain is in flight at once; producers fill
         // the bodies while the chains absorb them.
         if (maybe_sparse) { // heavy-dedup jobs: bodies first, parallel (sparse_job decides on device)
@@ -1243,11 +1187,13 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         // chain workgroups leave the assemble waves too little of each CU.)
         // The counts stay as a check: a chain whose block is short of values
         // reports an invariant error instead of checksumming a partial body.
-        const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-        hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status, d_masks,
-                           d_splits, d_ready, (const JobResultDev *)d_results);
-        if (hipGetLastError() != hipSuccess) return -1;
-        if (mark) mark(mark_ctx, "assemble");
+        if (!bodies_done) {
+            const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
+            if (hipGetLastError() != hipSuccess) return -1;
+            if (mark) mark(mark_ctx, "assemble");
+        }
         const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
         const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
         hipLaunchKernelGGL(k_data_blocks<false>, dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs, njobs,
@@ -1269,13 +1215,15 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
 int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks,
                         uint32_t *d_ready, const JobResultDev *d_results, const uint64_t *d_status,
                         const uint64_t *d_masks, const SplitDesc *d_splits, void *stream,
-                        void (*mark)(void *, const char *), void *mark_ctx) {
+                        void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done) {
     hipStream_t s = (hipStream_t)stream;
     if (total_dblocks) {
-        const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-        hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                           d_masks, d_splits, d_ready, d_results);
-        if (hipGetLastError() != hipSuccess) return -1;
+        if (!bodies_done) {
+            const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                               d_masks, d_splits, d_ready, d_results);
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
         hipLaunchKernelGGL(k_index_layout, dim3((total_dblocks + 255) / 256), dim3(256), 0, s, d_jobs, njobs,
                            total_dblocks, d_results);
         if (hipGetLastError() != hipSuccess) return -1;

@@ -27,6 +27,8 @@ using namespace tbc;
 namespace {
 
 constexpr uint64_t kDefaultArena = 256ull << 20;
+// aegis.hip kFusedMaxChainWaves: above it a batch is in the throughput regime.
+constexpr uint64_t kFusedChainWaves = 2048;
 constexpr uint64_t kPinnedArena = 64ull << 20;
 constexpr uint32_t kIndexLdsMax = 16384; // k_index_blocks LDS image
 constexpr int kMaxMarks = 16;
@@ -1112,7 +1114,9 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order + sz_checks + sz_resolve;
     const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
-    const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8, 256);
+    // tile status, block tiles, per-block landed counts, the assembling
+    // merge's look-back words (one per tile) and its ticket counters
+    const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8 + 8ull * tiles + 16 + 32, 256);
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
     b->dev_top = e->dev.top;
@@ -1132,6 +1136,20 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
     uint32_t *d_block_tile = (uint32_t *)(d_status + tiles);
     uint32_t *d_ready = d_block_tile + dblocks;
+    uint64_t *d_lookback = (uint64_t *)(uintptr_t)align_up((uint64_t)(uintptr_t)(d_ready + dblocks + 2), 8);
+    uint32_t *d_ticket = (uint32_t *)(d_lookback + tiles);
+    // The merge can write the bodies itself (tiles take their output offsets
+    // by look-back, merge.hip k_merge_tile<KIND, true>) instead of
+    // k_assemble walking its masks afterwards. Measured on MI355X it is not
+    // a win where it applies (config 5 alone 16.1 -> 15.1 ms, but grouped
+    // 14.3 -> 20.8 ms and the config 1 replay 75 -> 79 ms: the look-back
+    // serialises tiles that then copy), so it is off unless asked for
+    // (TBC_MERGE_BODIES=1, A/B measurement; parity-tested either way).
+    static const bool merge_bodies_env = getenv("TBC_MERGE_BODIES") != nullptr;
+    const bool throughput = (uint64_t)(dblocks + 1) / 2 > kFusedChainWaves;
+    const bool merge_bodies = merge_bodies_env && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
+                                                   throughput);
+    uint64_t *m_lb = merge_bodies ? d_lookback : nullptr;
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
     b->h_results = (JobResultDev *)(hbase + sz_in);
@@ -1236,10 +1254,10 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                      grid0->base, grid0->block_count, e->block_size, d_res, s) == 0;
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
-                                     e->masks, d_splits, s, mark_cb, b) == 0;
+                                     e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % tbc_engine::kTails;
         hipStream_t T = e->tail[ti];
@@ -1270,10 +1288,10 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // chains run beside the next group's merge and body assembly.
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
-                                     e->masks, d_splits, s, mark_cb, b) == 0;
+                                     e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % tbc_engine::kTails;
         hipStream_t T = e->tail[ti];
@@ -1289,11 +1307,11 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     } else {
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
         if (ok && count)
             ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos,
                                d_status, e->masks, d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0,
-                               maybe_sparse, s, mark_cb, b) == 0;
+                               maybe_sparse, s, mark_cb, b, merge_bodies) == 0;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
         ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     }
@@ -1310,7 +1328,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
 // kFusedMaxChainWaves): it is split into job groups that pipeline (each
 // group's chains beside the next group's merge and bodies).
 constexpr uint64_t kGroupMinChainWaves = 2048;
-constexpr uint32_t kMaxGroups = 6;
+constexpr uint32_t kMaxGroups = 4; // config 5: 1 -> 16.1, 2 -> 14.6, 3 -> 14.4, 4 -> 14.3, 6 -> 17.2 ms
 
 tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
@@ -1330,7 +1348,9 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
             waves += (n[i] + L.vcm - 1) / L.vcm / 2;
         }
         static const uint32_t max_groups = getenv("TBC_GROUPS") ? (uint32_t)atoi(getenv("TBC_GROUPS")) : kMaxGroups;
-        if (waves > kGroupMinChainWaves && max_groups > 1) groups = std::min<uint32_t>(max_groups, count);
+        static const uint64_t min_waves = getenv("TBC_FUSED_MAX_WAVES") ? (uint64_t)atoi(getenv("TBC_FUSED_MAX_WAVES"))
+                                                                       : kGroupMinChainWaves;
+        if (waves > min_waves && max_groups > 1) groups = std::min<uint32_t>(max_groups, count);
     }
     if (groups == 1) return submit_impl(e, jobs_in, count, false, out);
     // Contiguous groups of about equal input (job order kept inside a group).

@@ -119,14 +119,25 @@ template <int KL> struct TileShared {
     uint32_t wave_sums[kMergeThreads / 64];
 };
 
-template <int KIND>
+// Look-back words of the assembling merge (ASM): flag in the top two bits,
+// survivors (aggregate, or inclusive prefix of the job's tiles) below.
+constexpr uint64_t kMlbAggregate = 1ull << 62, kMlbPrefix = 2ull << 62, kMlbCount = (1ull << 62) - 1;
+
+template <int KIND, bool ASM>
 __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
                                                               uint32_t order_offset, const SplitDesc *splits,
-                                                              uint64_t *status, uint64_t *masks) {
+                                                              uint64_t *status, uint64_t *masks, uint64_t *lookback,
+                                                              uint32_t *ticket, uint32_t *ready) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const TileRef ref = order[order_offset + blockIdx.x];
+    // ASM: tiles are taken in ticket order (the order table interleaves the
+    // jobs tile by tile), so every tile a tile looks back on belongs to a
+    // workgroup that is running or done.
+    __shared__ uint32_t s_ticket;
+    if (ASM && tid == 0) s_ticket = atomicAdd(ticket, 1u);
+    if (ASM) __syncthreads();
+    const TileRef ref = order[order_offset + (ASM ? s_ticket : blockIdx.x)];
     const JobDesc &j = jobs[ref.job];
     const uint32_t t = ref.tile;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
@@ -286,18 +297,123 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
         aw |= __shfl_xor(aw, o, 64);
     }
     uint64_t *m = masks + (size_t)(j.tile_base + t) * (2 * kMaskWords);
+    __shared__ uint64_t s_m[2 * kMaskWords];
     if (tid % kThreadsPerWord == 0) {
         gst<uint64_t>(m + tid / kThreadsPerWord, sw);
         gst<uint64_t>(m + kMaskWords + tid / kThreadsPerWord, aw);
+        if (ASM) {
+            s_m[tid / kThreadsPerWord] = sw;
+            s_m[kMaskWords + tid / kThreadsPerWord] = aw;
+        }
     }
     uint32_t sum = __builtin_popcount(sbits);
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     if (lane == 0) sh.wave_sums[tid >> 6] = sum;
     __syncthreads();
-    if (tid == 0) {
-        uint32_t cnt = 0;
-        for (uint32_t w = 0; w < kMergeThreads / 64; w++) cnt += sh.wave_sums[w];
-        gst<uint64_t>(status + j.tile_base + t, (uint64_t)cnt);
+    uint32_t cnt = 0;
+    for (uint32_t w = 0; w < kMergeThreads / 64; w++) cnt += sh.wave_sums[w];
+    if (tid == 0) gst<uint64_t>(status + j.tile_base + t, (uint64_t)cnt);
+    if constexpr (ASM) {
+        // The job's survivors before this tile: decoupled look-back, wave 0
+        // reading 64 predecessors per round trip (nearest first; before the
+        // job's first tile reads as a prefix of 0).
+        __shared__ uint32_t s_excl;
+        if (tid < 64) {
+            uint64_t *lb = lookback + j.tile_base;
+            if (tid == 0) __hip_atomic_store(&lb[t], kMlbAggregate | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t excl = 0;
+            int64_t top = (int64_t)t - 1;
+            for (uint32_t spins = 0;;) {
+                const int64_t idx = top - (int64_t)lane;
+                const uint64_t v = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : kMlbPrefix;
+                const uint64_t fl = v >> 62;
+                const uint64_t pre = __ballot(fl == 2);
+                const uint32_t stop = pre ? __builtin_ctzll(pre) : 64u; // nearest prefix
+                const bool mine = lane <= stop;
+                if (__ballot(mine && fl == 0)) { // a tile up to the prefix has not published yet
+                    if (++spins > (1u << 18)) break; // bounded (a broken invariant, not a hang)
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint64_t c = mine ? (v & kMlbCount) : 0;
+                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+                excl += c;
+                if (stop < 64) break;
+                top -= 64;
+            }
+            if (tid == 0) {
+                __hip_atomic_store(&lb[t], kMlbPrefix | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_excl = (uint32_t)excl;
+            }
+        }
+        // Survivors into their output slots (k_assemble's walk, masks from LDS).
+        __shared__ uint32_t s_pre[3][kMaskWords + 1]; // survivors, A taken, B taken before word w
+        __shared__ uint64_t s_src[kMergeThreads / 64][64], s_dst[kMergeThreads / 64][64];
+        const uint32_t wv = tid >> 6;
+        const uint64_t lt = (1ull << lane) - 1;
+        auto valid_of = [&](uint32_t w) -> uint64_t {
+            const uint32_t pos0 = d0 + 64 * w;
+            return pos0 >= n ? 0ull : (n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1));
+        };
+        if (tid < kMaskWords) {
+            s_pre[0][tid + 1] = __builtin_popcountll(s_m[tid]);
+            s_pre[1][tid + 1] = __builtin_popcountll(s_m[kMaskWords + tid]);
+            s_pre[2][tid + 1] = __builtin_popcountll(valid_of(tid) & ~s_m[kMaskWords + tid]);
+        }
+        __syncthreads();
+        if (tid < 3) {
+            uint32_t acc = 0;
+            s_pre[tid][0] = 0;
+            for (uint32_t w = 1; w <= kMaskWords; w++) {
+                acc += s_pre[tid][w];
+                s_pre[tid][w] = acc;
+            }
+        }
+        __syncthreads();
+        const uint32_t out0 = s_excl;
+        const uint32_t vcm = j.vcm;
+        SegCursor ca, cb;
+        ca.init(j.a, s0.seg_a);
+        cb.init(j.b, s0.seg_b);
+        const uint32_t cpv_log = __builtin_ctz(vs >> 4);
+        for (uint32_t w = wv; w < kMaskWords; w += kMergeThreads / 64) {
+            if (d0 + 64 * w >= n) break;
+            const uint64_t smk = s_m[w], amk = s_m[kMaskWords + w];
+            const uint32_t ns = __builtin_popcountll(smk);
+            if (ns == 0) continue;
+            const uint64_t valid = valid_of(w);
+            const uint32_t ab = i0 + s_pre[1][w], bb = j0 + s_pre[2][w];
+            ca.advance(ab);
+            cb.advance(bb);
+            if ((smk >> lane) & 1) {
+                const uint32_t r = __builtin_popcountll(smk & lt);
+                const uint32_t o = out0 + s_pre[0][w] + r;
+                const uint8_t *src = ((amk >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(amk & lt), vs)
+                                                         : cb.elem(bb + __builtin_popcountll(valid & ~amk & lt), vs);
+                const uint32_t k = o / vcm;
+                s_src[wv][r] = (uint64_t)(uintptr_t)src;
+                s_dst[wv][r] = (uint64_t)(uintptr_t)(block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize +
+                                                     (size_t)(o - k * vcm) * vs);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            copy_staged(s_src[wv], s_dst[wv], ns, cpv_log);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        // Survivors landed per data block (the chains check them).
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t o = out0;
+            const uint32_t end = out0 + cnt;
+            while (o < end) {
+                const uint32_t k = o / vcm;
+                const uint32_t e = (k + 1) * vcm < end ? (k + 1) * vcm : end;
+                __hip_atomic_fetch_add(ready + j.dblock_base + k, e - o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                o = e;
+            }
+        }
     }
 }
 
@@ -357,7 +473,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const JobDesc *jobs,
 template <int KIND>
 static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
                        SplitDesc *d_splits, uint64_t *d_status, uint64_t *d_masks, const TileRef *d_order,
-                       hipStream_t s) {
+                       uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready, hipStream_t s) {
     const JobDesc &f = h_jobs[first];
     const JobDesc &l = h_jobs[first + count - 1];
     const uint32_t split_off = f.split_base;
@@ -367,9 +483,13 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
     (void)phase;
     (void)split_off;
     (void)nsplits;
-    if (ntiles)
-        hipLaunchKernelGGL(k_merge_tile<KIND>, dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,
-                           (const SplitDesc *)d_splits, d_status, d_masks);
+    if (ntiles && d_lookback)
+        hipLaunchKernelGGL((k_merge_tile<KIND, true>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
+                           tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket + KIND,
+                           d_ready);
+    else if (ntiles)
+        hipLaunchKernelGGL((k_merge_tile<KIND, false>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
+                           tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket, d_ready);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -378,7 +498,8 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
 // d_block_tile one u32 per data block (upper bound); results start zeroed.
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
                  uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
-                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
+                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx,
+                 uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready) {
     hipStream_t s = (hipStream_t)stream;
     auto for_each_kind = [&](auto fn) {
         int first = 0;
@@ -393,10 +514,10 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     auto phase = [&](int ph) {
         return for_each_kind([&](uint32_t kind, int first, int count) {
             switch (kind) {
-            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
-            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
-            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
-            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, s);
+            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
+            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
+            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
+            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
             }
         });
     };

@@ -162,6 +162,70 @@ __device__ inline uint32_t grid_header_check(const JobDesc &j, const InputCheck 
     return ok ? 0u : 7u;
 }
 
+// Cursor over a stream's segments (input data blocks): the segment holding
+// an element index, moving forward only (wave-uniform advance).
+struct SegCursor {
+    const uint64_t *ptrs;
+    const uint32_t *pre;
+    uint32_t nseg, seg, lo, hi;
+    uint64_t base;
+    __device__ __forceinline__ void load() {
+        lo = gld<uint32_t>(pre + seg);
+        hi = gld<uint32_t>(pre + seg + 1);
+        base = gld<uint64_t>(ptrs + seg);
+    }
+    __device__ __forceinline__ void init(const Stream &s, uint32_t seg0) {
+        ptrs = s.seg_ptr;
+        pre = s.seg_pre;
+        nseg = s.nseg;
+        seg = nseg ? (seg0 < nseg ? seg0 : nseg - 1) : 0;
+        if (nseg) load();
+        else lo = hi = 0, base = 0;
+    }
+    // Move forward to the segment holding element `idx` (wave-uniform).
+    __device__ __forceinline__ void advance(uint32_t idx) {
+        while (seg + 1 < nseg && idx >= hi) {
+            seg++;
+            load();
+        }
+    }
+    // Address of element idx >= lo (per lane; usually inside the cursor's segment).
+    __device__ __forceinline__ const uint8_t *elem(uint32_t idx, uint32_t vs) const {
+        uint32_t s = seg, l = lo, h = hi;
+        uint64_t b = base;
+        while (idx >= h && s + 1 < nseg) {
+            s++;
+            l = h;
+            h = gld<uint32_t>(pre + s + 1);
+            b = gld<uint64_t>(ptrs + s);
+        }
+        return (const uint8_t *)(uintptr_t)b + (size_t)(idx - l) * vs;
+    }
+};
+
+// Copy `count` staged values (source and destination pointers in LDS), 16
+// bytes per lane: eight loads in flight per lane before their stores (a
+// load-store loop keeps one, and is latency-bound).
+__device__ __forceinline__ void copy_staged(const uint64_t *src, const uint64_t *dst, uint32_t count,
+                                            uint32_t cpv_log) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t total = count << cpv_log;
+    const uint32_t qmask = (1u << cpv_log) - 1;
+    for (uint32_t c0 = 0; c0 < total; c0 += 64 * 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t c = c0 + lane + 64 * u;
+            if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)src[c >> cpv_log] + 16 * (c & qmask));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t c = c0 + lane + 64 * u;
+            if (c < total) gst<u32x4>((uint8_t *)(uintptr_t)dst[c >> cpv_log] + 16 * (c & qmask), v[u]);
+        }
+    }
+}
+
 __device__ inline const JobDesc &job_of_result(const JobDesc *jobs, int njobs, uint32_t job_index) {
     int found = 0;
     for (int k = 0; k < njobs; k++)
@@ -186,15 +250,19 @@ __device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F bas
 // Kernel launchers (implemented in the .hip translation units).
 struct hipStream_t_;
 namespace tbc {
+// d_lookback (one u64 per tile, zeroed), d_ticket (4 u32, zeroed) and d_ready
+// given: the merge also writes every survivor into its output block (the
+// throughput regime's body assembly, fused; tiles take look-back offsets).
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
                  uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
-                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+                 JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx,
+                 uint64_t *d_lookback = nullptr, uint32_t *d_ticket = nullptr, uint32_t *d_ready = nullptr);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, bool maybe_sparse,
                   void *stream,
-                  void (*mark)(void *, const char *), void *mark_ctx);
+                  void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done = false);
 int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uint32_t count, uint32_t block_size,
                           uint8_t *d_out, void *stream);
 // Grid inputs of a batch (engine.hip): resolve data blocks from the index
@@ -208,7 +276,7 @@ int launch_grid_expect(const ResolveItem *d_items, uint32_t count, InputCheck *d
 int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks,
                         uint32_t *d_ready, const JobResultDev *d_results, const uint64_t *d_status,
                         const uint64_t *d_masks, const SplitDesc *d_splits, void *stream,
-                        void (*mark)(void *, const char *), void *mark_ctx);
+                        void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done);
 int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
                        JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
