@@ -202,6 +202,41 @@ def test_sort_values_low_limbs_in_order(engine, oracle_lib):
         assert np.array_equal(got, want), spec.name
 
 
+def test_sort_truncated_top_bytes_and_rescue(engine, oracle_lib):
+    """Tables with many varying key bytes are sorted on their top bytes only
+    and each run of equal top bytes is ordered by k_sort_fixup (random u128
+    and u64 fields put in timestamp order); a table whose top bytes cluster
+    into runs too long to fix up is sorted again by k_sort_rescue. All equal
+    to the oracle's stable sort, equal keys included."""
+    rng = np.random.default_rng(16)
+    n = 300_001
+    ts = np.arange(1, n + 1, dtype=np.uint64) * np.uint64(7)
+    tables, wants = [], []
+
+    def add(name, limbs):
+        spec = trees.BY_NAME[name]
+        vals = workloads.values_from_keys(spec, limbs, np.zeros(n, bool), rng)
+        t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                            spec.value_count_max, 1 << 20)
+        wants.append(oracle_lib.sort_values(t, vals))
+        tables.append((spec, engine.upload(vals, pad=16), n))
+
+    lo = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    hi = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    lo[: n // 3], hi[: n // 3] = lo[n // 3: 2 * (n // 3)], hi[n // 3: 2 * (n // 3)]  # repeated fields: runs ordered by timestamp
+    add("transfers.user_data_128", [ts, lo, hi])
+    add("transfers.user_data_64", [ts, rng.integers(0, 1 << 63, n, dtype=np.uint64)])
+    # top four varying bytes take two values: runs of ~n/2 -> rescue
+    c = rng.integers(1, 3, n, dtype=np.uint64)
+    field = c * np.uint64(0x0101010100) + rng.integers(0, 256, n, dtype=np.uint64)
+    add("transfers.user_data_64", [ts, field])
+    engine.sort_values_batch(tables)
+    engine.synchronize()
+    for (spec, buf, _), want in zip(tables, wants):
+        got = buf.download(n * spec.value_size).reshape(n, spec.value_size)
+        assert np.array_equal(got, want), spec.name
+
+
 @pytest.mark.parametrize("name", ["accounts.user_data_64", "transfers.debit_account_id"])
 def test_sort_composite_key_cases(engine, oracle_lib, name):
     """composite_key.zig:88-124's cases on the device's key_from_value: the

@@ -54,6 +54,8 @@ constexpr uint32_t kSortTile = kSortThreads * kSortRounds; // 2,048 items
 constexpr uint32_t kRadix = 256;
 constexpr uint32_t kMaxLimbs = 3;
 constexpr uint32_t kMaxPasses = 8 * kMaxLimbs;
+constexpr uint32_t kTopBytes = 4;   // truncated sorts keep at least this many top bytes
+constexpr uint32_t kRunMax = 64;    // longest run of equal top bytes k_sort_fixup orders
 
 // Look-back words (64-bit): the pass launch's epoch in the top half (words
 // of earlier launches read as "not published", so the buffer is zeroed once,
@@ -75,7 +77,12 @@ struct SortSeg {
     uint32_t active;    // bit p: pass p moves this table's items (plan)
     uint32_t src_bits;  // bit p: pass p reads buffer 1
     uint32_t final_buf; // buffer the last pass would have written
+    uint32_t skip;      // packed bytes [0, skip): the table is in order on them
+    uint32_t top;       // truncated: passes cover only packed bytes [top, nbytes) (0: not truncated)
+    uint32_t overflow;  // truncated and a run of equal top bytes too long to fix up: rescued
+    uint32_t nact;      // passes of the table: pass q sorts on packed byte act[q]
     uint8_t byte_src[kMaxPasses]; // packed byte j = key byte byte_src[j] (limb * 8 + byte)
+    uint8_t act[kMaxPasses];
 };
 
 struct SortBatch {
@@ -274,20 +281,42 @@ __global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *
     uint32_t skip = 0;
     for (uint32_t j = 1; j < nb; j++)
         if (!((S.viol >> (j - 1)) & 1u)) skip = j;
-    uint32_t active = 0, src = 0, buf = 0;
-    for (uint32_t p = skip; p < nb; p++) {
-        active |= 1u << p;
-        src |= buf << p;
-        buf ^= 1u;
+    // Many varying bytes (random u64/u128 fields): sort on the top bytes
+    // only (at least kTopBytes, 10 bits beyond log2 n) and let k_sort_fixup
+    // order each run of equal top bytes by the full key -- when the top
+    // bytes' histograms predict short runs: n x prod(largest digit share)
+    // <= 1 if the bytes were independent. Clustered keys (config 3's Zipf
+    // accounts) keep every pass; a misprediction costs k_sort_rescue.
+    const uint32_t *h = hist + (size_t)s * kMaxPasses * kRadix;
+    const uint32_t log2n = 32 - __builtin_clz(S.n | 1);
+    const uint32_t top_bytes = (log2n + 10 + 7) / 8 > kTopBytes ? (log2n + 10 + 7) / 8 : kTopBytes;
+    uint32_t first = skip;
+    if (nb - skip > top_bytes) {
+        __shared__ uint32_t wmax[kRadix / 64];
+        float est = (float)S.n;
+        for (uint32_t b = nb - top_bytes; b < nb; b++) {
+            uint32_t mx = h[b * kRadix + d];
+            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+            if (lane == 0) wmax[wave] = mx;
+            __syncthreads();
+            mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            __syncthreads();
+            est *= (float)mx / (float)S.n;
+        }
+        if (est <= 1.0f) first = nb - top_bytes;
     }
+    uint32_t active = 0;
+    for (uint32_t p = first; p < nb; p++) active |= 1u << p;
     __syncthreads(); // every thread has read viol before thread 0 writes the plan
     if (d == 0) {
         S.active = active;
-        S.src_bits = src;
-        S.final_buf = buf;
-        if (active) atomicOr(&batch->active, active);
+        S.nact = nb - first;
+        for (uint32_t q = 0; q < nb - first; q++) S.act[q] = (uint8_t)(first + q);
+        S.final_buf = (nb - first) & 1u;
+        S.skip = skip;
+        S.top = first > skip ? first : 0;
+        if (nb > first) atomicOr(&batch->active, (1u << (nb - first)) - 1u); // pass q runs if some table has > q
     }
-    const uint32_t *h = hist + (size_t)s * kMaxPasses * kRadix;
     uint32_t *out = bins + (size_t)s * kMaxPasses * kRadix;
     for (uint32_t m = active; m; m &= m - 1) {
         const uint32_t p = __builtin_ctz(m);
@@ -338,8 +367,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
     __shared__ uint32_t s_idx[kSortTile];
     __shared__ uint8_t s_dig[kSortTile];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (!((batch->active >> p) & 1u)) return; // uniform: no table needs this pass
-    const uint32_t limb = p >> 3, shift = 8 * (p & 7);
+    if (!((batch->active >> p) & 1u)) return; // uniform: no table has this many passes
     const uint64_t ep = (uint64_t)epoch << 32;
     const uint64_t lt_mask = (1ull << lane) - 1;
     for (;;) {
@@ -351,14 +379,16 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
         if (t >= ntiles) return;
         const uint32_t sg = tile_seg[t];
         const SortSeg &S = segs[sg];
-        const uint32_t active = S.active;
-        if (!((active >> p) & 1u)) continue; // uniform: sorted table, skipped prefix
-        const bool last = (active >> p) == 1u;
+        const uint32_t nact = S.nact;
+        if (p >= nact) continue; // uniform: the table's passes are done (or it is in order)
+        const bool last = p + 1 == nact && S.top == 0; // truncated tables finish in k_sort_fixup
+        const uint32_t pb = S.act[p];                   // this pass's packed byte for the table
+        const uint32_t limb = pb >> 3, shift = 8 * (pb & 7);
         const uint32_t lt = t - S.tile_base;
         const uint32_t base = S.item_base + lt * kSortTile;
         const uint32_t m = (S.n - lt * kSortTile) < kSortTile ? (S.n - lt * kSortTile) : kSortTile;
         const uint32_t live = ((S.nbytes + 7) >> 3) - limb; // packed limbs [limb, ..) still move
-        const bool from1 = (S.src_bits >> p) & 1u;
+        const bool from1 = (p & 1u) != 0; // passes alternate buffers, the first reads buffer 0
         const uint64_t *ksrc = from1 ? keys1 : keys0;
         uint64_t *kdst = from1 ? keys0 : keys1;
         const uint32_t *isrc = from1 ? idx1 : idx0;
@@ -473,7 +503,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
         __syncthreads();
         // Destination of sorted position j = tid + 256 q: each digit's run
         // lands contiguously.
-        const uint32_t *bin = bins + ((size_t)sg * kMaxPasses + p) * kRadix;
+        const uint32_t *bin = bins + ((size_t)sg * kMaxPasses + pb) * kRadix;
         uint32_t dst[R];
 #pragma unroll
         for (uint32_t q = 0; q < R; q++) {
@@ -517,6 +547,169 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
                 if (j < m) gst<uint64_t>(kdst + (size_t)(limb + l) * N + dst[q], s_key[j]);
             }
         }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Truncated tables: the passes ordered the items by their top packed bytes
+// (stable); each run of equal top bytes is put in full-key order here (ties
+// by put order, i.e. by item index: stability), and every value is written.
+// One thread per sorted position; keys are re-read from the put-order copy.
+// A run longer than kRunMax marks the table for k_sort_rescue.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void packed_of(const SortSeg &S, const uint8_t *map, uint32_t item, uint64_t pk[3]) {
+    uint64_t k[3];
+    key_of(S.kind, S.copy + (size_t)item * S.vs, S.ts_off, k);
+    pack_key(map, S.nbytes, k, pk);
+}
+
+__device__ __forceinline__ bool top_eq(const uint64_t a[3], const uint64_t b[3], uint32_t top) {
+    // packed bytes [top, 24): limbs above top's limb whole, top's limb from byte top % 8
+    const uint32_t l0 = top >> 3, sh = 8 * (top & 7);
+    if ((a[l0] >> sh) != (b[l0] >> sh)) return false;
+    for (uint32_t l = l0 + 1; l < 3; l++)
+        if (a[l] != b[l]) return false;
+    return true;
+}
+
+__device__ __forceinline__ bool key_before(const uint64_t a[3], uint32_t ia, const uint64_t b[3], uint32_t ib) {
+    for (int l = 2; l >= 0; l--)
+        if (a[l] != b[l]) return a[l] < b[l];
+    return ia < ib;
+}
+
+__global__ __launch_bounds__(256) void k_sort_fixup(SortSeg *segs, const uint32_t *tile_seg, const uint32_t *idx0,
+                                                    const uint32_t *idx1) {
+    __shared__ uint8_t s_map[kMaxPasses];
+    const uint32_t sg = tile_seg[blockIdx.x];
+    const SortSeg S = segs[sg];
+    if (!S.top) return; // uniform: not truncated
+    if (threadIdx.x < kMaxPasses) s_map[threadIdx.x] = segs[sg].byte_src[threadIdx.x];
+    __syncthreads();
+    const uint32_t *idx = (S.final_buf ? idx1 : idx0) + S.item_base; // table-local sorted order
+    const uint32_t first = (blockIdx.x - S.tile_base) * kSortTile;
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const uint32_t i = first + r * kSortThreads + threadIdx.x;
+        if (i >= S.n) break;
+        const uint32_t me = idx[i] - S.item_base;
+        uint64_t pk[3];
+        packed_of(S, s_map, me, pk);
+        // run bounds [lo, hi) of equal top bytes around i
+        uint32_t lo = i, hi = i + 1;
+        bool too_long = false;
+        while (lo > 0) {
+            uint64_t q[3];
+            packed_of(S, s_map, idx[lo - 1] - S.item_base, q);
+            if (!top_eq(q, pk, S.top)) break;
+            if (i - --lo >= kRunMax) { too_long = true; break; }
+        }
+        while (!too_long && hi < S.n) {
+            uint64_t q[3];
+            packed_of(S, s_map, idx[hi] - S.item_base, q);
+            if (!top_eq(q, pk, S.top)) break;
+            if (++hi - lo > kRunMax) too_long = true;
+        }
+        if (too_long) {
+            atomicOr(&segs[sg].overflow, 1u);
+            continue;
+        }
+        uint32_t rank = 0;
+        for (uint32_t j = lo; j < hi; j++) {
+            if (j == i) continue;
+            const uint32_t other = idx[j] - S.item_base;
+            uint64_t q[3];
+            packed_of(S, s_map, other, q);
+            rank += key_before(q, other, pk, me) ? 1u : 0u;
+        }
+        const uint32_t to = lo + rank;
+        for (uint32_t b = 0; b < S.vs; b += 16)
+            gst<u32x4>(S.values + (size_t)to * S.vs + b, gld<u32x4>(S.copy + (size_t)me * S.vs + b));
+    }
+}
+
+// A truncated table whose top bytes left a run too long to fix up (rare:
+// keys clustered in their top bytes): one workgroup sorts it again, all its
+// varying bytes, LSD from the put-order copy, stable (ranks by wave match
+// ballots within 256-item chunks in order), then writes every value. Slow
+// but correct; the common case never launches work here.
+__global__ __launch_bounds__(256) void k_sort_rescue(SortSeg *segs, uint32_t N, uint64_t *keys0, uint64_t *keys1,
+                                                     uint32_t *idx0, uint32_t *idx1) {
+    __shared__ uint8_t s_map[kMaxPasses];
+    __shared__ uint32_t s_off[kRadix];
+    __shared__ uint32_t s_wc[4][kRadix];
+    __shared__ uint32_t s_wsum[4];
+    const SortSeg S = segs[blockIdx.x];
+    if (!S.overflow) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < kMaxPasses) s_map[tid] = segs[blockIdx.x].byte_src[tid];
+    __syncthreads();
+    const uint32_t nb = S.nbytes, pl = (nb + 7) >> 3, base = S.item_base;
+    for (uint32_t i = tid; i < S.n; i += 256) {
+        uint64_t pk[3];
+        packed_of(S, s_map, i, pk);
+        for (uint32_t l = 0; l < pl; l++) keys0[(size_t)l * N + base + i] = pk[l];
+        idx0[base + i] = i;
+    }
+    __syncthreads();
+    uint64_t *ks = keys0, *kd = keys1;
+    uint32_t *is = idx0, *id = idx1;
+    const uint64_t lt = (1ull << lane) - 1;
+    for (uint32_t p = S.skip; p < nb; p++) {
+        const uint32_t limb = p >> 3, sh = 8 * (p & 7);
+        s_off[tid] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < S.n; i += 256)
+            atomicAdd(&s_off[(uint32_t)(ks[(size_t)limb * N + base + i] >> sh) & 255u], 1u);
+        __syncthreads();
+        { // exclusive scan of the histogram (thread = digit)
+            const uint32_t c = s_off[tid];
+            uint32_t incl = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            if (lane == 63) s_wsum[wave] = incl;
+            __syncthreads();
+            uint32_t off = 0;
+            for (uint32_t w = 0; w < wave; w++) off += s_wsum[w];
+            s_off[tid] = off + incl - c;
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < S.n; c0 += 256) {
+            const uint32_t i = c0 + tid;
+            const bool in = i < S.n;
+            const uint32_t d = in ? (uint32_t)(ks[(size_t)limb * N + base + i] >> sh) & 255u : 0u;
+            for (uint32_t w = 0; w < 4; w++) s_wc[w][tid] = 0;
+            __syncthreads();
+            uint64_t peers = __ballot(in);
+            for (uint32_t b = 0; b < 8; b++) {
+                const uint64_t bal = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? bal : ~bal;
+            }
+            if (in && !(peers & lt)) s_wc[wave][d] = __builtin_popcountll(peers);
+            __syncthreads();
+            if (in) {
+                uint32_t pos = s_off[d] + __builtin_popcountll(peers & lt);
+                for (uint32_t w = 0; w < wave; w++) pos += s_wc[w][d];
+                for (uint32_t l = limb; l < pl; l++) kd[(size_t)l * N + base + pos] = ks[(size_t)l * N + base + i];
+                id[base + pos] = is[base + i];
+            }
+            __syncthreads();
+            s_off[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
+            __syncthreads();
+        }
+        uint64_t *tk = ks;
+        ks = kd;
+        kd = tk;
+        uint32_t *ti = is;
+        is = id;
+        id = ti;
+        __syncthreads();
+    }
+    for (uint32_t i = tid; i < S.n; i += 256) {
+        const uint32_t from = is[base + i];
+        for (uint32_t b = 0; b < S.vs; b += 16)
+            gst<u32x4>(S.values + (size_t)i * S.vs + b, gld<u32x4>(S.copy + (size_t)from * S.vs + b));
     }
 }
 
@@ -641,6 +834,9 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         hipLaunchKernelGGL(k_sort_pass, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, p, ntiles, N,
                            keys0, keys1, idx0, idx1, bins, status, (*epoch)++, counters);
     }
+    hipLaunchKernelGGL(k_sort_fixup, dim3(ntiles), dim3(256), 0, s, d_segs, (const uint32_t *)d_tile,
+                       (const uint32_t *)idx0, (const uint32_t *)idx1);
+    hipLaunchKernelGGL(k_sort_rescue, dim3(nseg), dim3(256), 0, s, d_segs, N, keys0, keys1, idx0, idx1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
