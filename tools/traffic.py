@@ -22,8 +22,8 @@ import sys
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0].replace("void ", "")
-    return n.split("::")[-1].split("<")[0]
+    n = name.split("(")[0].replace("void ", "").split("<")[0]  # template arguments may hold "::"
+    return n.split("::")[-1]
 
 
 def find(root: str, pattern: str) -> str:
