@@ -319,6 +319,16 @@ struct StepValuKey {
     }
 };
 
+// A step with `kMaskedMsg` takes the message word and its lane masks (the
+// lanes whose block absorbs it this step) instead of the selected word
+// (tools/aegis_lab.hip: hand-scheduled variants, measured no faster alone).
+template <class S, class = void> struct StepMasked {
+    static constexpr bool value = false;
+};
+template <class S> struct StepMasked<S, decltype((void)S::kMaskedMsg)> {
+    static constexpr bool value = S::kMaskedMsg;
+};
+
 // AEGIS-128L MAC of one message per 32-lane group. The two groups of a wave
 // may absorb messages of different lengths: both lengths are read into
 // scalars, so the control flow stays wave-uniform. Returns column c of the
@@ -353,13 +363,23 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     const uint32_t off_lo = 32 * k_lo + 4 * (lab_lo + c);
     const uint32_t off_hi = 32 * (k_lo + 4) + 4 * ((lab_lo ^ 4) + c);
     bool need[4];
+    uint64_t need_m[4];
+    uint32_t need_v[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) need[k] = ((p + k + 1) & 3) == 0;
+    for (int k = 0; k < 4; k++) {
+        need[k] = ((p + k + 1) & 3) == 0;
+        need_m[k] = __ballot(need[k]);
+        need_v[k] = need[k] ? ~0u : 0u;
+    }
 
 #define AEGIS_STEP(K, WLO, WHI)                                                   \
     do {                                                                          \
-        uint32_t m_ = need[(K)&3] ? ((K) < 4 ? (WLO) : (WHI)) : 0u;               \
-        x = Step::step(sT, tb, key_src, x, m_);                                   \
+        if constexpr (StepMasked<Step>::value) {                                  \
+            x = Step::step_m(sT, tb, key_src, x, (K) < 4 ? (WLO) : (WHI), need_m[(K)&3], need_v[(K)&3]); \
+        } else {                                                                  \
+            uint32_t m_ = need[(K)&3] ? ((K) < 4 ? (WLO) : (WHI)) : 0u;           \
+            x = Step::step(sT, tb, key_src, x, m_);                               \
+        }                                                                         \
     } while (0)
 
     // Lean loop over windows [w0, w1) of whole 32-byte blocks of both

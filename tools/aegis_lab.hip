@@ -27,6 +27,200 @@
 
 namespace tbc {
 
+// One AEGIS update step as a single hand-scheduled instruction sequence. A
+// chain wave alone on its SIMD issues one instruction at a time, so an
+// instruction between two updates costs latency unless it issues while the
+// table reads are in flight. The compiler's schedule of StepValuKey placed the
+// round-key selects and the message select after the first LDS wait (ten
+// instructions between the first table value returning and the next update's
+// addresses). Here the round key (row_ror:12 DPP + permlane16_swap + one
+// select with a precomputed lane mask), the message select and key ^ message
+// all issue under the reads' latency, and only the combining XORs follow the
+// returns. lgkmcnt waits count this block's own LDS reads, which complete in
+// order (older outstanding LDS/SMEM operations only make a wait conservative);
+// the block ends at lgkmcnt(0), so no result is pending when the compiler
+// takes over. The T-tables must sit at LDS address 0 (the address is
+// assembled by v_perm_b32 without a base; the kernels check it).
+//   VARIANT 0: ds_bpermute round key (one LDS operation more: measured slower
+//              alone, 62.5 vs 55.0 ns per update);
+//   VARIANT 1: VALU round key, DPP XOR tail with s_nop for the VALU-write ->
+//              DPP-read hazard;
+//   VARIANT 2: VALU round key, tail split over two accumulators (no s_nop,
+//              one more XOR after the last read).
+template <int VARIANT> struct StepAsmT {
+    static constexpr bool kMaskedMsg = true;
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t key_src,
+                                                    uint32_t x, uint32_t m) {
+        return step_m(sT, tb, key_src, x, m, ~0ull, ~0u);
+    }
+    // Lanes whose round key comes from the other 16-lane row (quads 3 and 7
+    // of each 32-lane group take quad 4 / quad 0 of their group).
+    __device__ static __forceinline__ uint64_t key_mask() {
+        const uint32_t lane = threadIdx.x & 63;
+        const bool row1 = (lane & 16) != 0, hi = (lane & 15) >= 12;
+        // after the in-place swap: r' = [r.row0, r.row0], B' = [r.row1, r.row1]
+        // per 32-lane group; row-0 lanes below 12 and row-1 lanes from 12 take r'.
+        return __ballot(row1 == hi);
+    }
+    // m is injected in the lanes of `mask` (a wave-uniform lane mask), 0 elsewhere.
+    __device__ static __forceinline__ uint32_t step_m(const uint32_t *, const TableBase &tb, uint32_t key_src,
+                                                      uint32_t x, uint32_t w, uint64_t mask, uint32_t mv) {
+        uint32_t xn, key, a0, a1, a2, a3, t0, t1, t2, t3, acc, m, r, b, y1, y2, y3;
+        (void)mv;
+        if constexpr (VARIANT == 0) {
+            asm volatile(
+                "ds_bpermute_b32 %[key], %[ks], %[x]\n\t"
+                "v_perm_b32 %[a0], %[x], %[lo], %[s0]\n\t"
+                "v_perm_b32 %[a1], %[x], %[lo], %[s1]\n\t"
+                "ds_read_b32 %[t0], %[a0]\n\t"
+                "v_perm_b32 %[a2], %[x], %[hi], %[s2]\n\t"
+                "ds_read_b32 %[t1], %[a1] offset:128\n\t"
+                "v_perm_b32 %[a3], %[x], %[hi], %[s3]\n\t"
+                "ds_read_b32 %[t2], %[a2]\n\t"
+                "ds_read_b32 %[t3], %[a3] offset:128\n\t"
+                "v_cndmask_b32_e64 %[m], 0, %[w], %[mask]\n\t"
+                "s_waitcnt lgkmcnt(4)\n\t"
+                "v_xor_b32 %[acc], %[key], %[m]\n\t"
+                "s_waitcnt lgkmcnt(3)\n\t"
+                "v_xor_b32 %[acc], %[t0], %[acc]\n\t"
+                "s_waitcnt lgkmcnt(2)\n\t"
+                "s_nop 1\n\t"
+                "v_xor_b32_dpp %[acc], %[t1], %[acc] quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n\t"
+                "s_waitcnt lgkmcnt(1)\n\t"
+                "s_nop 1\n\t"
+                "v_xor_b32_dpp %[acc], %[t2], %[acc] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                "s_waitcnt lgkmcnt(0)\n\t"
+                "s_nop 1\n\t"
+                "v_xor_b32_dpp %[xn], %[t3], %[acc] quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
+                : [xn] "=&v"(xn), [key] "=&v"(key), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2),
+                  [a3] "=&v"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+                  [acc] "=&v"(acc), [m] "=&v"(m)
+                : [x] "v"(x), [ks] "v"(key_src), [w] "v"(w), [mask] "s"(mask), [lo] "v"(tb.lo), [hi] "v"(tb.hi),
+                  [s0] "s"(0x03020400u), [s1] "s"(0x03020500u), [s2] "s"(0x03020600u), [s3] "s"(0x03020700u)
+                : "memory");
+        } else if constexpr (VARIANT == 1) {
+            (void)key_src;
+            asm volatile(
+                "v_perm_b32 %[a0], %[x], %[lo], %[s0]\n\t"
+                "v_perm_b32 %[a1], %[x], %[lo], %[s1]\n\t"
+                "ds_read_b32 %[t0], %[a0]\n\t"
+                "v_perm_b32 %[a2], %[x], %[hi], %[s2]\n\t"
+                "ds_read_b32 %[t1], %[a1] offset:128\n\t"
+                "v_perm_b32 %[a3], %[x], %[hi], %[s3]\n\t"
+                "ds_read_b32 %[t2], %[a2]\n\t"
+                "ds_read_b32 %[t3], %[a3] offset:128\n\t"
+                "v_mov_b32_dpp %[r], %[x] row_ror:12 row_mask:0xf bank_mask:0xf\n\t"
+                "v_cndmask_b32_e64 %[m], 0, %[w], %[mask]\n\t"
+                "v_mov_b32 %[b], %[r]\n\t"
+                "s_nop 1\n\t"
+                "v_permlane16_swap_b32 %[r], %[b]\n\t"
+                "s_nop 1\n\t"
+                "v_cndmask_b32_e64 %[key], %[b], %[r], %[kmask]\n\t"
+                "v_xor_b32 %[acc], %[key], %[m]\n\t"
+                "s_waitcnt lgkmcnt(3)\n\t"
+                "v_xor_b32 %[acc], %[t0], %[acc]\n\t"
+                "s_waitcnt lgkmcnt(2)\n\t"
+                "s_nop 1\n\t"
+                "v_xor_b32_dpp %[acc], %[t1], %[acc] quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n\t"
+                "s_waitcnt lgkmcnt(1)\n\t"
+                "s_nop 1\n\t"
+                "v_xor_b32_dpp %[acc], %[t2], %[acc] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                "s_waitcnt lgkmcnt(0)\n\t"
+                "s_nop 1\n\t"
+                "v_xor_b32_dpp %[xn], %[t3], %[acc] quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
+                : [xn] "=&v"(xn), [key] "=&v"(key), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2),
+                  [a3] "=&v"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+                  [acc] "=&v"(acc), [m] "=&v"(m), [r] "=&v"(r), [b] "=&v"(b)
+                : [x] "v"(x), [w] "v"(w), [mask] "s"(mask), [kmask] "s"(key_mask()), [lo] "v"(tb.lo),
+                  [hi] "v"(tb.hi), [s0] "s"(0x03020400u), [s1] "s"(0x03020500u), [s2] "s"(0x03020600u),
+                  [s3] "s"(0x03020700u)
+                : "memory");
+        } else if constexpr (VARIANT == 3 || VARIANT == 4) {
+            // Round key from two DPP copies (no copy hazard), acc = key ^ (w & mv)
+            // in one v_bitop3, xor3 tail (VARIANT 4: one wait for all reads).
+            (void)key_src;
+            (void)mask;
+            (void)m;
+#define TBC_ASM_HEAD                                                                               \
+    "v_perm_b32 %[a0], %[x], %[lo], %[s0]\n\t"                                                    \
+    "v_perm_b32 %[a1], %[x], %[lo], %[s1]\n\t"                                                    \
+    "ds_read_b32 %[t0], %[a0]\n\t"                                                                \
+    "v_mov_b32_dpp %[r], %[x] row_ror:12 row_mask:0xf bank_mask:0xf\n\t"                          \
+    "v_perm_b32 %[a2], %[x], %[hi], %[s2]\n\t"                                                    \
+    "ds_read_b32 %[t1], %[a1] offset:128\n\t"                                                     \
+    "v_mov_b32_dpp %[b], %[x] row_ror:12 row_mask:0xf bank_mask:0xf\n\t"                          \
+    "v_perm_b32 %[a3], %[x], %[hi], %[s3]\n\t"                                                    \
+    "ds_read_b32 %[t2], %[a2]\n\t"                                                                \
+    "ds_read_b32 %[t3], %[a3] offset:128\n\t"                                                     \
+    "v_permlane16_swap_b32 %[r], %[b]\n\t"                                                        \
+    "s_nop 1\n\t"                                                                                 \
+    "v_cndmask_b32_e64 %[key], %[b], %[r], %[kmask]\n\t"                                          \
+    "v_bitop3_b32 %[acc], %[key], %[w], %[mv] bitop3:0x78\n\t"
+#define TBC_ASM_OPERANDS                                                                           \
+    : [xn] "=&v"(xn), [key] "=&v"(key), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), \
+      [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [acc] "=&v"(acc), [r] "=&v"(r),  \
+      [b] "=&v"(b), [y1] "=&v"(y1), [y2] "=&v"(y2), [y3] "=&v"(y3)                                   \
+    : [x] "v"(x), [w] "v"(w), [mv] "v"(mv), [kmask] "s"(key_mask()), [lo] "v"(tb.lo), [hi] "v"(tb.hi), \
+      [s0] "s"(0x03020400u), [s1] "s"(0x03020500u), [s2] "s"(0x03020600u), [s3] "s"(0x03020700u)    \
+    : "memory"
+            if constexpr (VARIANT == 3)
+                asm volatile(TBC_ASM_HEAD
+                             "s_waitcnt lgkmcnt(2)\n\t"
+                             "v_xor_b32_dpp %[y1], %[t1], %[t0] quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n\t"
+                             "s_waitcnt lgkmcnt(1)\n\t"
+                             "v_xor_b32_dpp %[y2], %[t2], %[acc] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                             "s_waitcnt lgkmcnt(0)\n\t"
+                             "v_mov_b32_dpp %[y3], %[t3] quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n\t"
+                             "v_bitop3_b32 %[xn], %[y1], %[y2], %[y3] bitop3:0x96" TBC_ASM_OPERANDS);
+            else
+                asm volatile(TBC_ASM_HEAD
+                             "s_waitcnt lgkmcnt(0)\n\t"
+                             "v_xor_b32_dpp %[y1], %[t1], %[t0] quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n\t"
+                             "v_xor_b32_dpp %[y2], %[t2], %[acc] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                             "v_mov_b32_dpp %[y3], %[t3] quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n\t"
+                             "v_bitop3_b32 %[xn], %[y1], %[y2], %[y3] bitop3:0x96" TBC_ASM_OPERANDS);
+#undef TBC_ASM_HEAD
+#undef TBC_ASM_OPERANDS
+        } else {
+            (void)key_src;
+            asm volatile(
+                "v_perm_b32 %[a0], %[x], %[lo], %[s0]\n\t"
+                "v_perm_b32 %[a1], %[x], %[lo], %[s1]\n\t"
+                "ds_read_b32 %[t0], %[a0]\n\t"
+                "v_perm_b32 %[a2], %[x], %[hi], %[s2]\n\t"
+                "ds_read_b32 %[t1], %[a1] offset:128\n\t"
+                "v_perm_b32 %[a3], %[x], %[hi], %[s3]\n\t"
+                "ds_read_b32 %[t2], %[a2]\n\t"
+                "ds_read_b32 %[t3], %[a3] offset:128\n\t"
+                "v_mov_b32_dpp %[r], %[x] row_ror:12 row_mask:0xf bank_mask:0xf\n\t"
+                "v_cndmask_b32_e64 %[m], 0, %[w], %[mask]\n\t"
+                "v_mov_b32 %[b], %[r]\n\t"
+                "s_nop 1\n\t"
+                "v_permlane16_swap_b32 %[r], %[b]\n\t"
+                "s_nop 1\n\t"
+                "v_cndmask_b32_e64 %[key], %[b], %[r], %[kmask]\n\t"
+                "v_xor_b32 %[acc], %[key], %[m]\n\t"
+                "s_waitcnt lgkmcnt(2)\n\t"
+                "v_xor_b32_dpp %[y1], %[t1], %[t0] quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n\t"
+                "s_waitcnt lgkmcnt(1)\n\t"
+                "v_xor_b32_dpp %[y2], %[t2], %[acc] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                "s_waitcnt lgkmcnt(0)\n\t"
+                "v_xor_b32_dpp %[y3], %[t3], %[y1] quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_xor_b32 %[xn], %[y3], %[y2]"
+                : [xn] "=&v"(xn), [key] "=&v"(key), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2),
+                  [a3] "=&v"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+                  [acc] "=&v"(acc), [m] "=&v"(m), [r] "=&v"(r), [b] "=&v"(b), [y1] "=&v"(y1), [y2] "=&v"(y2),
+                  [y3] "=&v"(y3)
+                : [x] "v"(x), [w] "v"(w), [mask] "s"(mask), [kmask] "s"(key_mask()), [lo] "v"(tb.lo),
+                  [hi] "v"(tb.hi), [s0] "s"(0x03020400u), [s1] "s"(0x03020500u), [s2] "s"(0x03020600u),
+                  [s3] "s"(0x03020700u)
+                : "memory");
+        }
+        return xn;
+    }
+};
+
+
 constexpr uint32_t kLen = 1048320;        // one 1 MiB data block body (constants.zig:500)
 constexpr uint32_t kAbs = kLen / 32;      // 32,760 absorbs
 constexpr uint32_t kWin = kAbs / 8;       // 4,095 windows of 8 updates
@@ -141,6 +335,7 @@ __global__ __launch_bounds__(1024) void k_col4(const uint8_t *base, uint32_t cou
     __shared__ uint32_t sT[kTableDwords];
     load_tables(sT);
     __syncthreads();
+    if ((uint32_t)(uintptr_t)sT != 0) return; // StepAsm addresses the tables from LDS 0 (tags stay 0: mismatch)
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t half = (threadIdx.x >> 5) & 1;
     if (wave * per_wave >= count) return;
@@ -269,6 +464,30 @@ __global__ __launch_bounds__(64) void k_lds_chain(uint32_t iters, uint32_t *out)
     out[threadIdx.x] = x;
 }
 
+// Dependent steps of K table reads each (K perms, K ds_read_b32, XOR-combined
+// into the next step's input): the per-wave LDS issue interval is
+// (ns(K) - ns(1)) / (K - 1).
+template <int K>
+__global__ __launch_bounds__(64) void k_lds_k(uint32_t iters, uint32_t *out) {
+    __shared__ uint32_t sT[kTableDwords];
+    for (uint32_t i = threadIdx.x; i < kTableDwords; i += 64) sT[i] = (i * 2654435761u) >> 8;
+    __syncthreads();
+    const TableBase tb;
+    uint32_t x = threadIdx.x;
+    for (uint32_t k = 0; k < iters; k++) {
+        uint32_t t[K];
+#pragma unroll
+        for (int r = 0; r < K; r++)
+            t[r] = lds_u32(sT, __builtin_amdgcn_perm(x, (r & 2) ? tb.hi : tb.lo, 0x03020400u + 0x100u * r) +
+                                   128 * (r & 1));
+        uint32_t y = t[0];
+#pragma unroll
+        for (int r = 1; r < K; r++) y ^= t[r];
+        x = y;
+    }
+    out[threadIdx.x] = x;
+}
+
 __global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         uint32_t x = (uint32_t)i * 0x9E3779B9u ^ seed;
@@ -287,6 +506,7 @@ __global__ __launch_bounds__(1024) void k_prod(const uint8_t *base, uint32_t cou
     __shared__ uint32_t sT[kTableDwords];
     load_tables(sT);
     __syncthreads();
+    if ((uint32_t)(uintptr_t)sT != 0) return; // StepAsm addresses the tables from LDS 0 (tags stay 0: mismatch)
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t half = (threadIdx.x >> 5) & 1;
     if (wave * per_wave >= count) return;
@@ -361,6 +581,12 @@ int main(int argc, char **argv) {
         const uint32_t iters = 1u << 20;
         float ms = timed([&] { hipLaunchKernelGGL(k_lds_chain, dim3(1), dim3(64), 0, 0, iters, d_c); });
         printf("{\"variant\": \"lds-chain\", \"ns_per_read\": %.2f}\n", ms * 1e6 / iters);
+        float k1 = timed([&] { hipLaunchKernelGGL(k_lds_k<1>, dim3(1), dim3(64), 0, 0, iters, d_c); });
+        float k2 = timed([&] { hipLaunchKernelGGL(k_lds_k<2>, dim3(1), dim3(64), 0, 0, iters, d_c); });
+        float k3 = timed([&] { hipLaunchKernelGGL(k_lds_k<3>, dim3(1), dim3(64), 0, 0, iters, d_c); });
+        float k4 = timed([&] { hipLaunchKernelGGL(k_lds_k<4>, dim3(1), dim3(64), 0, 0, iters, d_c); });
+        printf("{\"variant\": \"lds-k\", \"ns_per_step\": [%.2f, %.2f, %.2f, %.2f]}\n", k1 * 1e6 / iters,
+               k2 * 1e6 / iters, k3 * 1e6 / iters, k4 * 1e6 / iters);
         CK(hipFree(d_c));
     }
     std::vector<uint8_t> h_ref(16ull * nmax), h_out(16ull * nmax);
@@ -385,6 +611,21 @@ int main(int argc, char **argv) {
                 bad++;
             }
         };
+        auto run_asm = [&](auto step, const char *name) {
+            using S = decltype(step);
+            const uint32_t waves = (count + 1) / 2, wpb = wpb_for(waves, 16);
+            CK(hipMemset(d_out, 0, 16ull * count));
+            const float ms = timed([&] {
+                hipLaunchKernelGGL(k_prod<S>, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs, count, 2u,
+                                   d_out);
+            });
+            report(name, count, waves, wpb, ms);
+            check(name);
+        };
+
+        run_asm(StepAsmT<2>{}, "asm-valu-split");
+        run_asm(StepAsmT<3>{}, "asm-xor3");
+        run_asm(StepAsmT<4>{}, "asm-xor3-1wait");
         if (count >= 8192) {
             const uint32_t waves = (count + 1) / 2, wpb = wpb_for(waves, 16);
             const float ms = timed([&] {
