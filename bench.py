@@ -31,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from tigerbeetle_amd import Engine, Grid, Job, benchmark_load, configs, forest  # noqa: E402
+from tigerbeetle_amd import Engine, Grid, Job, abi, benchmark_load, configs, forest  # noqa: E402
 from tigerbeetle_amd.shard import plan_shards, reduce_step  # noqa: E402
 
 METRIC = "compacted input MB/s per GPU and per node (1/2/4/8) + % HBM roofline"
@@ -103,7 +103,7 @@ class Workload:
             addrs = np.arange(base_addr, base_addr + reservation, dtype=np.uint64)
             base_addr += reservation
             self.jobs.append(Job(spec, segs_a, segs_b, js.a_immutable, js.drop_tombstones, js.level_b, 0xA5A5, 48,
-                                 addrs, out))
+                                 addrs, out, flags=abi.COMPACTION_UNIQUE_KEYS if js.unique_keys else 0))
             self.specs.append(js)
             self.bufs.append(out)
             self.input_values += js.input_values

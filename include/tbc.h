@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TBC_ABI_VERSION 2u
+#define TBC_ABI_VERSION 3u
 
 typedef enum tbc_status {
     TBC_OK = 0,
@@ -112,6 +112,19 @@ typedef struct tbc_segment {
  * acquired address (segments_b and output_blocks are ignored). */
 #define TBC_COMPACTION_VALUES_ONLY 1u
 #define TBC_COMPACTION_GRID 2u
+/* UNIQUE_KEYS (per compaction, may differ within a batch): the caller expects
+ * no key to occur twice in A u B and no tombstone to be dropped — true by
+ * construction for trees whose keys are never updated or removed (the id
+ * trees, the object and index trees of immutable objects such as Transfers).
+ * Then every value survives, every output block's contents are known before
+ * any merge, and the engine starts all AEGIS chains at once, producers
+ * merging each block's values as its chain absorbs them (no merge pass in
+ * front). The expectation is verified on the device; a compaction that
+ * breaks it is recomputed through the ordinary merge path in the same batch
+ * (identical results, slower; tbc_batch_speculation reports it). Honoured in
+ * the latency regime of a plain batch (no GRID / VALUES_ONLY, few enough
+ * output blocks that every chain runs at once); ignored elsewhere. */
+#define TBC_COMPACTION_UNIQUE_KEYS 4u
 
 /* ---- GPU-resident grid (src/vsr/grid.zig, src/lsm/set_associative_cache.zig) ----
  * The blocks of the data file's grid zone for addresses [1, block_count],
@@ -306,6 +319,14 @@ tbc_status tbc_batch_wait(tbc_batch *batch);
  * for Manifest.insert_table at level_b (manifest.zig:233-255). */
 tbc_status tbc_batch_result(tbc_batch *batch, uint32_t index, tbc_compaction_result *out_result,
                             uint8_t *table_infos, uint32_t table_info_capacity);
+/* Outcome of TBC_COMPACTION_UNIQUE_KEYS for compaction `index` once the batch
+ * is complete: TBC_SPECULATION_NONE (not speculated), _HELD (blocks written
+ * by the speculative pass) or _BROKEN (a key repeated or a tombstone was
+ * dropped: recomputed through the merge path, same results). */
+#define TBC_SPECULATION_NONE 0u
+#define TBC_SPECULATION_HELD 1u
+#define TBC_SPECULATION_BROKEN 2u
+tbc_status tbc_batch_speculation(tbc_batch *batch, uint32_t index, uint32_t *out_outcome);
 /* Per-kernel device times of the batch in microseconds (TBC_CONFIG_PROFILE).
  * names/us are host arrays of `capacity` entries; returns the entry count in *out_count. */
 tbc_status tbc_batch_kernel_times(tbc_batch *batch, const char **names, double *us, uint32_t capacity,

@@ -80,11 +80,14 @@ def data_values_from_blocks(blocks: np.ndarray, value_size: int) -> np.ndarray:
 
 
 def gpu_run(engine, jobs_inputs: list, block_size, addresses_list, *, level_b=1, cluster=0x1234,
-            snapshot_min=48):
-    """Submit several compactions as one batch; returns per job (result, infos, blocks)."""
+            snapshot_min=48, flags=0, speculation: list | None = None):
+    """Submit several compactions as one batch; returns per job (result, infos, blocks).
+    `flags`: TBC_COMPACTION_* for every job, or a list per job; `speculation`
+    (a list) receives each job's tbc_batch_speculation outcome."""
     from tigerbeetle_amd.engine import Job, stage_blocks
     jobs, keep = [], []
-    for ji, addrs in zip(jobs_inputs, addresses_list):
+    job_flags = flags if isinstance(flags, (list, tuple)) else [flags] * len(jobs_inputs)
+    for ji, addrs, fl in zip(jobs_inputs, addresses_list, job_flags):
         lay = engine.layout(ji.tree)
         vcm = lay.block_value_count_max
         if ji.a_immutable:
@@ -104,12 +107,14 @@ def gpu_run(engine, jobs_inputs: list, block_size, addresses_list, *, level_b=1,
         out = engine.alloc(len(addrs) * block_size)
         out.zero()
         jobs.append(Job(ji.tree, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, level_b, cluster,
-                        snapshot_min, np.asarray(addrs, dtype=np.uint64), out))
+                        snapshot_min, np.asarray(addrs, dtype=np.uint64), out, flags=fl))
     batch = engine.submit(jobs)
     batch.wait()
     results = []
     for i, job in enumerate(jobs):
         r, infos = batch.result(i)
+        if speculation is not None:
+            speculation.append(batch.speculation(i))
         blocks = job.output.download(r.block_count * block_size).reshape(-1, block_size) \
             if r.block_count else np.zeros((0, block_size), dtype=np.uint8)
         results.append((r, infos, blocks))

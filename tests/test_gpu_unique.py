@@ -1,0 +1,140 @@
+"""TBC_COMPACTION_UNIQUE_KEYS (include/tbc.h): the speculated block pass.
+
+A job flagged UNIQUE_KEYS skips the merge pass: each data block's producer
+merges its own positions while its AEGIS chain absorbs them (aegis.hip
+produce_unique). Whether the speculation holds (no repeated key, no dropped
+tombstone: every value survives) or breaks (then the batch's second phase
+recomputes the job through the merge path), every output block's on-disk
+image and every TableInfo must equal the oracle's restatement of
+compaction.zig / table.zig, and tbc_batch_speculation must say which path
+ran.
+"""
+import numpy as np
+import pytest
+
+from helpers import disk_image, gpu_run, run_oracle
+from tigerbeetle_amd import abi, trees, workloads
+
+pytestmark = pytest.mark.gpu
+
+U = abi.COMPACTION_UNIQUE_KEYS
+HELD, BROKEN, NONE = abi.SPECULATION_HELD, abi.SPECULATION_BROKEN, abi.SPECULATION_NONE
+
+
+def _spec(name, block_size):
+    """The tree at this block size: 4 KiB blocks get tables of ~5 data blocks
+    (+3 values), so jobs span several output tables (test_gpu_parity.py)."""
+    base = trees.BY_NAME[name]
+    if block_size == 1 << 20:
+        return base
+    return trees.with_table_size(base, 5 * (block_size - 256) // base.value_size + 3)
+
+
+def _run(oracle_lib, engine, cases, block_size, seed):
+    """cases: (tree name, make_job_inputs kwargs, flags, expected speculation)."""
+    rng = np.random.default_rng(seed)
+    inputs, addrs, flags = [], [], []
+    for name, kw, fl, _ in cases:
+        spec = _spec(name, block_size)
+        ji = workloads.make_job_inputs(spec, rng, **kw)
+        n = len(ji.a_values) + sum(len(t) for t in ji.b_tables)
+        addrs.append(workloads.addresses_for(workloads.worst_case_blocks(spec, n, block_size) + 3, rng,
+                                             int(rng.integers(1, 1000)), 0.1))
+        inputs.append(ji)
+        flags.append(fl)
+    outcome = []
+    results, _ = gpu_run(engine, inputs, block_size, addrs, flags=flags, speculation=outcome)
+    for (name, _, _, want), ji, a, (r, infos, blocks), got in zip(cases, inputs, addrs, results, outcome):
+        o = run_oracle(oracle_lib, ji, block_size, a)
+        assert o.status == 0 and r.status == 0, name
+        assert got == want, (name, got, want)
+        assert r.value_count == o.value_count and r.block_count == len(o.blocks), name
+        for g, w in zip(blocks, o.blocks):
+            assert np.array_equal(disk_image(g), disk_image(w)), name
+        assert np.array_equal(infos, o.table_infos), name
+
+
+UNIQUE_TREES = ["transfers.id", "transfers.timestamp", "transfers.debit_account_id", "transfers.ledger",
+                "account_history.timestamp"]
+
+
+@pytest.mark.parametrize("name", UNIQUE_TREES)
+def test_unique_held_small_blocks(oracle_lib, engine_small, name):
+    """Unique keys (disk A, immutable A, A only, B only): speculation holds."""
+    cases = [
+        (name, dict(n_a=3000, b_table_sizes=[2000, 1500, 900], a_immutable=False, overlap=0.0), U, HELD),
+        (name, dict(n_a=2500, b_table_sizes=[4000], a_immutable=True, overlap=0.0), U, HELD),
+        (name, dict(n_a=1700, b_table_sizes=[], a_immutable=True, overlap=0.0), U, HELD),
+        (name, dict(n_a=0, b_table_sizes=[777, 123], a_immutable=False, overlap=0.0), U, HELD),
+        (name, dict(n_a=1, b_table_sizes=[1], a_immutable=False, overlap=0.0), U, HELD),
+    ]
+    _run(oracle_lib, engine_small, cases, 4096, seed=11)
+
+
+@pytest.mark.parametrize("name", ["transfers.id", "transfers.timestamp", "transfers.debit_account_id",
+                                  "accounts.ledger"])
+def test_unique_broken_small_blocks(oracle_lib, engine_small, name):
+    """Repeated keys (A/B overlap, immutable duplicates, secondary put/remove
+    pairs) and dropped tombstones break the speculation; the recomputation
+    must give the merge path's blocks, beside jobs whose speculation holds and
+    jobs not speculated at all."""
+    secondary = trees.BY_NAME[name].usage == abi.USAGE_SECONDARY_INDEX
+    cases = [
+        (name, dict(n_a=3000, b_table_sizes=[2000, 1500], a_immutable=False, overlap=0.05), U, BROKEN),
+        (name, dict(n_a=2600, b_table_sizes=[1800], a_immutable=True, overlap=0.0, dup_frac=0.01), U, BROKEN),
+        (name, dict(n_a=2000, b_table_sizes=[2000], a_immutable=False, overlap=0.0), U, HELD),
+        (name, dict(n_a=2000, b_table_sizes=[2000], a_immutable=False, overlap=0.1), 0, NONE),
+    ]
+    if not secondary:
+        cases.append((name, dict(n_a=2500, b_table_sizes=[900], a_immutable=False, overlap=0.0, tomb_frac=0.01,
+                                 drop_tombstones=True), U, BROKEN))
+        # tombstones kept (not the last level): speculation holds
+        cases.append((name, dict(n_a=2500, b_table_sizes=[900], a_immutable=False, overlap=0.0, tomb_frac=0.05),
+                      U, HELD))
+    _run(oracle_lib, engine_small, cases, 4096, seed=12)
+
+
+def test_unique_one_repeat_at_a_block_boundary(oracle_lib, engine_small):
+    """A single repeated key exactly where a data block starts (the check that
+    crosses producers)."""
+    spec = _spec("transfers.id", 4096)
+    rng = np.random.default_rng(3)
+    ji = workloads.make_job_inputs(spec, rng, n_a=1000, b_table_sizes=[1000], a_immutable=False, overlap=0.0)
+    vcm = engine_small.layout(spec).block_value_count_max
+    # merged position vcm*2 (block 2's first value) takes the key of position vcm*2 - 1
+    merged = np.concatenate([ji.a_values, ji.b_tables[0]])
+    keys = workloads.keys_of(merged, spec)
+    order = np.lexsort(tuple(keys))
+    p, q = order[2 * vcm - 1], order[2 * vcm]
+    src, dst = merged[p].copy(), merged[q].copy()
+    # give dst src's key (ids are the first 16 bytes): dst then equals src in key
+    dst[:16] = src[:16]
+    na = len(ji.a_values)
+    if q < na:
+        ji.a_values[q] = dst
+    else:
+        ji.b_tables[0][q - na] = dst
+    # keep each stream sorted and B strictly increasing (A/B equal keys are the repeat)
+    if (p < na) == (q < na):
+        pytest.skip("both in one stream for this seed")
+    n = len(merged)
+    addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, n, 4096) + 3, rng, 5)
+    outcome = []
+    (res,), _ = gpu_run(engine_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
+    r, infos, blocks = res
+    o = run_oracle(oracle_lib, ji, 4096, addrs)
+    assert outcome == [BROKEN]
+    assert r.block_count == len(o.blocks)
+    for g, w in zip(blocks, o.blocks):
+        assert np.array_equal(disk_image(g), disk_image(w))
+    assert np.array_equal(infos, o.table_infos)
+
+
+def test_unique_config2_shape(oracle_lib, engine):
+    """1 MiB blocks, BASELINE config 2's job shape scaled down (disk A + 8 B
+    tables of the transfers.id tree), held; plus one broken job in the batch."""
+    name = "transfers.id"
+    cases = [(name, dict(n_a=120_000, b_table_sizes=[40_000] * 8, a_immutable=False, overlap=0.0), U, HELD)
+             for _ in range(3)]
+    cases.append((name, dict(n_a=90_000, b_table_sizes=[30_000] * 4, a_immutable=False, overlap=0.001), U, BROKEN))
+    _run(oracle_lib, engine, cases, 1 << 20, seed=21)

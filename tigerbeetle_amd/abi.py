@@ -32,7 +32,9 @@ USAGE_GENERAL, USAGE_SECONDARY_INDEX = 0, 1
 CONFIG_PROFILE = 1
 COMPACTION_VALUES_ONLY = 1  # tbc_compaction.flags
 COMPACTION_GRID = 2
-ABI_VERSION = 2
+COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped
+SPECULATION_NONE, SPECULATION_HELD, SPECULATION_BROKEN = 0, 1, 2
+ABI_VERSION = 3
 
 
 class TbcError(RuntimeError):
@@ -158,6 +160,7 @@ _SIGNATURES = {
     "tbc_batch_wait": (ctypes.c_int, [_P]),
     "tbc_batch_result": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(CompactionResult), _P,
                                         ctypes.c_uint32]),
+    "tbc_batch_speculation": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "tbc_batch_kernel_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p),
                                               ctypes.POINTER(ctypes.c_double), ctypes.c_uint32,
                                               ctypes.POINTER(ctypes.c_uint32)]),

@@ -56,6 +56,10 @@ class JobSpec:
     b_tables: list            # [(n_i, vs) uint8], ascending, disjoint
     drop_tombstones: bool
     level_b: int
+    # TBC_COMPACTION_UNIQUE_KEYS: the tree's keys are never repeated or removed
+    # (ids, immutable Transfers' object and index trees), so every value
+    # survives and the engine may start every block's chain before merging.
+    unique_keys: bool = False
 
     @property
     def input_values(self) -> int:
@@ -87,7 +91,7 @@ def config2_job(job: int, n_b_tables: int = 8) -> JobSpec:
     a = vals[mask]
     b = vals[~mask]
     return JobSpec(trees.BY_NAME["transfers.id"], a, False, False,
-                   [b[i * TABLE_T:(i + 1) * TABLE_T] for i in range(n_b_tables)], False, 1)
+                   [b[i * TABLE_T:(i + 1) * TABLE_T] for i in range(n_b_tables)], False, 1, unique_keys=True)
 
 
 def _zipf_accounts(rng, n: int, s: float = 1.1) -> np.ndarray:
@@ -122,7 +126,7 @@ def config3_job(job: int, n_b_tables: int = 8) -> JobSpec:
         spec = trees.BY_NAME["transfers.timestamp"]
         ts = bar_ts0 + np.arange(TABLE_T, dtype=np.uint64)
         a = workloads.values_from_keys(spec, [ts], np.zeros(TABLE_T, dtype=bool), rng)
-        return JobSpec(spec, a, True, False, [], False, 0)
+        return JobSpec(spec, a, True, False, [], False, 0, unique_keys=True)
     spec = trees.BY_NAME["transfers.debit_account_id" if job % 2 == 0 else "transfers.credit_account_id"]
     # B: 8 L0 tables of older puts (timestamps before this bar), sorted, cut.
     nb = n_b_tables * TABLE_T
@@ -246,7 +250,9 @@ def config4_job(job: int) -> JobSpec:
         old_ts = np.uint64(ACCOUNTS + 1 + (bar - L0_TABLES) * n) + np.arange(L0_TABLES * n, dtype=np.uint64)
         old_ids = np.uint64(1 + (bar - L0_TABLES) * n) + np.arange(L0_TABLES * n, dtype=np.uint64)
         b_all = _sorted_by_key(spec, _bar_values(spec, name, rng, old_ts, old_ids))
-        return JobSpec(spec, a, True, unsorted, [b_all[i * n:(i + 1) * n] for i in range(L0_TABLES)], False, 0)
+        # Transfers are immutable: their trees' bar-end keys are all new.
+        return JobSpec(spec, a, True, unsorted, [b_all[i * n:(i + 1) * n] for i in range(L0_TABLES)], False, 0,
+                       unique_keys=True)
     name = FOREST_DEEP[k - len(FOREST_BAR)]
     spec = trees.BY_NAME[name]
     ji = workloads.make_job_inputs(spec, rng, n_a=n, b_table_sizes=[n] * 4, a_immutable=False, overlap=0.05,

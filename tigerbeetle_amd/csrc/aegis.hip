@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include "tbc_internal.h"
+#include "keys.h"
 
 namespace tbc {
 
@@ -591,8 +592,6 @@ __global__ __launch_bounds__(1024) void k_grid_validate(const InputCheck *checks
     }
 }
 
-__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return gld<uint64_t>(p); }
-
 // Key (as 4 little-endian limbs) of a value; see composite_key.zig:48-50,
 // groove.zig:27-29, 59-61.
 __device__ __forceinline__ void value_key(const JobDesc &j, const uint8_t *v, uint64_t k[4]) {
@@ -772,6 +771,477 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
     }
 }
 
+// Key of lane `src` (ds_bpermute of each 32-bit half; the whole wave active).
+template <int KL> __device__ __forceinline__ Key<KL> key_of_lane(const Key<KL> &k, uint32_t src) {
+    Key<KL> r;
+    const int addr = (int)(src << 2);
+#pragma unroll
+    for (int l = 0; l < KL; l++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)k.l[l]);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(k.l[l] >> 32));
+        r.l[l] = (uint64_t)hi << 32 | lo;
+    }
+    return r;
+}
+
+// Producer of a speculated job (TBC_COMPACTION_UNIQUE_KEYS): no merge pass ran.
+// If no key occurs twice in A u B and no tombstone is dropped, every value
+// survives (compaction.zig:483-559 dedup and :757-798 merge rules all keep
+// it), so block k is merged positions [k * vcm, k * vcm + cnt) and the
+// producer merges them itself, 64 outputs per step: lane l holds A[ia + l]
+// and B[ib + l]; A[ia + l] lands at l + |{B-window keys < it}| and B[ib + l]
+// at l + |{A-window keys <= it}| (A first on equal keys); the outputs below
+// 64 are exactly the next 64 merged values. Both ranks are binary searches
+// over the other window's keys by ds_bpermute (no LDS). The speculation
+// holds iff no output key equals its merged predecessor's and, when dropping
+// tombstones, no A output is a tombstone: an equal key of B for an A value is
+// its lower bound in the B window (a B value equal to an A value follows it),
+// equal keys inside a stream are adjacent lanes, and the values before the
+// block on each side carry the check across blocks and steps. A broken
+// speculation marks the job (JobResultDev.spec): the batch's second phase
+// recomputes its blocks through the merge path, bit-exact; the chains of
+// this pass absorb what was written and are overwritten.
+//
+// VW > 0 (values of 16 or 32 bytes, VW x 16 B): each lane loads its whole A
+// and B value into registers with the window and stores it straight to its
+// output slot, one memory round trip per step; the key is taken from the
+// registers. VW = 0 (larger values, whose chains leave the producer more
+// time): keys only, the outputs copied through the wave's LDS staging.
+// Progress is published every other step, once the stores have completed.
+template <int KIND>
+__device__ __forceinline__ Key<KeyLimbs<KIND>::value> key_of_words(const uint64_t *w, uint32_t ts_word) {
+    Key<KeyLimbs<KIND>::value> k;
+    if constexpr (KIND == kKeyTimestamp) {
+        uint64_t t = w[0];
+#pragma unroll
+        for (int q = 1; q < 4; q++)
+            if (ts_word == (uint32_t)q) t = w[q];
+        k.l[0] = t & ~kTombstoneBit;
+    } else if constexpr (KIND == kKeyIdU128) {
+        k.l[0] = w[0];
+        k.l[1] = w[1];
+    } else if constexpr (KIND == kKeyCompositeU64) {
+        k.l[0] = w[1] & ~kTombstoneBit;
+        k.l[1] = w[0];
+    } else {
+        k.l[0] = w[2] & ~kTombstoneBit;
+        k.l[1] = w[0];
+        k.l[2] = w[1];
+    }
+    return k;
+}
+
+template <int KIND, int VW>
+__device__ __forceinline__ void produce_unique(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
+                                               uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
+                                               uint64_t *stage) {
+    constexpr int KL = KeyLimbs<KIND>::value;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset, na = j.a.n, nb = j.b.n;
+    const uint32_t len = cnt * vs;
+    uint32_t ia = sp.i, ib = k * j.vcm - sp.i;
+    SegCursor ca, cb;
+    ca.init(j.a, sp.seg_a); // segment of A[max(ia - 1, 0)]
+    cb.init(j.b, sp.seg_b); // segment of B[min(ib, nb - 1)]
+    Key<KL> inf;
+#pragma unroll
+    for (int l = 0; l < KL; l++) inf.l[l] = ~0ull;
+    // Keys of the values just before the block on each side.
+    bool has_a = ia > 0, has_b = ib > 0;
+    Key<KL> last_a = inf, last_b = inf;
+    if (has_a) last_a = load_key<KIND>(ca.elem(ia - 1, vs), ts);
+    if (has_b) {
+        const uint32_t s = sp.pad; // segment of B[ib - 1]
+        last_b = load_key<KIND>((const uint8_t *)(uintptr_t)gld<uint64_t>(j.b.seg_ptr + s) +
+                                    (size_t)(ib - 1 - gld<uint32_t>(j.b.seg_pre + s)) * vs, ts);
+    }
+    uint64_t *st_src = stage, *st_dst = stage + 64;
+    const uint32_t cpv_log = __builtin_ctz(vs >> 4);
+    bool bad = false;
+    // Window at (ia, ib): pointers and values or keys; invalid lanes +inf.
+    const uint8_t *pa, *pb;
+    u32x4 xa[VW > 0 ? VW : 1], xb[VW > 0 ? VW : 1];
+    Key<KL> ka, kb;
+    uint32_t nav, nbv;
+    auto load_window = [&]() {
+        ca.advance(ia);
+        cb.advance(ib);
+        nav = na - ia < 64 ? na - ia : 64;
+        nbv = nb - ib < 64 ? nb - ib : 64;
+        pa = lane < nav ? ca.elem(ia + lane, vs) : nullptr;
+        pb = lane < nbv ? cb.elem(ib + lane, vs) : nullptr;
+        if constexpr (VW > 0) {
+#pragma unroll
+            for (int q = 0; q < VW; q++) {
+                xa[q] = pa ? gld<u32x4>(pa + 16 * q) : u32x4{0, 0, 0, 0};
+                xb[q] = pb ? gld<u32x4>(pb + 16 * q) : u32x4{0, 0, 0, 0};
+            }
+        } else {
+            ka = pa ? load_key<KIND>(pa, ts) : inf;
+            kb = pb ? load_key<KIND>(pb, ts) : inf;
+        }
+    };
+    auto words_key = [&](const u32x4 *x, bool valid) {
+        uint64_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < VW; q++) {
+            w[2 * q] = (uint64_t)x[q].y << 32 | x[q].x;
+            w[2 * q + 1] = (uint64_t)x[q].w << 32 | x[q].z;
+        }
+        return valid ? key_of_words<KIND>(w, ts >> 3) : inf;
+    };
+    load_window();
+    uint32_t out = 0, since = 0, published = 0;
+    while (out < cnt) {
+        const uint32_t E = cnt - out < 64 ? cnt - out : 64;
+        if constexpr (VW > 0) {
+            ka = words_key(xa, pa != nullptr);
+            kb = words_key(xb, pb != nullptr);
+            // The window has landed, and the previous steps' stores were
+            // issued before it (nothing after it): the wait is free; publish.
+            if (out != published) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(prog, (out * vs) & ~255u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                published = out;
+            }
+        }
+        // Ranks: lower bound of ka among the B window, upper bound of kb among the A window.
+        uint32_t lo_a = 0, hi_a = nbv, lo_b = 0, hi_b = nav;
+#pragma unroll
+        for (int it = 0; it < 7; it++) {
+            const uint32_t ma = (lo_a + hi_a) >> 1, mb = (lo_b + hi_b) >> 1;
+            const Key<KL> at_b = key_of_lane(kb, ma < 63 ? ma : 63);
+            const Key<KL> at_a = key_of_lane(ka, mb < 63 ? mb : 63);
+            if (lo_a < hi_a) {
+                if (key_lt(at_b, ka)) lo_a = ma + 1;
+                else hi_a = ma;
+            }
+            if (lo_b < hi_b) {
+                if (key_le(at_a, kb)) lo_b = mb + 1;
+                else hi_b = mb;
+            }
+        }
+        const uint32_t pos_a = lane + lo_a, pos_b = lane + lo_b;
+        const bool ea = lane < nav && pos_a < E, eb = lane < nbv && pos_b < E;
+        const uint32_t n_a = __builtin_popcountll(__ballot(ea)), n_b = __builtin_popcountll(__ballot(eb));
+        // Equal neighbours (speculation broken) and dropped tombstones.
+        const Key<KL> lb = key_of_lane(kb, lo_a < 63 ? lo_a : 63);
+        const Key<KL> prev_a = key_of_lane(ka, lane ? lane - 1 : 0);
+        const Key<KL> prev_b = key_of_lane(kb, lane ? lane - 1 : 0);
+        bool eq = ea && lo_a < nbv && key_eq(lb, ka);
+        eq |= ea && (lane ? key_eq(prev_a, ka) : (has_a && key_eq(last_a, ka)));
+        eq |= eb && (lane ? key_eq(prev_b, kb) : (has_b && key_eq(last_b, kb)));
+        if (j.drop_tombstones && ea) eq |= (ld64(pa + ts) >> 63) != 0;
+        bad |= __ballot(eq) != 0;
+        if (n_a + n_b != E) { // the windows always hold the next E values: a broken invariant
+            if (lane == 0) gst<uint32_t>(err, 0xbad1u);
+            bad = true;
+            break;
+        }
+        if (n_a) last_a = key_of_lane(ka, n_a - 1), has_a = true;
+        if (n_b) last_b = key_of_lane(kb, n_b - 1), has_b = true;
+        if constexpr (VW > 0) {
+            // Every output straight from its lane's registers.
+            if (ea)
+#pragma unroll
+                for (int q = 0; q < VW; q++) gst<u32x4>(body + (size_t)(out + pos_a) * vs + 16 * q, xa[q]);
+            if (eb)
+#pragma unroll
+                for (int q = 0; q < VW; q++) gst<u32x4>(body + (size_t)(out + pos_b) * vs + 16 * q, xb[q]);
+            ia += n_a;
+            ib += n_b;
+            out += E;
+            if (out < cnt) load_window();
+        } else {
+            // Stage this step's copies, then load the next window before copying.
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (ea) {
+                st_src[pos_a] = (uint64_t)(uintptr_t)pa;
+                st_dst[pos_a] = (uint64_t)(uintptr_t)(body + (size_t)(out + pos_a) * vs);
+            }
+            if (eb) {
+                st_src[pos_b] = (uint64_t)(uintptr_t)pb;
+                st_dst[pos_b] = (uint64_t)(uintptr_t)(body + (size_t)(out + pos_b) * vs);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            ia += n_a;
+            ib += n_b;
+            out += E;
+            if (out < cnt) load_window();
+            copy_staged(st_src, st_dst, E, cpv_log);
+        }
+        // VW = 0: publish every other step (and at the end): stores complete,
+        // then progress in whole 256-byte units. VW > 0: at the end (else at
+        // the next window's arrival).
+        if (VW > 0 ? out >= cnt : (++since >= 2 || out >= cnt)) {
+            since = 0;
+            const uint32_t bytes = out * vs;
+            const uint32_t pub = bytes >= len ? len : (bytes & ~255u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(prog, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    if (bad) {
+        if (lane == 0) __hip_atomic_store(spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // The chains still run to the end of the block: release them.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(prog, len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// Wide steps for small values (VW x 16 B, VW = 1 or 2): 128 outputs per
+// memory round trip. Lane l holds A[ia + l + 64q] and B[ib + l + 64q] in slot
+// q < 2 (whole values in registers). Only the A values are ranked among the
+// B window (lower bound, binary search over window positions: lane m & 63,
+// slot m >> 6, by ds_bpermute); a B value's position is its index plus the
+// number of A values ranked at or before it, from a 128-bin histogram of
+// the A ranks in the wave's LDS slot and a wave prefix sum. The speculation
+// checks, stores and publication are produce_unique's.
+template <int KL> __device__ __forceinline__ Key<KL> key_of_slot(const Key<KL> (&k)[2], uint32_t pos) {
+    const Key<KL> k0 = key_of_lane(k[0], pos & 63), k1 = key_of_lane(k[1], pos & 63);
+    return (pos >> 6) & 1 ? k1 : k0;
+}
+
+template <int KL> __device__ __forceinline__ Key<KL> key_readlane(const Key<KL> &k, uint32_t src) {
+    Key<KL> r;
+#pragma unroll
+    for (int l = 0; l < KL; l++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k.l[l], (int)src);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k.l[l] >> 32), (int)src);
+        r.l[l] = (uint64_t)hi << 32 | lo;
+    }
+    return r;
+}
+
+template <int KIND, int VW>
+__device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
+                                                    uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
+                                                    uint64_t *stage, uint64_t *probe) {
+    // probe (timing probe only): wall-clock ticks spent waiting for windows,
+    // searching, in the histogram, in the rest, and the step count.
+    uint64_t t_wait = 0, t_search = 0, t_hist = 0, t_rest = 0, steps = 0, t_mark = wall_clock64();
+    constexpr int KL = KeyLimbs<KIND>::value;
+    constexpr uint32_t W = 128;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset, na = j.a.n, nb = j.b.n;
+    const uint32_t len = cnt * vs;
+    uint32_t ia = sp.i, ib = k * j.vcm - sp.i;
+    SegCursor ca, cb;
+    ca.init(j.a, sp.seg_a); // segment of A[max(ia - 1, 0)]
+    cb.init(j.b, sp.seg_b); // segment of B[min(ib, nb - 1)]
+    Key<KL> inf;
+#pragma unroll
+    for (int l = 0; l < KL; l++) inf.l[l] = ~0ull;
+    bool has_a = ia > 0, has_b = ib > 0;
+    Key<KL> last_a = inf, last_b = inf;
+    if (has_a) last_a = load_key<KIND>(ca.elem(ia - 1, vs), ts);
+    if (has_b) {
+        const uint32_t s = sp.pad; // segment of B[ib - 1]
+        last_b = load_key<KIND>((const uint8_t *)(uintptr_t)gld<uint64_t>(j.b.seg_ptr + s) +
+                                    (size_t)(ib - 1 - gld<uint32_t>(j.b.seg_pre + s)) * vs, ts);
+    }
+    uint32_t *hist = (uint32_t *)stage; // 128 bins
+    bool bad = false;
+    u32x4 xa[2][VW], xb[2][VW];
+    bool va[2], vb[2];
+    uint32_t nav, nbv;
+    auto load_window = [&]() {
+        ca.advance(ia);
+        cb.advance(ib);
+        nav = na - ia < W ? na - ia : W;
+        nbv = nb - ib < W ? nb - ib : W;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t idx = lane + 64 * q;
+            va[q] = idx < nav;
+            vb[q] = idx < nbv;
+            const uint8_t *pa = va[q] ? ca.elem(ia + idx, vs) : nullptr;
+            const uint8_t *pb = vb[q] ? cb.elem(ib + idx, vs) : nullptr;
+#pragma unroll
+            for (int v = 0; v < VW; v++) {
+                xa[q][v] = pa ? gld<u32x4>(pa + 16 * v) : u32x4{0, 0, 0, 0};
+                xb[q][v] = pb ? gld<u32x4>(pb + 16 * v) : u32x4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto words = [&](const u32x4 *x, uint64_t (&w)[4]) {
+        w[0] = w[1] = w[2] = w[3] = 0;
+#pragma unroll
+        for (int v = 0; v < VW; v++) {
+            w[2 * v] = (uint64_t)x[v].y << 32 | x[v].x;
+            w[2 * v + 1] = (uint64_t)x[v].w << 32 | x[v].z;
+        }
+    };
+    load_window();
+    uint32_t out = 0, published = 0;
+    while (out < cnt) {
+        const uint32_t E = cnt - out < W ? cnt - out : W;
+        if (probe) {
+            const uint64_t t = wall_clock64();
+            t_rest += t - t_mark;
+            t_mark = t;
+        }
+        Key<KL> ka[2], kb[2];
+        bool ta[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            uint64_t w[4];
+            words(xa[q], w);
+            ka[q] = va[q] ? key_of_words<KIND>(w, ts >> 3) : inf;
+            ta[q] = (((ts >> 3) == 0 ? w[0] : (ts >> 3) == 1 ? w[1] : (ts >> 3) == 2 ? w[2] : w[3]) >> 63) != 0;
+            words(xb[q], w);
+            kb[q] = vb[q] ? key_of_words<KIND>(w, ts >> 3) : inf;
+        }
+        // The window has landed, and the previous steps' stores were issued
+        // before it (nothing after it): the wait is free; publish.
+        if (out != published) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(prog, (out * vs) & ~255u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            published = out;
+        }
+        if (probe) {
+            asm volatile("" ::"v"(ka[0].l[0]), "v"(kb[1].l[0]));
+            const uint64_t t = wall_clock64();
+            t_wait += t - t_mark;
+            t_mark = t;
+        }
+        // A ranks among the B window (lower bound).
+        uint32_t lo[2] = {0, 0}, hi[2] = {nbv, nbv};
+#pragma unroll
+        for (int it = 0; it < 8; it++) {
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const uint32_t m = (lo[q] + hi[q]) >> 1;
+                const Key<KL> at = key_of_slot(kb, m < W - 1 ? m : W - 1);
+                if (lo[q] < hi[q]) {
+                    if (key_lt(at, ka[q])) lo[q] = m + 1;
+                    else hi[q] = m;
+                }
+            }
+        }
+        if (probe) {
+            asm volatile("" ::"v"(lo[0]), "v"(lo[1]));
+            const uint64_t t = wall_clock64();
+            t_search += t - t_mark;
+            t_mark = t;
+        }
+        // Histogram of the A ranks, prefix: A values at or before each B position.
+        hist[lane] = 0;
+        hist[lane + 64] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            if (va[q] && lo[q] < W) __hip_atomic_fetch_add(&hist[lo[q]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t c0 = hist[lane], c1 = hist[lane + 64];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y0 = __shfl_up(c0, o, 64), y1 = __shfl_up(c1, o, 64);
+            if (lane >= (uint32_t)o) c0 += y0, c1 += y1;
+        }
+        c1 += __shfl(c0, 63, 64);
+        if (probe) {
+            asm volatile("" ::"v"(c0), "v"(c1));
+            const uint64_t t = wall_clock64();
+            t_hist += t - t_mark;
+            t_mark = t;
+            steps++;
+        }
+        uint32_t pos_a[2], pos_b[2];
+        bool ea[2], eb[2];
+        pos_a[0] = lane + lo[0];
+        pos_a[1] = lane + 64 + lo[1];
+        pos_b[0] = lane + c0;
+        pos_b[1] = lane + 64 + c1;
+        uint32_t n_a = 0, n_b = 0;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            ea[q] = va[q] && pos_a[q] < E;
+            eb[q] = vb[q] && pos_b[q] < E;
+            n_a += __builtin_popcountll(__ballot(ea[q]));
+            n_b += __builtin_popcountll(__ballot(eb[q]));
+        }
+        // Equal neighbours (speculation broken) and dropped tombstones.
+        bool eq = false;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const Key<KL> lb = key_of_slot(kb, lo[q] < W - 1 ? lo[q] : W - 1);
+            eq |= ea[q] && lo[q] < nbv && key_eq(lb, ka[q]);
+            const Key<KL> pa_ = key_of_lane(ka[q], lane ? lane - 1 : 0);
+            const Key<KL> pb_ = key_of_lane(kb[q], lane ? lane - 1 : 0);
+            const Key<KL> first_a = q == 0 ? last_a : key_readlane(ka[0], 63);
+            const Key<KL> first_b = q == 0 ? last_b : key_readlane(kb[0], 63);
+            const bool ha = q == 0 ? has_a : true, hb = q == 0 ? has_b : true;
+            eq |= ea[q] && (lane ? key_eq(pa_, ka[q]) : (ha && key_eq(first_a, ka[q])));
+            eq |= eb[q] && (lane ? key_eq(pb_, kb[q]) : (hb && key_eq(first_b, kb[q])));
+            if (j.drop_tombstones) eq |= ea[q] && ta[q];
+        }
+        bad |= __ballot(eq) != 0;
+        if (n_a + n_b != E) { // the windows always hold the next E values: a broken invariant
+            if (lane == 0) gst<uint32_t>(err, 0xbad2u);
+            bad = true;
+            break;
+        }
+        if (n_a) {
+            const uint32_t t = n_a - 1;
+            last_a = key_readlane(t < 64 ? ka[0] : ka[1], t & 63);
+            has_a = true;
+        }
+        if (n_b) {
+            const uint32_t t = n_b - 1;
+            last_b = key_readlane(t < 64 ? kb[0] : kb[1], t & 63);
+            has_b = true;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            if (ea[q])
+#pragma unroll
+                for (int v = 0; v < VW; v++) gst<u32x4>(body + (size_t)(out + pos_a[q]) * vs + 16 * v, xa[q][v]);
+            if (eb[q])
+#pragma unroll
+                for (int v = 0; v < VW; v++) gst<u32x4>(body + (size_t)(out + pos_b[q]) * vs + 16 * v, xb[q][v]);
+        }
+        ia += n_a;
+        ib += n_b;
+        out += E;
+        if (out < cnt) load_window();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (bad && lane == 0) __hip_atomic_store(spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(prog, len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (probe && lane == 0) {
+        t_rest += wall_clock64() - t_mark;
+        probe[0] = t_wait;
+        probe[1] = t_search;
+        probe[2] = t_hist;
+        probe[3] = t_rest;
+        probe[4] = steps;
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ void produce_unique_vs(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
+                                                  uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
+                                                  uint64_t *stage, uint32_t phase) {
+    // Timing probe (TBC_PROBE_PRODUCERS_ONLY, no chains): the block's header
+    // bytes receive the producer's time split.
+    uint64_t *probe = phase == kPhaseProducersOnly ? (uint64_t *)(body - kHeaderSize) : nullptr;
+    if (j.value_size == 32) produce_unique_wide<KIND, 2>(j, k, cnt, sp, body, prog, err, spec, stage, probe);
+    else if (j.value_size == 16) produce_unique_wide<KIND, 1>(j, k, cnt, sp, body, prog, err, spec, stage, probe);
+    else produce_unique<KIND, 0>(j, k, cnt, sp, body, prog, err, spec, stage);
+}
+
 // Data blocks: data_block_finish (table.zig:306-384) for every output data
 // block. Blocks are numbered batch-wide by their upper bound (job base + k).
 // A workgroup holds C chain waves and 2C producer waves: chain wave c takes
@@ -788,33 +1258,43 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
 // chain waves only, up to 16 per workgroup (4 per SIMD), so the AES rounds of
 // four waves hide each other's LDS latency instead of one chain per SIMD
 // waiting on it.
-constexpr uint32_t kMaxChainWaves = 5;
+// Fused: C chain + 2C producer waves, C <= 4 (768 threads), so the kernel may
+// use 168 VGPRs (3 waves per SIMD) and the producers do not spill.
+constexpr uint32_t kMaxChainWaves = 4;
 constexpr uint32_t kMaxChainOnlyWaves = 16;
 // Above this many chain waves (2 per SIMD) the two-pass path wins.
 constexpr uint32_t kFusedMaxChainWaves = 2048;
 
 template <bool Fused, class ChainStep = StepBpermute>
-__global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
+__global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
                                                       const JobResultDev *res, const uint64_t *status,
                                                       const uint64_t *masks, const uint32_t *block_tile,
                                                       const SplitDesc *splits, uint32_t chain_waves,
-                                                      const uint32_t *ready) {
+                                                      const uint32_t *ready, const SplitDesc *bsplits,
+                                                      uint32_t phase) {
     constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
     __shared__ uint64_t sStage[Fused ? 2 * kMaxChainWaves : 1][128]; // producer copy staging
-    load_tables(sT);
-    if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = 0;
-    __syncthreads();
     const uint32_t C = chain_waves;
-    const uint32_t wave_in_block = threadIdx.x >> 6;
-    const uint32_t lane = threadIdx.x & 63;
     auto locate = [&](uint32_t m, int &ji_, uint32_t &k_) {
         ji_ = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
         k_ = m - jobs[ji_].dblock_base;
-        return m < total && k_ < res[jobs[ji_].job_index].data_block_count;
+        return m < total && k_ < res[jobs[ji_].job_index].data_block_count &&
+               (phase != 1 || !phase_skips(jobs[ji_], res, phase));
     };
+    if (phase == 1) { // recomputation of broken speculations: leave at once if none of ours
+        int ji_;
+        uint32_t k_;
+        const bool mine = threadIdx.x < 2 * C && locate(2 * blockIdx.x * C + threadIdx.x, ji_, k_);
+        if (!__syncthreads_or(mine)) return;
+    }
+    load_tables(sT);
+    if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t wave_in_block = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
     auto block_count = [&](const JobDesc &j, uint32_t k_) {
         const uint64_t n_out = res[j.job_index].value_count;
         const uint64_t first = (uint64_t)k_ * j.vcm;
@@ -827,6 +1307,29 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
         const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
         if (!locate(mine, ji, k)) return;
         const JobDesc &j = jobs[ji];
+        if (j.unique && phase != 1) { // speculated: this producer merges the block's values itself
+            uint8_t *blk = block_ptr(j, data_block_slot(k, j.dbcm));
+            const SplitDesc sp = bsplits[j.dblock_base + k];
+            uint32_t *err = const_cast<uint32_t *>(&res[j.job_index].invariant);
+            uint32_t *spec = const_cast<uint32_t *>(&res[j.job_index].spec);
+            uint64_t *stage = sStage[Fused ? p : 0];
+            const uint32_t cnt = block_count(j, k);
+            switch (j.key_kind) {
+            case kKeyTimestamp:
+                produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                break;
+            case kKeyIdU128:
+                produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                break;
+            case kKeyCompositeU64:
+                produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                break;
+            default:
+                produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                break;
+            }
+            return;
+        }
         if (sparse_job(j, res)) { // body written by k_assemble<true> (stream order)
             if (lane == 0)
                 __hip_atomic_store(&sProg[p], block_count(j, k) * j.value_size, __ATOMIC_RELAXED,
@@ -838,6 +1341,7 @@ __global__ __launch_bounds__(1024) void k_data_blocks(const JobDesc *jobs, int n
                      const_cast<uint32_t *>(&res[j.job_index].invariant), sStage[Fused ? p : 0]);
         return;
     }
+    if (phase == kPhaseProducersOnly) return; // timing probe: no chains
     const uint32_t wave = blockIdx.x * C + wave_in_block;
     const bool upper = lane >= 32;
     const uint32_t mine = 2 * wave + (upper ? 1u : 0u);
@@ -910,7 +1414,7 @@ template <bool SparseOnly>
 __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs, uint32_t total_tiles,
                                                   const uint64_t *status, const uint64_t *masks,
                                                   const SplitDesc *splits, uint32_t *ready,
-                                                  const JobResultDev *res) {
+                                                  const JobResultDev *res, uint32_t phase) {
     constexpr uint32_t W = kMergeTile / 64; // mask words per kind per tile
     __shared__ uint32_t s_pre[3][W + 1];    // survivors, A taken, B taken before word w
     __shared__ uint64_t s_src[4][64], s_dst[4][64];
@@ -919,6 +1423,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
     for (uint32_t g = blockIdx.x; g < total_tiles; g += gridDim.x) {
         const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.tile_base; });
         const JobDesc &j = jobs[ji];
+        if (phase_skips(j, res, phase)) continue;          // uniform per workgroup
         if (SparseOnly && !sparse_job(j, res)) continue; // uniform per workgroup
         const uint32_t t = g - j.tile_base;
         const uint32_t n = j.a.n + j.b.n, vs = j.value_size, vcm = j.vcm;
@@ -1167,7 +1672,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, bool maybe_sparse,
                   void *stream,
-                  void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done) {
+                  void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done,
+                  const SplitDesc *d_bsplits, uint32_t phase, bool index_blocks) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t waves = (total_dblocks + 1) / 2; // chain waves
     if (values_only) {
@@ -1176,7 +1682,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         if (total_dblocks && !bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
             hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, phase);
             if (hipGetLastError() != hipSuccess) return -1;
         }
         if (mark) mark(mark_ctx, "assemble");
@@ -1190,15 +1696,17 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         if (maybe_sparse) { // heavy-dedup jobs: bodies first, parallel (sparse_job decides on device)
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
             hipLaunchKernelGGL(k_assemble<true>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, phase);
             if (hipGetLastError() != hipSuccess) return -1;
-            if (mark) mark(mark_ctx, "assemble");
+            if (mark) mark(mark_ctx, phase ? "recompute_assemble" : "assemble");
         }
         uint32_t c = waves_per_block(waves);
         c = c > kMaxChainWaves ? kMaxChainWaves : c;
+        static const bool producers_only = getenv("TBC_PROBE_PRODUCERS_ONLY") != nullptr; // timing probe only
         hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
                            total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
-                           c, (const uint32_t *)d_ready);
+                           c, (const uint32_t *)d_ready, d_bsplits,
+                           phase == 0 && producers_only ? kPhaseProducersOnly : phase);
         if (hipGetLastError() != hipSuccess) return -1;
     } else if (total_dblocks) {
         // Throughput regime: assemble every body, then the chains, 4 per SIMD.
@@ -1210,7 +1718,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         if (!bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
             hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results);
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, phase);
             if (hipGetLastError() != hipSuccess) return -1;
             if (mark) mark(mark_ctx, "assemble");
         }
@@ -1218,10 +1726,11 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
         hipLaunchKernelGGL(k_data_blocks<false>, dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs, njobs,
                            total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
-                           c, (const uint32_t *)d_ready);
+                           c, (const uint32_t *)d_ready, d_bsplits, phase);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    if (mark) mark(mark_ctx, "data_blocks");
+    if (mark) mark(mark_ctx, phase ? "recompute_blocks" : "data_blocks");
+    if (!index_blocks) return 0;
     if (total_tables) {
         hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -1241,7 +1750,7 @@ int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, 
         if (!bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
             hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, d_results);
+                               d_masks, d_splits, d_ready, d_results, 0u);
             if (hipGetLastError() != hipSuccess) return -1;
         }
         hipLaunchKernelGGL(k_index_layout, dim3((total_dblocks + 255) / 256), dim3(256), 0, s, d_jobs, njobs,
@@ -1272,13 +1781,13 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
             if (c > waves) c = waves;
             hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
                                d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
-                               d_block_tile, d_splits, c, d_ready);
+                               d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         } else {
             const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
             const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
             hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
                                d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
-                               d_block_tile, d_splits, c, d_ready);
+                               d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         }
         if (hipGetLastError() != hipSuccess) return -1;
     }

@@ -992,7 +992,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             (c.a_immutable && c.segment_count_a > 1) || (!grid && !c.output_blocks) ||
             (c.segment_count_a && !c.segments_a) || (!grid && c.segment_count_b && !c.segments_b) ||
             (c.address_count && !c.addresses) ||
-            (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID)) || c.flags != flags0 ||
+            (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID | TBC_COMPACTION_UNIQUE_KEYS)) ||
+            ((c.flags ^ flags0) & ~TBC_COMPACTION_UNIQUE_KEYS) ||
             (grid && ((c.flags & TBC_COMPACTION_VALUES_ONLY) || c.grid != grid0 || !c.grid || c.grid->engine != e ||
                       (c.table_count_a && (c.a_immutable || !c.tables_a)) || (c.table_count_b && !c.tables_b) ||
                       (!c.a_immutable && c.segment_count_a)))) {
@@ -1103,6 +1104,20 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         infos += d.table_max;
     }
 
+    // TBC_COMPACTION_UNIQUE_KEYS is honoured in the latency regime of a plain
+    // batch: every chain runs at once, so starting them before any merge is
+    // what it buys (aegis.hip produce_unique).
+    const bool spec_regime = !grid_mode && !pipeline && !(flags0 & TBC_COMPACTION_VALUES_ONLY) &&
+                             (uint64_t)(dblocks + 1) / 2 <= kFusedChainWaves;
+    static const bool no_spec = getenv("TBC_NO_SPECULATION") != nullptr; // A/B measurement only
+    bool any_unique = false;
+    for (uint32_t k = 0; k < count; k++) {
+        JobDesc &d = sj[k];
+        d.unique = spec_regime && !no_spec && (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) &&
+                   d.dblock_max > 0;
+        any_unique |= d.unique != 0;
+    }
+
     // Device layout of the batch.
     const uint64_t sz_jobs = align_up(sizeof(JobDesc) * (uint64_t)count, 256);
     const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
@@ -1112,7 +1127,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     const uint64_t sz_checks = align_up(sizeof(InputCheck) * n_checks, 256);
     const uint64_t sz_resolve = align_up(sizeof(ResolveItem) * (uint64_t)resolve.size(), 256);
     const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order + sz_checks + sz_resolve;
-    const uint64_t sz_splits = align_up(sizeof(SplitDesc) * (uint64_t)splits, 256);
+    // tile splits, then (speculated jobs) one split per data block
+    const uint64_t sz_splits = align_up(sizeof(SplitDesc) * ((uint64_t)splits + (any_unique ? dblocks : 0)), 256);
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     // tile status, block tiles, per-block landed counts, the assembling
     // merge's look-back words (one per tile) and its ticket counters
@@ -1133,6 +1149,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     e->host.live++;
     uint8_t *d_in = dbase;
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
+    SplitDesc *d_bsplits = any_unique ? d_splits + splits : nullptr;
     uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
     uint32_t *d_block_tile = (uint32_t *)(d_status + tiles);
     uint32_t *d_ready = d_block_tile + dblocks;
@@ -1304,6 +1321,26 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                     e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+    } else if (any_unique) {
+        // Speculated jobs: their block splits and results first, then the
+        // merge of the others, then ONE block pass for all (speculated
+        // producers merge their blocks themselves), then the recomputation of
+        // broken speculations (every kernel leaves at once when none broke),
+        // then the index blocks.
+        const JobDesc *dj = (const JobDesc *)d_in;
+        ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
+        mark_cb(b, "partition_blocks");
+        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
+                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
+        ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
+                                 d_block_tile, d_splits, false, maybe_sparse, s, mark_cb, b, false, d_bsplits, 0,
+                                 false) == 0;
+        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
+                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+        ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
+                                 d_block_tile, d_splits, false, true, s, mark_cb, b, false, d_bsplits, 1, true) == 0;
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     } else {
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
@@ -1473,6 +1510,18 @@ tbc_status tbc_batch_result(tbc_batch *b, uint32_t index, tbc_compaction_result 
         memcpy(table_infos, b->h_infos + (size_t)b->info_base[index] * kTableInfoSize,
                (size_t)r.table_count * kTableInfoSize);
     }
+    return TBC_OK;
+}
+
+tbc_status tbc_batch_speculation(tbc_batch *b, uint32_t index, uint32_t *out) {
+    if (!b || !out || index >= b->count) return TBC_ERR_INVALID_ARGUMENT;
+    if (!b->complete) return TBC_PENDING;
+    if (!b->children.empty()) {
+        const auto m = b->job_map[index];
+        return tbc_batch_speculation(b->children[m.first], m.second, out);
+    }
+    if (b->result == TBC_ERR_DEVICE) return TBC_ERR_DEVICE;
+    *out = b->h_results[index].spec;
     return TBC_OK;
 }
 

@@ -76,11 +76,12 @@ __device__ __forceinline__ uint32_t merge_path_split(const JobDesc &j, uint32_t 
 }
 
 __global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int njobs, uint32_t nsplits,
-                                                       SplitDesc *splits) {
+                                                       SplitDesc *splits, const JobResultDev *res, uint32_t phase) {
     const uint32_t gsplit = blockIdx.x * 256 + threadIdx.x;
     if (gsplit >= nsplits) return;
     const int ji = find_job(jobs, njobs, gsplit, [](const JobDesc &d) { return d.split_base; });
     const JobDesc &j = jobs[ji];
+    if (phase_skips(j, res, phase)) return;
     const uint32_t t = gsplit - j.split_base;
     const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
     const uint32_t d = (uint64_t)t * kMergeTile < n ? t * kMergeTile : n;
@@ -98,6 +99,56 @@ __global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int 
     s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
     s.pad = 0;
     splits[gsplit] = s;
+}
+
+// Speculated jobs (TBC_COMPACTION_UNIQUE_KEYS): with every value surviving,
+// data block k holds merged positions [k * vcm, (k + 1) * vcm); its producer
+// starts from the merge-path split at k * vcm. The thread of block 0 also
+// writes the job's speculative results (write_blocks' shape for n values,
+// compaction.zig:806-850); a broken speculation has them rewritten by the
+// recomputation's k_tile_scan.
+__global__ __launch_bounds__(256) void k_partition_blocks(const JobDesc *jobs, int njobs, uint32_t total,
+                                                          SplitDesc *bsplits, JobResultDev *res) {
+    const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= total) return;
+    const int ji = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
+    const JobDesc &j = jobs[ji];
+    const uint32_t k = m - j.dblock_base;
+    if (!j.unique || k >= j.dblock_max) return;
+    const uint32_t na = j.a.n, nb = j.b.n;
+    const uint32_t d = k * j.vcm;
+    uint32_t lo;
+    switch (j.key_kind) {
+    case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
+    case kKeyIdU128: lo = merge_path_split<kKeyIdU128>(j, d); break;
+    case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
+    default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
+    }
+    SplitDesc s;
+    s.i = lo;
+    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
+    const uint32_t jb = d - lo;
+    s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
+    // Segment of B[jb - 1] (the value before the block on the B side).
+    s.pad = nb && jb > 0 ? seg_search(j.b, jb - 1 < nb ? jb - 1 : nb - 1) : 0;
+    bsplits[m] = s;
+    if (k == 0) {
+        JobResultDev &r = res[j.job_index];
+        const uint64_t n = (uint64_t)na + nb;
+        r.value_count = n;
+        r.data_block_count = j.dblock_max;
+        r.table_count = j.table_max;
+        r.block_count = j.dblock_max + j.table_max;
+        r.spec = kSpecHeld;
+    }
+}
+
+int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, SplitDesc *d_bsplits,
+                            JobResultDev *d_results, void *stream) {
+    if (!total_dblocks) return 0;
+    hipLaunchKernelGGL(k_partition_blocks, dim3((total_dblocks + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       d_jobs, njobs, total_dblocks, d_bsplits, d_results);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // --------------------------------------------------------------------------
@@ -127,7 +178,8 @@ template <int KIND, bool ASM>
 __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
                                                               uint32_t order_offset, const SplitDesc *splits,
                                                               uint64_t *status, uint64_t *masks, uint64_t *lookback,
-                                                              uint32_t *ticket, uint32_t *ready) {
+                                                              uint32_t *ticket, uint32_t *ready,
+                                                              const JobResultDev *res, uint32_t phase) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -139,6 +191,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     if (ASM) __syncthreads();
     const TileRef ref = order[order_offset + (ASM ? s_ticket : blockIdx.x)];
     const JobDesc &j = jobs[ref.job];
+    if (!ASM && phase_skips(j, res, phase)) return; // (speculating batches never assemble in the merge)
     const uint32_t t = ref.tile;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * kMergeTile;
@@ -425,10 +478,11 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
 constexpr uint32_t kScanThreads = 1024;
 
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const JobDesc *jobs, uint64_t *status,
-                                                           uint32_t *block_tile, JobResultDev *res) {
+                                                           uint32_t *block_tile, JobResultDev *res, uint32_t phase) {
     __shared__ uint32_t wsum[kScanThreads / 64];
     __shared__ uint64_t carry;
     const JobDesc &j = jobs[blockIdx.x];
+    if (phase_skips(j, res, phase)) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     uint64_t *st = status + j.tile_base;
     if (tid == 0) carry = 0;
@@ -471,25 +525,30 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const JobDesc *jobs,
 }
 
 template <int KIND>
-static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
+static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
                        SplitDesc *d_splits, uint64_t *d_status, uint64_t *d_masks, const TileRef *d_order,
-                       uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready, hipStream_t s) {
+                       uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready, const JobResultDev *d_res,
+                       hipStream_t s) {
     const JobDesc &f = h_jobs[first];
     const JobDesc &l = h_jobs[first + count - 1];
     const uint32_t split_off = f.split_base;
     const uint32_t nsplits = l.split_base + l.tile_count + 1 - split_off;
     const uint32_t tile_off = f.tile_base;
     const uint32_t ntiles = l.tile_base + l.tile_count - tile_off;
-    (void)phase;
     (void)split_off;
     (void)nsplits;
+    // Jobs of this kind that the phase runs (host-known: speculated or not).
+    bool any = false;
+    for (int k = first; k < first + count; k++) any |= phase == 0 ? !h_jobs[k].unique : h_jobs[k].unique != 0;
+    if (!any) return 0;
     if (ntiles && d_lookback)
         hipLaunchKernelGGL((k_merge_tile<KIND, true>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
                            tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket + KIND,
-                           d_ready);
+                           d_ready, d_res, phase);
     else if (ntiles)
         hipLaunchKernelGGL((k_merge_tile<KIND, false>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
-                           tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket, d_ready);
+                           tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket, d_ready,
+                           d_res, phase);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -499,8 +558,11 @@ static int launch_kind(int phase, const JobDesc *d_jobs, const JobDesc *h_jobs, 
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
                  uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
                  JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx,
-                 uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready) {
+                 uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready, uint32_t phase) {
     hipStream_t s = (hipStream_t)stream;
+    bool any = false;
+    for (int k = 0; k < njobs; k++) any |= phase == 0 ? !h_jobs[k].unique : h_jobs[k].unique != 0;
+    if (!any) return 0;
     auto for_each_kind = [&](auto fn) {
         int first = 0;
         while (first < njobs) {
@@ -511,13 +573,13 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
         }
         return 0;
     };
-    auto phase = [&](int ph) {
+    auto run = [&](uint32_t ph) {
         return for_each_kind([&](uint32_t kind, int first, int count) {
             switch (kind) {
-            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
-            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
-            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
-            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, s);
+            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
+            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
+            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
+            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
             }
         });
     };
@@ -525,15 +587,15 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
         const JobDesc &l = h_jobs[njobs - 1];
         const uint32_t nsplits = l.split_base + l.tile_count + 1;
         hipLaunchKernelGGL(k_partition_all, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
-                           d_splits);
+                           d_splits, (const JobResultDev *)d_results, phase);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    if (mark) mark(mark_ctx, "merge_partition");
-    if (phase(1)) return -1;
+    if (mark) mark(mark_ctx, phase ? "recompute_partition" : "merge_partition");
+    if (run(phase)) return -1;
     hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
-                       d_results);
+                       d_results, phase);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (mark) mark(mark_ctx, "merge");
+    if (mark) mark(mark_ctx, phase ? "recompute_merge" : "merge");
     return 0;
 }
 

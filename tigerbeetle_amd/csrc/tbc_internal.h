@@ -48,7 +48,9 @@ struct JobDesc {
     uint32_t block_size;
     uint16_t tree_id;
     uint8_t a_immutable, drop_tombstones;
-    uint8_t level_b, pad0[3];
+    uint8_t level_b;
+    uint8_t unique; // TBC_COMPACTION_UNIQUE_KEYS held by the batch's plan (latency regime): blocks by speculation
+    uint8_t pad0[2];
     uint64_t cluster_lo, cluster_hi, snapshot_min;
     Stream a, b;
     const uint64_t *addresses;
@@ -88,7 +90,19 @@ struct JobResultDev {
     uint32_t status;
     uint32_t invariant;   // nonzero if an input broke a reference invariant
     uint32_t block_error; // nonzero if a grid input block failed its checks (tbc_block_check code)
+    uint32_t spec;        // unique-keys speculation: 0 none, 1 held, 2 broken (recomputed by the merge path)
+    uint32_t pad;
 };
+
+constexpr uint32_t kSpecNone = 0, kSpecHeld = 1, kSpecBroken = 2;
+constexpr uint32_t kPhaseProducersOnly = 2; // timing probe (TBC_PROBE_PRODUCERS_ONLY): blocks without chains
+// Launch phases of a batch with speculated jobs: phase 0 runs every
+// non-speculated job (and the speculative block phase), phase 1 only the
+// speculated jobs whose speculation broke.
+__device__ __forceinline__ bool phase_skips(const JobDesc &j, const JobResultDev *res, uint32_t phase) {
+    if (phase == 0) return j.unique != 0;
+    return !j.unique || *(volatile const uint32_t *)&res[j.job_index].spec != kSpecBroken;
+}
 
 // One grid input block of a batch (TBC_COMPACTION_GRID): the cache-hit checks
 // of read_block_from_cache (grid.zig:802-841) plus the header fields the
@@ -256,13 +270,20 @@ namespace tbc {
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
                  uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
                  JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx,
-                 uint64_t *d_lookback = nullptr, uint32_t *d_ticket = nullptr, uint32_t *d_ready = nullptr);
+                 uint64_t *d_lookback = nullptr, uint32_t *d_ticket = nullptr, uint32_t *d_ready = nullptr,
+                 uint32_t phase = 0);
+// Merge-path splits at the data-block boundaries of speculated jobs
+// (d_bsplits[dblock_base + k] for block k) and their results (every value
+// survives).
+int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, SplitDesc *d_bsplits,
+                            JobResultDev *d_results, void *stream);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                   const uint32_t *d_block_tile, const SplitDesc *d_splits, bool values_only, bool maybe_sparse,
                   void *stream,
-                  void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done = false);
+                  void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done = false,
+                  const SplitDesc *d_bsplits = nullptr, uint32_t phase = 0, bool index_blocks = true);
 int launch_validate_blocks(const uint64_t *d_ptrs, const uint64_t *d_expect, uint32_t count, uint32_t block_size,
                           uint8_t *d_out, void *stream);
 // Grid inputs of a batch (engine.hip): resolve data blocks from the index

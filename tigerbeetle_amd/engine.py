@@ -69,7 +69,7 @@ class Job:
     snapshot_min: int
     addresses: np.ndarray  # uint64, acquire order
     output: DeviceBuffer
-    flags: int = 0  # TBC_COMPACTION_* (abi.COMPACTION_VALUES_ONLY, abi.COMPACTION_GRID)
+    flags: int = 0  # TBC_COMPACTION_* (abi.COMPACTION_VALUES_ONLY, abi.COMPACTION_GRID, abi.COMPACTION_UNIQUE_KEYS)
     grid: "Grid | None" = None   # COMPACTION_GRID: disk tables by reference, outputs into the grid
     tables_a: list = field(default_factory=list)  # [(index address, index checksum u128, value_count)]
     tables_b: list = field(default_factory=list)
@@ -214,6 +214,12 @@ class Batch:
         check(lib().tbc_batch_result(self.handle, index, ctypes.byref(r), infos.ctypes.data, r.table_count),
               "tbc_batch_result")
         return r, infos[: r.table_count]
+
+    def speculation(self, index: int) -> int:
+        """abi.SPECULATION_NONE / _HELD / _BROKEN of compaction `index` (tbc_batch_speculation)."""
+        out = ctypes.c_uint32()
+        check(lib().tbc_batch_speculation(self.handle, index, ctypes.byref(out)), "tbc_batch_speculation")
+        return out.value
 
     def kernel_times(self) -> dict:
         cap = 32

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Wide producers: unique tests + parity, producer-only probes and full lines of configs 2 and 4.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r02q
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_unique.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $OUT/unique.log 2>&1 || { echo UNIQUE_FAILED; tail -30 $OUT/unique.log; exit 1; }
+tail -1 $OUT/unique.log
+for c in 2 4; do
+TBC_PROBE_PRODUCERS_ONLY=1 timeout -k 10 200 python -u bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline > $OUT/p$c.log 2>&1 || { echo P${c}_FAILED; tail -20 $OUT/p$c.log; exit 1; }
+echo "p$c $(grep -o '"ms_per_step": [0-9.]*' $OUT/p$c.log) $(grep -o '"data_blocks": [0-9.]*' $OUT/p$c.log)"
+timeout -k 10 200 python -u bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline > $OUT/c$c.log 2>&1 || { echo C${c}_FAILED; tail -20 $OUT/c$c.log; exit 1; }
+echo "c$c $(grep -o '"ms_per_step": [0-9.]*' $OUT/c$c.log) $(grep -o '"kernels_us_per_step[^}]*}' $OUT/c$c.log)"
+done
