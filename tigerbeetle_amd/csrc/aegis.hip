@@ -987,7 +987,10 @@ __device__ __forceinline__ void produce_unique(const JobDesc &j, uint32_t k, uin
         }
     }
     if (bad) {
-        if (lane == 0) __hip_atomic_store(spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            __hip_atomic_store(spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // The chains still run to the end of the block: release them.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1019,6 +1022,38 @@ template <int KL> __device__ __forceinline__ Key<KL> key_readlane(const Key<KL> 
     return r;
 }
 
+// Inclusive wave prefix sum by DPP (row shifts, then row broadcasts 15/31).
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true); // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true); // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true); // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true); // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false); // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return x;
+}
+
+// Key of lane - 1 (wave_shr:1 DPP; lane 0 gets `first`).
+template <int KL> __device__ __forceinline__ Key<KL> key_prev_lane(const Key<KL> &k, const Key<KL> &first) {
+    Key<KL> r;
+    const bool l0 = (threadIdx.x & 63) == 0;
+#pragma unroll
+    for (int l = 0; l < KL; l++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)k.l[l], 0x138, 0xf, 0xf, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(k.l[l] >> 32), 0x138, 0xf, 0xf,
+                                                                  false);
+        r.l[l] = l0 ? first.l[l] : ((uint64_t)hi << 32 | lo);
+    }
+    return r;
+}
+
+template <int KL> __device__ __forceinline__ Key<KL> key_lds(const uint64_t *keys, uint32_t pos) {
+    Key<KL> r;
+#pragma unroll
+    for (int l = 0; l < KL; l++) r.l[l] = keys[l * 128 + pos];
+    return r;
+}
+
 template <int KIND, int VW>
 __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
                                                     uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
@@ -1046,7 +1081,8 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
         last_b = load_key<KIND>((const uint8_t *)(uintptr_t)gld<uint64_t>(j.b.seg_ptr + s) +
                                     (size_t)(ib - 1 - gld<uint32_t>(j.b.seg_pre + s)) * vs, ts);
     }
-    uint32_t *hist = (uint32_t *)stage; // 128 bins
+    uint64_t *bkeys = stage;                     // KL x 128 keys of the B window
+    uint32_t *hist = (uint32_t *)(stage + 3 * 128); // 128 bins
     bool bad = false;
     u32x4 xa[2][VW], xb[2][VW];
     bool va[2], vb[2];
@@ -1112,14 +1148,24 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
             t_wait += t - t_mark;
             t_mark = t;
         }
-        // A ranks among the B window (lower bound).
+        // The B window's keys into this wave's LDS (limb-major, 128 per limb).
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int l = 0; l < KL; l++) bkeys[l * 128 + lane + 64 * q] = kb[q].l[l];
+        hist[lane] = 0;
+        hist[lane + 64] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // A ranks among the B window (lower bound), binary search in LDS.
         uint32_t lo[2] = {0, 0}, hi[2] = {nbv, nbv};
 #pragma unroll
         for (int it = 0; it < 8; it++) {
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 const uint32_t m = (lo[q] + hi[q]) >> 1;
-                const Key<KL> at = key_of_slot(kb, m < W - 1 ? m : W - 1);
+                const Key<KL> at = key_lds<KL>(bkeys, m < W - 1 ? m : W - 1);
                 if (lo[q] < hi[q]) {
                     if (key_lt(at, ka[q])) lo[q] = m + 1;
                     else hi[q] = m;
@@ -1133,23 +1179,14 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
             t_mark = t;
         }
         // Histogram of the A ranks, prefix: A values at or before each B position.
-        hist[lane] = 0;
-        hist[lane + 64] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int q = 0; q < 2; q++)
             if (va[q] && lo[q] < W) __hip_atomic_fetch_add(&hist[lo[q]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t c0 = hist[lane], c1 = hist[lane + 64];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y0 = __shfl_up(c0, o, 64), y1 = __shfl_up(c1, o, 64);
-            if (lane >= (uint32_t)o) c0 += y0, c1 += y1;
-        }
-        c1 += __shfl(c0, 63, 64);
+        uint32_t c0 = wave_scan_incl(hist[lane]), c1 = wave_scan_incl(hist[lane + 64]);
+        c1 += __builtin_amdgcn_readlane((int)c0, 63);
         if (probe) {
             asm volatile("" ::"v"(c0), "v"(c1));
             const uint64_t t = wall_clock64();
@@ -1175,15 +1212,14 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
         bool eq = false;
 #pragma unroll
         for (int q = 0; q < 2; q++) {
-            const Key<KL> lb = key_of_slot(kb, lo[q] < W - 1 ? lo[q] : W - 1);
+            const Key<KL> lb = key_lds<KL>(bkeys, lo[q] < W - 1 ? lo[q] : W - 1);
             eq |= ea[q] && lo[q] < nbv && key_eq(lb, ka[q]);
-            const Key<KL> pa_ = key_of_lane(ka[q], lane ? lane - 1 : 0);
-            const Key<KL> pb_ = key_of_lane(kb[q], lane ? lane - 1 : 0);
             const Key<KL> first_a = q == 0 ? last_a : key_readlane(ka[0], 63);
             const Key<KL> first_b = q == 0 ? last_b : key_readlane(kb[0], 63);
             const bool ha = q == 0 ? has_a : true, hb = q == 0 ? has_b : true;
-            eq |= ea[q] && (lane ? key_eq(pa_, ka[q]) : (ha && key_eq(first_a, ka[q])));
-            eq |= eb[q] && (lane ? key_eq(pb_, kb[q]) : (hb && key_eq(first_b, kb[q])));
+            const Key<KL> pa_ = key_prev_lane(ka[q], first_a), pb_ = key_prev_lane(kb[q], first_b);
+            eq |= ea[q] && (lane || ha) && key_eq(pa_, ka[q]);
+            eq |= eb[q] && (lane || hb) && key_eq(pb_, kb[q]);
             if (j.drop_tombstones) eq |= ea[q] && ta[q];
         }
         bad |= __ballot(eq) != 0;
@@ -1218,7 +1254,10 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (bad && lane == 0) __hip_atomic_store(spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bad && lane == 0) {
+        __hip_atomic_store(spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (lane == 0) __hip_atomic_store(prog, len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (probe && lane == 0) {
         t_rest += wall_clock64() - t_mark;
@@ -1261,6 +1300,7 @@ __device__ __forceinline__ void produce_unique_vs(const JobDesc &j, uint32_t k, 
 // Fused: C chain + 2C producer waves, C <= 4 (768 threads), so the kernel may
 // use 168 VGPRs (3 waves per SIMD) and the producers do not spill.
 constexpr uint32_t kMaxChainWaves = 4;
+constexpr uint32_t kStageWords = 448; // producer LDS (u64): 3 x 128 B-window key limbs + 128 rank bins
 constexpr uint32_t kMaxChainOnlyWaves = 16;
 // Above this many chain waves (2 per SIMD) the two-pass path wins.
 constexpr uint32_t kFusedMaxChainWaves = 2048;
@@ -1276,7 +1316,10 @@ __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
-    __shared__ uint64_t sStage[Fused ? 2 * kMaxChainWaves : 1][128]; // producer copy staging
+    // Producer LDS: copy staging (merge-path producers), or the speculated
+    // producers' B window keys + rank histogram; everything the tables,
+    // headers and progress words leave of the CU's 160 KiB.
+    __shared__ uint64_t sStage[Fused ? 2 * kMaxChainWaves : 1][kStageWords];
     const uint32_t C = chain_waves;
     auto locate = [&](uint32_t m, int &ji_, uint32_t &k_) {
         ji_ = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
@@ -1342,6 +1385,9 @@ __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data
         return;
     }
     if (phase == kPhaseProducersOnly) return; // timing probe: no chains
+    // The chain is the critical path and mostly waits on LDS: let its
+    // instructions win the SIMD's issue arbitration over the producers'.
+    if constexpr (Fused) __builtin_amdgcn_s_setprio(2);
     const uint32_t wave = blockIdx.x * C + wave_in_block;
     const bool upper = lane >= 32;
     const uint32_t mine = 2 * wave + (upper ? 1u : 0u);
@@ -1420,6 +1466,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
     __shared__ uint64_t s_src[4][64], s_dst[4][64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1;
+    if (phase == 1 && *(volatile const uint32_t *)jobs[0].spec_any == 0) return; // no speculation broke
     for (uint32_t g = blockIdx.x; g < total_tiles; g += gridDim.x) {
         const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.tile_base; });
         const JobDesc &j = jobs[ji];

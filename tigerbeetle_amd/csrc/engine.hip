@@ -1066,6 +1066,13 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         d.a.n = (uint32_t)na;
         d.b.nseg = (uint32_t)seg_in[2 * (size_t)i + 1].size();
         d.b.n = (uint32_t)nb;
+        for (int side = 0; side < 2; side++) {
+            const auto &segs = seg_in[2 * (size_t)i + side];
+            bool uniform = !segs.empty();
+            for (size_t q = 0; q + 1 < segs.size() && uniform; q++) uniform = segs[q].second == segs[0].second;
+            (side == 0 ? d.a : d.b).uniform = uniform && !segs.empty() && segs.back().second <= segs[0].second
+                                                  ? segs[0].second : 0;
+        }
         d.address_count = c.address_count;
         d.out_blocks = grid ? nullptr : (uint8_t *)c.output_blocks;
         d.grid_base = grid ? c.grid->base : nullptr;
@@ -1207,6 +1214,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         memcpy(haddr + ap, c.addresses, 8ull * c.address_count);
         ap += c.address_count;
     }
+    for (uint32_t k = 0; k < count; k++) sj[k].spec_any = d_ticket + 4;
     memcpy(h_in, sj.data(), sizeof(JobDesc) * count);
     InputCheck *hchecks = (InputCheck *)(h_in + sz_jobs + sz_segs + sz_addr + sz_order);
     InputCheck *d_checks = (InputCheck *)(d_in + sz_jobs + sz_segs + sz_addr + sz_order);

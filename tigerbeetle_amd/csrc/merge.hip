@@ -23,6 +23,8 @@
 // AEGIS chain checksums it (aegis.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "tbc_internal.h"
 #include "keys.h"
 
@@ -38,6 +40,10 @@ __device__ __forceinline__ uint32_t load_tomb(const uint8_t *v, uint32_t ts_off)
 
 // Segment containing element idx: the largest s with seg_pre[s] <= idx.
 __device__ __forceinline__ uint32_t seg_search(const Stream &s, uint32_t idx) {
+    if (s.uniform) {
+        const uint32_t q = idx / s.uniform;
+        return q < s.nseg ? q : s.nseg - 1;
+    }
     uint32_t lo = 0, hi = s.nseg - 1;
     while (lo < hi) {
         uint32_t mid = (lo + hi + 1) >> 1;
@@ -107,9 +113,39 @@ __global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int 
 // writes the job's speculative results (write_blocks' shape for n values,
 // compaction.zig:806-850); a broken speculation has them rewritten by the
 // recomputation's k_tile_scan.
+// One wave per block: a 64-ary merge-path search (each round, the 64 lanes
+// probe 64 evenly spaced candidates and a ballot keeps the interval between
+// the last true and the first false), 4 dependent rounds for 2^24 values
+// instead of ~24 single-lane probes.
+template <int KIND>
+__device__ __forceinline__ uint32_t merge_path_split_wave(const JobDesc &j, uint32_t d) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nb = j.b.n, vs = j.value_size, ts = j.timestamp_offset;
+    uint32_t lo = d > nb ? d - nb : 0, hi = d < j.a.n ? d : j.a.n; // answer in [lo, hi]
+    while (lo < hi) {
+        const uint32_t span = hi - lo;
+        // candidate i: "A[i] sorts before B[d - 1 - i]" holds for i < answer
+        const uint32_t i = span <= 64 ? lo + lane : lo + (uint32_t)(((uint64_t)span * lane) >> 6);
+        bool pred = false;
+        if (i < hi) {
+            const uint8_t *pa = elem_ptr(j.a, seg_search(j.a, i), i, vs);
+            const uint8_t *pb = elem_ptr(j.b, seg_search(j.b, d - 1 - i), d - 1 - i, vs);
+            pred = key_le(load_key<KIND>(pa, ts), load_key<KIND>(pb, ts));
+        }
+        const uint64_t t = __ballot(pred && i < hi);
+        const uint32_t c = __builtin_popcountll(t); // predicates hold on a prefix of the lanes
+        if (span <= 64) return lo + c;
+        const uint32_t last_true = c ? lo + (uint32_t)(((uint64_t)span * (c - 1)) >> 6) : lo;
+        const uint32_t first_false = c < 64 ? lo + (uint32_t)(((uint64_t)span * c) >> 6) : hi;
+        lo = c ? last_true + 1 : lo;
+        hi = first_false;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(256) void k_partition_blocks(const JobDesc *jobs, int njobs, uint32_t total,
                                                           SplitDesc *bsplits, JobResultDev *res) {
-    const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (m >= total) return;
     const int ji = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
     const JobDesc &j = jobs[ji];
@@ -119,11 +155,12 @@ __global__ __launch_bounds__(256) void k_partition_blocks(const JobDesc *jobs, i
     const uint32_t d = k * j.vcm;
     uint32_t lo;
     switch (j.key_kind) {
-    case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
-    case kKeyIdU128: lo = merge_path_split<kKeyIdU128>(j, d); break;
-    case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
-    default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
+    case kKeyTimestamp: lo = merge_path_split_wave<kKeyTimestamp>(j, d); break;
+    case kKeyIdU128: lo = merge_path_split_wave<kKeyIdU128>(j, d); break;
+    case kKeyCompositeU64: lo = merge_path_split_wave<kKeyCompositeU64>(j, d); break;
+    default: lo = merge_path_split_wave<kKeyCompositeU128>(j, d); break;
     }
+    if ((threadIdx.x & 63) != 0) return;
     SplitDesc s;
     s.i = lo;
     s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
@@ -146,7 +183,7 @@ __global__ __launch_bounds__(256) void k_partition_blocks(const JobDesc *jobs, i
 int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, SplitDesc *d_bsplits,
                             JobResultDev *d_results, void *stream) {
     if (!total_dblocks) return 0;
-    hipLaunchKernelGGL(k_partition_blocks, dim3((total_dblocks + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_partition_blocks, dim3((total_dblocks + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                        d_jobs, njobs, total_dblocks, d_bsplits, d_results);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -175,11 +212,10 @@ template <int KL> struct TileShared {
 constexpr uint64_t kMlbAggregate = 1ull << 62, kMlbPrefix = 2ull << 62, kMlbCount = (1ull << 62) - 1;
 
 template <int KIND, bool ASM>
-__global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
-                                                              uint32_t order_offset, const SplitDesc *splits,
-                                                              uint64_t *status, uint64_t *masks, uint64_t *lookback,
-                                                              uint32_t *ticket, uint32_t *ready,
-                                                              const JobResultDev *res, uint32_t phase) {
+__device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *order, uint32_t order_offset,
+                                           const SplitDesc *splits, uint64_t *status, uint64_t *masks,
+                                           uint64_t *lookback, uint32_t *ticket, uint32_t *ready,
+                                           const JobResultDev *res, uint32_t phase, uint32_t slot) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -189,7 +225,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     __shared__ uint32_t s_ticket;
     if (ASM && tid == 0) s_ticket = atomicAdd(ticket, 1u);
     if (ASM) __syncthreads();
-    const TileRef ref = order[order_offset + (ASM ? s_ticket : blockIdx.x)];
+    const TileRef ref = order[order_offset + (ASM ? s_ticket : slot)];
     const JobDesc &j = jobs[ref.job];
     if (!ASM && phase_skips(j, res, phase)) return; // (speculating batches never assemble in the merge)
     const uint32_t t = ref.tile;
@@ -470,6 +506,32 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     }
 }
 
+// One merge tile per workgroup.
+template <int KIND, bool ASM>
+__global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
+                                                              uint32_t order_offset, const SplitDesc *splits,
+                                                              uint64_t *status, uint64_t *masks, uint64_t *lookback,
+                                                              uint32_t *ticket, uint32_t *ready,
+                                                              const JobResultDev *res, uint32_t phase) {
+    merge_tile<KIND, ASM>(jobs, order, order_offset, splits, status, masks, lookback, ticket, ready, res, phase,
+                          blockIdx.x);
+}
+
+// The recomputation phase of a speculating batch: a small grid strides over
+// the tiles (most leave at once, all of them while no speculation broke).
+template <int KIND>
+__global__ __launch_bounds__(kMergeThreads) void k_merge_tile_redo(const JobDesc *jobs, const TileRef *order,
+                                                                   uint32_t order_offset, const SplitDesc *splits,
+                                                                   uint64_t *status, uint64_t *masks,
+                                                                   const JobResultDev *res, uint32_t ntiles) {
+    if (*(volatile const uint32_t *)jobs[0].spec_any == 0) return;
+    for (uint32_t slot = blockIdx.x; slot < ntiles; slot += gridDim.x) {
+        merge_tile<KIND, false>(jobs, order, order_offset, splits, status, masks, nullptr, nullptr, nullptr, res, 1u,
+                                slot);
+        __syncthreads();
+    }
+}
+
 // Per job (one workgroup): exclusive scan of the tile survivor counts into
 // status[t] = count | offset << 32, the output shape (write_blocks,
 // compaction.zig:806-850: full data blocks except the last, full tables
@@ -541,7 +603,10 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
     bool any = false;
     for (int k = first; k < first + count; k++) any |= phase == 0 ? !h_jobs[k].unique : h_jobs[k].unique != 0;
     if (!any) return 0;
-    if (ntiles && d_lookback)
+    if (ntiles && phase)
+        hipLaunchKernelGGL((k_merge_tile_redo<KIND>), dim3(std::min<uint32_t>(ntiles, 1024)), dim3(kMergeThreads), 0,
+                           s, d_jobs, d_order, tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_res, ntiles);
+    else if (ntiles && d_lookback)
         hipLaunchKernelGGL((k_merge_tile<KIND, true>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
                            tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket + KIND,
                            d_ready, d_res, phase);

@@ -38,6 +38,11 @@ struct Stream {
     const uint32_t *seg_pre; // prefix counts, nseg + 1 entries
     uint32_t nseg;
     uint32_t n; // total values
+    // Nonzero when every segment but the last holds exactly this many values
+    // (full data blocks: one disk table, or tables of whole blocks): the
+    // segment of an element is then a division, not a binary search.
+    uint32_t uniform;
+    uint32_t pad;
 };
 
 struct JobDesc {
@@ -66,6 +71,9 @@ struct JobDesc {
     uint32_t job_index;
     // TBC_COMPACTION_GRID: output block `slot` lives at grid_base + (addresses[slot] - 1) * block_size.
     uint8_t *grid_base;
+    // Speculating batches: the number of broken speculations (one word of the
+    // batch's zeroed scratch); phase-1 kernels leave at once while it is 0.
+    uint32_t *spec_any;
 };
 
 struct SplitDesc {
@@ -101,7 +109,8 @@ constexpr uint32_t kPhaseProducersOnly = 2; // timing probe (TBC_PROBE_PRODUCERS
 // speculated jobs whose speculation broke.
 __device__ __forceinline__ bool phase_skips(const JobDesc &j, const JobResultDev *res, uint32_t phase) {
     if (phase == 0) return j.unique != 0;
-    return !j.unique || *(volatile const uint32_t *)&res[j.job_index].spec != kSpecBroken;
+    return !j.unique || *(volatile const uint32_t *)j.spec_any == 0 ||
+           *(volatile const uint32_t *)&res[j.job_index].spec != kSpecBroken;
 }
 
 // One grid input block of a batch (TBC_COMPACTION_GRID): the cache-hit checks
