@@ -1306,12 +1306,11 @@ constexpr uint32_t kMaxChainOnlyWaves = 16;
 constexpr uint32_t kFusedMaxChainWaves = 2048;
 
 template <bool Fused, class ChainStep = StepBpermute>
-__global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data_blocks(const JobDesc *jobs, int njobs, uint32_t total,
-                                                      const JobResultDev *res, const uint64_t *status,
-                                                      const uint64_t *masks, const uint32_t *block_tile,
-                                                      const SplitDesc *splits, uint32_t chain_waves,
-                                                      const uint32_t *ready, const SplitDesc *bsplits,
-                                                      uint32_t phase) {
+__device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res,
+                                            const uint64_t *status, const uint64_t *masks,
+                                            const uint32_t *block_tile, const SplitDesc *splits,
+                                            uint32_t chain_waves, const uint32_t *ready, const SplitDesc *bsplits,
+                                            uint32_t phase) {
     constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
@@ -1350,7 +1349,7 @@ __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data
         const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
         if (!locate(mine, ji, k)) return;
         const JobDesc &j = jobs[ji];
-        if (j.unique && phase != 1) { // speculated: this producer merges the block's values itself
+        if (j.unique && phase != 1 && phase != kPhaseChainsAlone) { // speculated: merges the block's values itself
             uint8_t *blk = block_ptr(j, data_block_slot(k, j.dbcm));
             const SplitDesc sp = bsplits[j.dblock_base + k];
             uint32_t *err = const_cast<uint32_t *>(&res[j.job_index].invariant);
@@ -1373,7 +1372,7 @@ __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data
             }
             return;
         }
-        if (sparse_job(j, res)) { // body written by k_assemble<true> (stream order)
+        if (sparse_job(j, res) || phase == kPhaseChainsAlone) { // body written by k_assemble (stream order)
             if (lane == 0)
                 __hip_atomic_store(&sProg[p], block_count(j, k) * j.value_size, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1446,6 +1445,24 @@ __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data
         const uint32_t end = (uint32_t)sector_ceil(size);
         for (uint32_t o = size + 4 * g; o < end; o += 128) gst<uint32_t>(blk + o, 0u);
     }
+}
+
+template <bool Fused, class ChainStep = StepBpermute>
+__global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data_blocks(
+    const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res, const uint64_t *status,
+    const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
+    const uint32_t *ready, const SplitDesc *bsplits, uint32_t phase) {
+    data_blocks<Fused, ChainStep>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready,
+                                  bsplits, phase);
+}
+
+// The recomputation of broken speculations (phase 1) in its own symbol, so
+// profiles keep it apart from the block pass.
+__global__ __launch_bounds__(3 * 64 * kMaxChainWaves) void k_data_blocks_redo(
+    const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res, const uint64_t *status,
+    const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
+    const uint32_t *ready) {
+    data_blocks<true>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready, nullptr, 1u);
 }
 
 // Throughput regime, pass 1: assemble every data block body from the merge's
@@ -1750,10 +1767,22 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         uint32_t c = waves_per_block(waves);
         c = c > kMaxChainWaves ? kMaxChainWaves : c;
         static const bool producers_only = getenv("TBC_PROBE_PRODUCERS_ONLY") != nullptr; // timing probe only
-        hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
-                           total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile, d_splits,
-                           c, (const uint32_t *)d_ready, d_bsplits,
-                           phase == 0 && producers_only ? kPhaseProducersOnly : phase);
+        static const bool chains_alone = getenv("TBC_PROBE_CHAINS_ALONE") != nullptr;      // timing probe only
+        if (chains_alone && phase == 0) {
+            const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, 0u);
+            if (mark) mark(mark_ctx, "probe_assemble");
+        }
+        if (phase == 1)
+            hipLaunchKernelGGL(k_data_blocks_redo, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
+                               total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
+                               d_splits, c, (const uint32_t *)d_ready);
+        else
+            hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
+                               total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
+                               d_splits, c, (const uint32_t *)d_ready, d_bsplits,
+                               producers_only ? kPhaseProducersOnly : chains_alone ? kPhaseChainsAlone : 0u);
         if (hipGetLastError() != hipSuccess) return -1;
     } else if (total_dblocks) {
         // Throughput regime: assemble every body, then the chains, 4 per SIMD.

@@ -104,6 +104,7 @@ struct JobResultDev {
 
 constexpr uint32_t kSpecNone = 0, kSpecHeld = 1, kSpecBroken = 2;
 constexpr uint32_t kPhaseProducersOnly = 2; // timing probe (TBC_PROBE_PRODUCERS_ONLY): blocks without chains
+constexpr uint32_t kPhaseChainsAlone = 3;   // timing probe (TBC_PROBE_CHAINS_ALONE): bodies first, chains alone
 // Launch phases of a batch with speculated jobs: phase 0 runs every
 // non-speculated job (and the speculative block phase), phase 1 only the
 // speculated jobs whose speculation broke.

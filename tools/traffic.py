@@ -51,7 +51,12 @@ def main() -> None:
     stats = find(os.path.join(src, "trace"), "*kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
-    avg_ns = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
+    # Instantiations of one kernel share a short name: keep the heaviest.
+    avg_ns, tot_ns = {}, {}
+    for r in csv.DictReader(open(stats)):
+        k = short(r["Name"])
+        if float(r["TotalDurationNs"]) > tot_ns.get(k, -1.0):
+            avg_ns[k], tot_ns[k] = float(r["AverageNs"]), float(r["TotalDurationNs"])
     fetch = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(src, "write"), "WRITE_SIZE")
     md5 = open(os.path.join(src, "lib.md5")).read().split()[0]
