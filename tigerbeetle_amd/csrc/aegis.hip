@@ -265,6 +265,7 @@ struct BodyMsg {
     uint32_t max_off;
     const uint32_t *prog; // LDS
     uint32_t *err;        // JobResultDev.invariant: set if the producer never delivers
+    mutable uint32_t seen = 0; // progress already acquired: no LDS read, no fence below it
     __device__ __forceinline__ BodyMsg(const uint8_t *b, uint32_t l, const uint32_t *p, uint32_t *e)
         : base(b), len(l), max_off(l >= 4 ? l - 4 : 0), prog(p), err(e) {}
     __device__ __forceinline__ Addr addr(uint32_t off) const { return base + (off < max_off ? off : max_off); }
@@ -273,8 +274,11 @@ struct BodyMsg {
     __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
     __device__ __forceinline__ void ready(uint32_t upto) const {
         const uint32_t need = upto < len ? upto : len;
+        // Whole wave: both 32-lane groups' blocks covered by what was acquired.
+        if (!__any(need > seen)) return;
+        uint32_t have = 0;
         for (uint32_t spins = 0;; spins++) {
-            const uint32_t have = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            have = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const bool late = have < need;
             if (!__any(late)) break;
             if (spins > (1u << 22)) { // bounded: report instead of hanging
@@ -284,6 +288,7 @@ struct BodyMsg {
             __builtin_amdgcn_s_sleep(2);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        seen = have; // everything published up to `have` is now visible to this wave
     }
 };
 
