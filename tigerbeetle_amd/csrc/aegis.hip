@@ -776,6 +776,40 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
     }
 }
 
+// Data block k of job j, body checksummed (`body_tag`: column lane & 3 of
+// the tag, per 32-lane group): header fields, header checksum, the header
+// and the zeroed sector tail stored by the `writer` group.
+__device__ __forceinline__ void finish_data_block(const uint32_t *sT, uint32_t *hdr, const JobDesc &j, uint32_t k,
+                                                  uint32_t cnt, uint32_t body_tag, bool writer) {
+    const uint32_t slot = data_block_slot(k, j.dbcm);
+    uint8_t *blk = block_ptr(j, slot);
+    const uint32_t size = kHeaderSize + cnt * j.value_size;
+    HeaderFields h;
+    h.cluster_lo = j.cluster_lo;
+    h.cluster_hi = j.cluster_hi;
+    h.address = gld<uint64_t>(j.addresses + slot);
+    h.snapshot = j.snapshot_min;
+    h.size = size;
+    h.meta0 = j.vcm;        // TableData.Metadata.value_count_max
+    h.meta1 = cnt;          // .value_count
+    h.meta2 = j.value_size; // .value_size
+    h.meta3 = j.tree_id;    // .tree_id (u16), reserved = 0
+    h.block_type = 5;       // BlockType.data (schema.zig:65)
+    const uint32_t hdr_tag = finish_header(sT, hdr, h, body_tag);
+    const uint32_t g = threadIdx.x & 31;
+    if (g < 4) hdr[g] = hdr_tag;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (writer) {
+        gst<uint32_t>(blk + 4 * g, hdr[g]);
+        gst<uint32_t>(blk + 4 * (g + 32), hdr[g + 32]);
+        // Zero [size, sector_ceil(size)) (grid.zig:686).
+        const uint32_t end = (uint32_t)sector_ceil(size);
+        for (uint32_t o = size + 4 * g; o < end; o += 128) gst<uint32_t>(blk + o, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Key of lane `src` (ds_bpermute of each 32-bit half; the whole wave active).
 template <int KL> __device__ __forceinline__ Key<KL> key_of_lane(const Key<KL> &k, uint32_t src) {
     Key<KL> r;
@@ -1426,30 +1460,8 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         body_tag = aegis_mac32<GlobalMsg, ChainStep>(sT, body);
     }
 
-    HeaderFields h;
-    h.cluster_lo = j.cluster_lo;
-    h.cluster_hi = j.cluster_hi;
-    h.address = gld<uint64_t>(j.addresses + slot);
-    h.snapshot = j.snapshot_min;
-    h.size = size;
-    h.meta0 = j.vcm;        // TableData.Metadata.value_count_max
-    h.meta1 = cnt;          // .value_count
-    h.meta2 = j.value_size; // .value_size
-    h.meta3 = j.tree_id;    // .tree_id (u16), reserved = 0
-    h.block_type = 5;       // BlockType.data (schema.zig:65)
-    uint32_t *hdr = sHdr[wave_in_block][upper ? 1 : 0];
-    const uint32_t hdr_tag = finish_header(sT, hdr, h, body_tag);
-    const uint32_t g = lane & 31;
-    if (g < 4) hdr[g] = hdr_tag;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (writer) {
-        gst<uint32_t>(blk + 4 * g, hdr[g]);
-        gst<uint32_t>(blk + 4 * (g + 32), hdr[g + 32]);
-        // Zero [size, sector_ceil(size)) (grid.zig:686).
-        const uint32_t end = (uint32_t)sector_ceil(size);
-        for (uint32_t o = size + 4 * g; o < end; o += 128) gst<uint32_t>(blk + o, 0u);
-    }
+    (void)size;
+    finish_data_block(sT, sHdr[wave_in_block][upper ? 1 : 0], j, k, cnt, body_tag, writer);
 }
 
 template <bool Fused, class ChainStep = StepBpermute>
