@@ -201,6 +201,7 @@ static bool stage_d2h(tbc_engine *e, void *dst, const void *src, uint64_t bytes)
     return true;
 }
 
+constexpr uint64_t kInitialMaskWords = (1ull << 28) / kMergeTile * (2 * kMergeTile / 64);
 static bool ensure_masks(tbc_engine *e, uint64_t words) {
     if (words <= e->mask_words) return true;
     if (hipStreamSynchronize(e->stream) != hipSuccess) return false;
@@ -332,6 +333,10 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
                   hipSuccess;
     for (int s = 0; ok && s < Staging::kSlots; s++)
         ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
+    // The merge's mask buffer, sized up front for batches of up to 2^28
+    // values (64 MiB of HBM), so submitting never waits on the device to grow
+    // it; a larger batch still grows it (after a stream synchronize).
+    ok = ok && ensure_masks(e, kInitialMaskWords);
     if (!ok) {
         tbc_engine_deinit(e);
         return TBC_ERR_OUT_OF_MEMORY;
