@@ -1197,10 +1197,21 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // A ranks among the B window (lower bound), binary search in LDS.
-        uint32_t lo[2] = {0, 0}, hi[2] = {nbv, nbv};
+        // A ranks among the B window (lower bound): the bucket of 16 among
+        // eight splitters B[16s + 15] (uniform LDS reads, all independent;
+        // positions past the window hold +inf), then a binary search of the
+        // bucket in LDS.
+        uint32_t lo[2] = {0, 0}, hi[2];
 #pragma unroll
-        for (int it = 0; it < 8; it++) {
+        for (int sp = 0; sp < 8; sp++) {
+            const Key<KL> at = key_lds<KL>(bkeys, 16 * sp + 15);
+#pragma unroll
+            for (int q = 0; q < 2; q++) lo[q] += key_lt(at, ka[q]) ? 16u : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) hi[q] = lo[q] + 15 < nbv ? lo[q] + 15 : nbv;
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 const uint32_t m = (lo[q] + hi[q]) >> 1;
