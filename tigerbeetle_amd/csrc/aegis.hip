@@ -266,14 +266,16 @@ struct BodyMsg {
     const uint32_t *prog; // LDS
     uint32_t *err;        // JobResultDev.invariant: set if the producer never delivers
     mutable uint32_t seen = 0; // progress already acquired: no LDS read, no fence below it
-    __device__ __forceinline__ BodyMsg(const uint8_t *b, uint32_t l, const uint32_t *p, uint32_t *e)
-        : base(b), len(l), max_off(l >= 4 ? l - 4 : 0), prog(p), err(e) {}
+    uint32_t *cons = nullptr;  // LDS: this chain's position, for the producer's throttle
+    __device__ __forceinline__ BodyMsg(const uint8_t *b, uint32_t l, const uint32_t *p, uint32_t *e, uint32_t *c)
+        : base(b), len(l), max_off(l >= 4 ? l - 4 : 0), prog(p), err(e), cons(c) {}
     __device__ __forceinline__ Addr addr(uint32_t off) const { return base + (off < max_off ? off : max_off); }
     __device__ __forceinline__ uint32_t word(Addr a) const { return gld<uint32_t>(a); }
     __device__ __forceinline__ uint32_t exact(uint32_t off) const { return off < len ? gld<uint32_t>(base + off) : 0u; }
     __device__ __forceinline__ void sink(uint32_t, uint32_t) const {}
     __device__ __forceinline__ void ready(uint32_t upto) const {
         const uint32_t need = upto < len ? upto : len;
+        if ((threadIdx.x & 31) == 0) __hip_atomic_store(cons, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         // Whole wave: both 32-lane groups' blocks covered by what was acquired.
         if (!__any(need > seen)) return;
         uint32_t have = 0;
@@ -673,6 +675,31 @@ __device__ __forceinline__ bool sparse_job(const JobDesc &j, const JobResultDev 
 }
 
 
+// Producer throttle: a speculated producer stays at most `lead` body bytes ahead of
+// what its block's chain has asked for (BodyMsg::ready stores the chain's
+// position in LDS). Unthrottled, a producer runs up to a whole block ahead of
+// its chain at the start of the kernel, every producer of the chip at once;
+// throttled, the input reads spread over the chain's time (config 2: 2.46 ->
+// 2.36 ms). The chains' re-reads of the bodies still miss L2: 256 blocks in
+// flight per XCD, each with its lead and the inputs read meanwhile, exceed
+// the XCD's 4 MiB. The lead is at least one unpublished
+// step, so a chain waiting for data never waits on its throttled producer;
+// bounded anyway. The merge-path producer (produce_body) is not throttled:
+// there it cost 2-4 % on configs 4 and 5. TBC_LEAD_BYTES overrides the lead
+// for ablation builds.
+#ifndef TBC_LEAD_BYTES
+#define TBC_LEAD_BYTES 12288
+#endif
+constexpr uint32_t kLeadBytes = TBC_LEAD_BYTES;
+__device__ __forceinline__ void throttle(const uint32_t *cons, uint32_t produced, uint32_t lead) {
+    if (!cons) return;
+    for (uint32_t spins = 0; spins < (1u << 21); spins++) {
+        const uint32_t c = __hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (produced <= c + lead) return;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint32_t cnt, const uint64_t *status,
                                              const uint64_t *masks, const uint32_t *block_tile,
                                              const SplitDesc *splits, uint8_t *body, uint32_t *prog,
@@ -873,7 +900,7 @@ __device__ __forceinline__ Key<KeyLimbs<KIND>::value> key_of_words(const uint64_
 template <int KIND, int VW>
 __device__ __forceinline__ void produce_unique(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
                                                uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
-                                               uint64_t *stage) {
+                                               uint64_t *stage, const uint32_t *cons) {
     constexpr int KL = KeyLimbs<KIND>::value;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t vs = j.value_size, ts = j.timestamp_offset, na = j.a.n, nb = j.b.n;
@@ -1010,6 +1037,7 @@ __device__ __forceinline__ void produce_unique(const JobDesc &j, uint32_t k, uin
             ia += n_a;
             ib += n_b;
             out += E;
+            throttle(cons, out * vs, 3 * 64 * vs > kLeadBytes ? 3 * 64 * vs : kLeadBytes);
             if (out < cnt) load_window();
             copy_staged(st_src, st_dst, E, cpv_log);
         }
@@ -1096,7 +1124,7 @@ template <int KL> __device__ __forceinline__ Key<KL> key_lds(const uint64_t *key
 template <int KIND, int VW>
 __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
                                                     uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
-                                                    uint64_t *stage, uint64_t *probe) {
+                                                    uint64_t *stage, uint64_t *probe, const uint32_t *cons) {
     // probe (timing probe only): wall-clock ticks spent waiting for windows,
     // searching, in the histogram, in the rest, and the step count.
     uint64_t t_wait = 0, t_search = 0, t_hist = 0, t_rest = 0, steps = 0, t_mark = wall_clock64();
@@ -1300,6 +1328,7 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
         ia += n_a;
         ib += n_b;
         out += E;
+        throttle(cons, out * vs, kLeadBytes);
         if (out < cnt) load_window();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1322,13 +1351,14 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
 template <int KIND>
 __device__ __forceinline__ void produce_unique_vs(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
                                                   uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
-                                                  uint64_t *stage, uint32_t phase) {
+                                                  uint64_t *stage, uint32_t phase, const uint32_t *cons) {
     // Timing probe (TBC_PROBE_PRODUCERS_ONLY, no chains): the block's header
     // bytes receive the producer's time split.
     uint64_t *probe = phase == kPhaseProducersOnly ? (uint64_t *)(body - kHeaderSize) : nullptr;
-    if (j.value_size == 32) produce_unique_wide<KIND, 2>(j, k, cnt, sp, body, prog, err, spec, stage, probe);
-    else if (j.value_size == 16) produce_unique_wide<KIND, 1>(j, k, cnt, sp, body, prog, err, spec, stage, probe);
-    else produce_unique<KIND, 0>(j, k, cnt, sp, body, prog, err, spec, stage);
+    if (phase == kPhaseProducersOnly) cons = nullptr; // no chains to wait for
+    if (j.value_size == 32) produce_unique_wide<KIND, 2>(j, k, cnt, sp, body, prog, err, spec, stage, probe, cons);
+    else if (j.value_size == 16) produce_unique_wide<KIND, 1>(j, k, cnt, sp, body, prog, err, spec, stage, probe, cons);
+    else produce_unique<KIND, 0>(j, k, cnt, sp, body, prog, err, spec, stage, cons);
 }
 
 // Data blocks: data_block_finish (table.zig:306-384) for every output data
@@ -1365,6 +1395,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
+    __shared__ uint32_t sCons[2 * kMaxChainWaves]; // the chains' positions (body bytes needed so far)
     // Producer LDS: copy staging (merge-path producers), or the speculated
     // producers' B window keys + rank histogram; everything the tables,
     // headers and progress words leave of the CU's 160 KiB.
@@ -1383,7 +1414,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         if (!__syncthreads_or(mine)) return;
     }
     load_tables(sT);
-    if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = sCons[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t wave_in_block = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
@@ -1408,16 +1439,20 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
             const uint32_t cnt = block_count(j, k);
             switch (j.key_kind) {
             case kKeyTimestamp:
-                produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                                                   &sCons[p]);
                 break;
             case kKeyIdU128:
-                produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                                                   &sCons[p]);
                 break;
             case kKeyCompositeU64:
-                produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                                                   &sCons[p]);
                 break;
             default:
-                produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase);
+                produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                                                   &sCons[p]);
                 break;
             }
             return;
@@ -1456,7 +1491,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     uint32_t body_tag;
     if constexpr (Fused) {
         BodyMsg body(blk + kHeaderSize, cnt * j.value_size, &sProg[2 * wave_in_block + src_half],
-                     const_cast<uint32_t *>(&res[j.job_index].invariant));
+                     const_cast<uint32_t *>(&res[j.job_index].invariant), &sCons[2 * wave_in_block + src_half]);
         body_tag = aegis_mac32(sT, body);
     } else {
         (void)src_half;
