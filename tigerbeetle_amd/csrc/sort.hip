@@ -244,6 +244,9 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
         uint64_t k[3], kn[3], pk[3], pn[3];
         row_keys(S, li, in, k, kn);
         pack_key(s_map, nb, k, pk);
+        // the next item's packed key: the next lane's (lane 63 packs its own)
+        for (uint32_t l = 0; l < 3; l++) pn[l] = __shfl_down(pk[l], 1, 64);
+        if ((tid & 63) == 63) pack_key(s_map, nb, kn, pn);
         const uint32_t i = S.item_base + li;
         if (in) {
             for (uint32_t l = 0; l < pl; l++) keys[(size_t)l * N + i] = pk[l];
@@ -251,7 +254,6 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
         }
         for (uint32_t j = 0; j < nb; j++) hist_add(s_hist[j], (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u, in);
         if (in && li + 1 < S.n) {
-            pack_key(s_map, nb, kn, pn);
             int cmp = 0; // order of (item, next) on packed bytes [0, j]
             for (uint32_t j = 0; j < nb; j++) {
                 const uint32_t x = (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u;
@@ -352,7 +354,8 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
 // A table's last pass moves the values themselves (values[dst] =
 // copy[index]) instead of keys and indices: the gather is fused into it.
 __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
-                                                            const uint32_t *tile_seg, uint32_t p, uint32_t ntiles,
+                                                            const uint32_t *tile_seg, const uint32_t *tile_order,
+                                                            uint32_t p, uint32_t ntiles,
                                                             uint32_t N, uint64_t *keys0, uint64_t *keys1,
                                                             uint32_t *idx0, uint32_t *idx1, const uint32_t *bins,
                                                             uint64_t *status, uint32_t epoch,
@@ -375,8 +378,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
         if (tid == 0) s_tile = atomicAdd(&tile_counter[p], 1u);
         for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
         __syncthreads();
-        const uint32_t t = s_tile;
-        if (t >= ntiles) return;
+        if (s_tile >= ntiles) return;
+        const uint32_t t = tile_order[s_tile];
         const uint32_t sg = tile_seg[t];
         const SortSeg &S = segs[sg];
         const uint32_t nact = S.nact;
@@ -458,7 +461,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
             // Tiles in flight together all publish their aggregates at about
             // the same time, so a walk can be long: read a window of kLook
             // predecessors per round trip, nearest first.
-            constexpr uint32_t kLook = 8;
+            constexpr uint32_t kLook = 16;
             uint32_t pred = t - 1;
             for (uint32_t spins = 0;;) {
                 uint64_t v[kLook];
@@ -722,7 +725,7 @@ static uint64_t align256(uint64_t x) { return (x + 255) / 256 * 256; }
 // look-back words live in their own buffer (sort_status_words): epochs are
 // only unique there.
 struct SortScratch {
-    uint64_t segs, tile_seg, hist, counters, batch, bins, keys, idx, copies, total;
+    uint64_t segs, tile_seg, tile_order, hist, counters, batch, bins, keys, idx, copies, total;
 };
 
 static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
@@ -740,6 +743,8 @@ static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
     s.segs = o;
     o += align256(sizeof(SortSeg) * count);
     s.tile_seg = o;
+    o += align256(4 * tiles);
+    s.tile_order = o;
     o += align256(4 * tiles);
     s.hist = o; // zeroed per batch: hist, counters, batch
     o += align256(4ull * nseg * kMaxPasses * kRadix);
@@ -812,8 +817,20 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         hsegs[nseg++] = g;
     }
     if (!nseg) return 0;
+    // Pass tile order: round-robin over the tables (local tile 0 of every
+    // table, then local tile 1, ...). A table's tiles are still taken in
+    // order (the look-back's progress guarantee), but fewer of one table's
+    // tiles are in flight together, so a tile's look-back walk to the nearest
+    // inclusive prefix is shorter.
+    {
+        uint32_t *horder = (uint32_t *)(hbase + L.tile_order), o = 0;
+        for (uint32_t lt = 0; o < ntiles; lt++)
+            for (uint32_t g = 0; g < nseg; g++)
+                if (lt < hsegs[g].tiles) horder[o++] = hsegs[g].tile_base + lt;
+    }
     SortSeg *d_segs = (SortSeg *)(base + L.segs);
     uint32_t *d_tile = (uint32_t *)(base + L.tile_seg);
+    const uint32_t *d_order = (const uint32_t *)(base + L.tile_order);
     const uint64_t klw = align256(8ull * N * max_kl);
     uint64_t *keys0 = (uint64_t *)(base + L.keys), *keys1 = (uint64_t *)(base + L.keys + klw);
     uint32_t *idx0 = (uint32_t *)(base + L.idx), *idx1 = (uint32_t *)(base + L.idx + align256(4ull * N));
@@ -827,12 +844,23 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     hipLaunchKernelGGL(k_sort_layout, dim3((nseg + 63) / 64), dim3(64), 0, s, d_segs, nseg);
     hipLaunchKernelGGL(k_sort_pack, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, N, keys0, idx0, hist);
     hipLaunchKernelGGL(k_sort_plan, dim3(nseg), dim3(kRadix), 0, s, d_segs, d_batch, hist, bins);
-    // Persistent: five workgroups per CU fit the LDS.
-    const uint32_t pgrid = ntiles < 1280 ? ntiles : 1280;
+    // Persistent: as many workgroups as are resident at once (VGPRs allow
+    // three per CU): more would only start after the tiles run out, and an
+    // idle pass (no table has that many bytes) costs its launch alone.
+    static uint32_t resident = 0;
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_pass, kSortThreads, 0) != hipSuccess ||
+            hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1)
+            return -1;
+        resident = (uint32_t)(per_cu * cus);
+    }
+    const uint32_t pgrid = ntiles < resident ? ntiles : resident;
     for (uint32_t p = 0; p < 8 * max_kl; p++) {
         if (*epoch == 0) *epoch = 1; // 0 is the zeroed buffer's
-        hipLaunchKernelGGL(k_sort_pass, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, p, ntiles, N,
-                           keys0, keys1, idx0, idx1, bins, status, (*epoch)++, counters);
+        hipLaunchKernelGGL(k_sort_pass, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, d_order, p,
+                           ntiles, N, keys0, keys1, idx0, idx1, bins, status, (*epoch)++, counters);
     }
     hipLaunchKernelGGL(k_sort_fixup, dim3(ntiles), dim3(256), 0, s, d_segs, (const uint32_t *)d_tile,
                        (const uint32_t *)idx0, (const uint32_t *)idx1);
