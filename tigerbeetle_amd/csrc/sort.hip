@@ -244,9 +244,6 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
         uint64_t k[3], kn[3], pk[3], pn[3];
         row_keys(S, li, in, k, kn);
         pack_key(s_map, nb, k, pk);
-        // the next item's packed key: the next lane's (lane 63 packs its own)
-        for (uint32_t l = 0; l < 3; l++) pn[l] = __shfl_down(pk[l], 1, 64);
-        if ((tid & 63) == 63) pack_key(s_map, nb, kn, pn);
         const uint32_t i = S.item_base + li;
         if (in) {
             for (uint32_t l = 0; l < pl; l++) keys[(size_t)l * N + i] = pk[l];
@@ -254,6 +251,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
         }
         for (uint32_t j = 0; j < nb; j++) hist_add(s_hist[j], (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u, in);
         if (in && li + 1 < S.n) {
+            pack_key(s_map, nb, kn, pn);
             int cmp = 0; // order of (item, next) on packed bytes [0, j]
             for (uint32_t j = 0; j < nb; j++) {
                 const uint32_t x = (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u;
@@ -461,7 +459,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
             // Tiles in flight together all publish their aggregates at about
             // the same time, so a walk can be long: read a window of kLook
             // predecessors per round trip, nearest first.
-            constexpr uint32_t kLook = 16;
+            constexpr uint32_t kLook = 8;
             uint32_t pred = t - 1;
             for (uint32_t spins = 0;;) {
                 uint64_t v[kLook];
