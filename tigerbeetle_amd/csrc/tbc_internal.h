@@ -24,11 +24,10 @@ constexpr uint32_t kSectorSize = 4096; // constants.sector_size (constants.zig:4
 constexpr uint32_t kTableInfoSize = 128;
 constexpr uint64_t kTombstoneBit = 1ull << 63;
 
-// Merge tile: merged-sequence positions handled by one workgroup.
-#ifndef TBC_MERGE_TILE
-#define TBC_MERGE_TILE 2048
-#endif
-constexpr uint32_t kMergeTile = TBC_MERGE_TILE;
+// Merge tile: merged-sequence positions handled by one workgroup. Fixed:
+// other sizes are not supported builds (a 1024 build faulted in
+// test_gpu_parity's minimum-size blocks).
+constexpr uint32_t kMergeTile = 2048;
 constexpr uint32_t kMergeThreads = kMergeTile / 4;
 
 enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };
