@@ -25,9 +25,10 @@ constexpr uint32_t kTableInfoSize = 128;
 constexpr uint64_t kTombstoneBit = 1ull << 63;
 
 // Merge tile: merged-sequence positions handled by one workgroup. Fixed:
-// other sizes are not supported builds (a 1024 build faulted in
-// test_gpu_parity's minimum-size blocks).
+// the block producers load a tile's 2 x 32 mask words one per lane of a wave
+// (aegis.hip produce_body), so other sizes are not supported builds.
 constexpr uint32_t kMergeTile = 2048;
+static_assert(2 * (kMergeTile / 64) == 64, "one mask word per lane");
 constexpr uint32_t kMergeThreads = kMergeTile / 4;
 
 enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };
