@@ -681,8 +681,8 @@ __device__ __forceinline__ bool sparse_job(const JobDesc &j, const JobResultDev 
 // its chain at the start of the kernel, every producer of the chip at once;
 // throttled, the input reads spread over the chain's time (config 2: 2.46 ->
 // 2.36 ms). The chains' re-reads of the bodies still miss L2 at any lead
-// from 4 to 64 KiB (fresh lines written by plain stores are
-// not there for a later read). The lead is at least one unpublished
+// from 4 to 64 KiB (256 blocks per XCD churn ~3 MiB of L2
+// per chain step). The lead is at least one unpublished
 // step, so a chain waiting for data never waits on its throttled producer;
 // bounded anyway. The merge-path producer (produce_body) is not throttled:
 // there it cost 2-4 % on configs 4 and 5. TBC_LEAD_BYTES overrides the lead
