@@ -31,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from tigerbeetle_amd import Engine, Grid, Job, abi, benchmark_load, configs, forest  # noqa: E402
+from tigerbeetle_amd import Engine, Grid, Job, abi, benchmark_load, configs, forest, manifest  # noqa: E402
 from tigerbeetle_amd.shard import plan_shards, reduce_step  # noqa: E402
 
 METRIC = "compacted input MB/s per GPU and per node (1/2/4/8) + % HBM roofline"
@@ -178,10 +178,14 @@ class ReplayWorkload:
                 for dst, src, n in landings:
                     eng.copy_device_async(dst, src, n)
                 eng.sort_values_batch(jobs)
+            elif kind == "manifest":  # ManifestLog.close_block on the device (manifest.py)
+                images, addresses, prev = rest
+                manifest.close_on_grid(self.grid, images, addresses, prev, None if prev else 0)
             else:
                 live.append(eng.submit(rest[0]))
         for b in live:
             b.wait()
+            b.check_results()  # every replayed compaction ends TBC_OK (block checks, invariants)
             if ktimes is not None:
                 for k, v in b.kernel_times().items():
                     ktimes[k] = ktimes.get(k, 0.0) + v

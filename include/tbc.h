@@ -188,6 +188,12 @@ uint32_t tbc_abi_version(void);
 tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine);
 void tbc_engine_deinit(tbc_engine *engine);
 tbc_status tbc_tree_layout_get(const tbc_engine *engine, const tbc_tree *tree, tbc_tree_layout *out_layout);
+/* Diagnostics: bytes of the static device and pinned host arenas held by
+ * submitted batches and k-way merges not yet released, and how many of them.
+ * Released handles give their region back (out of order too, once the
+ * regions above it are released), so a steady-state caller sees these bounded. */
+tbc_status tbc_engine_arena_usage(const tbc_engine *engine, uint64_t *out_device_bytes, uint64_t *out_host_bytes,
+                                  uint32_t *out_regions);
 
 /* ---- grid ------------------------------------------------------------------- */
 tbc_status tbc_grid_init(tbc_engine *engine, uint64_t block_count, tbc_grid **out_grid);
@@ -206,6 +212,25 @@ tbc_status tbc_grid_put_blocks(tbc_grid *grid, const uint64_t *addresses, const 
  * buffers are valid after tbc_synchronize (or a later batch's completion). */
 tbc_status tbc_grid_get_blocks(tbc_grid *grid, const uint64_t *addresses, void *const *host_blocks,
                                uint32_t count);
+
+/* ---- ManifestLog.close_block (src/lsm/manifest_log.zig:876-952) ----------------
+ * Close `count` manifest blocks of the log, oldest first, into the grid at
+ * `addresses` (ManifestLog.acquire_block's grid.acquire, one each). The host
+ * packs each block image as the reference's append/close_block do (header:
+ * cluster, size = 256 + 128 * entry_count, command block, metadata
+ * {previous checksum left 0, previous address, entry_count}, address,
+ * block_type manifest; body: the 128-byte TableInfo entries; zero padding to
+ * the sector); the engine stages the images into their grid slots and, on
+ * the device, sets every block's checksum_body, its metadata's previous
+ * checksum (block i links block i-1; block 0 links `previous_checksum`, or,
+ * when that is NULL, the header checksum of the block at `previous_address`
+ * in the grid — an earlier close — or 0 when previous_address is 0) and its
+ * header checksum. Enqueued on the engine stream; no host wait beyond the
+ * pinned staging copies. The blocks are trusted grid blocks afterwards.
+ * TBC_ERR_INVALID_ARGUMENT if a packed header contradicts its address, the
+ * chain or ManifestNode.metadata's asserts (schema.zig:534-554). */
+tbc_status tbc_manifest_close_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_images,
+                                     uint32_t count, uint64_t previous_address, const uint64_t *previous_checksum);
 
 /* ---- TableMemory on the device (src/lsm/table_memory.zig:79-124) ------------
  * Groove.insert/update -> Tree.put (groove.zig:911-1006, tree.zig:268-270)
@@ -272,8 +297,9 @@ tbc_status tbc_sort_values_async(tbc_engine *engine, const tbc_tree *tree, void 
  * segmented launch sequence (tree.zig:979-999 calls TableMemory.sort once per
  * tree; the batch is the same work without a launch train per tree). Same
  * semantics per table as tbc_sort_values; tables that are already sorted are
- * left untouched. Enqueued on the engine stream; blocks once on a small
- * device->host read of the key probe (the radix digit plan). */
+ * left untouched. Enqueued on the engine stream with no host wait: the digit
+ * plan (which bytes vary, which passes run) is computed and read on the
+ * device (sort.hip k_sort_plan). */
 typedef struct tbc_sort_job {
     tbc_tree tree;
     void *values;   /* device pointer, 16-byte aligned */

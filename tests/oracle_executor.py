@@ -23,6 +23,59 @@ class _Result:
         self.block_count = len(o.blocks)
 
 
+class OracleManifestStore:
+    """Manifest blocks closed by the oracle's restatement of close_block
+    (oracle.manifest_blocks) into the executor's host grid."""
+
+    def __init__(self, oracle, grid: dict, cluster: int, block_size: int):
+        self.oracle, self.grid, self.cluster, self.bs = oracle, grid, cluster, block_size
+        self.checksums: dict = {}
+        self.closed: list = []
+
+    def close(self, infos, address, previous_address):
+        prev = self.checksums[previous_address] if previous_address else 0
+        imgs, sums = self.oracle.manifest_blocks(infos, [address], self.cluster, self.bs, previous_checksum=prev,
+                                                 previous_address=previous_address)
+        assert len(imgs) == 1
+        self.grid[int(address)] = imgs[0]
+        self.checksums[int(address)] = sums[0]
+        self.closed.append(int(address))
+
+    def read(self, address):
+        return self.grid[int(address)]
+
+
+class LockstepManifestStore:
+    """Every manifest block closed on the GPU grid and by the oracle; reads
+    return the GPU's block after comparing it with the oracle's."""
+
+    def __init__(self, gpu_store, ref_store):
+        self.gpu, self.ref = gpu_store, ref_store
+        self.compared = 0
+
+    def close(self, infos, address, previous_address):
+        self.gpu.close(infos, address, previous_address)
+        self.ref.close(infos, address, previous_address)
+
+    def read(self, address):
+        got = self.gpu.read(address)
+        want = self.ref.read(address)
+        assert np.array_equal(got, want), f"manifest block {address}"
+        self.compared += 1
+        return got
+
+    def check_all(self) -> int:
+        """Every block closed so far, GPU grid vs oracle, byte for byte."""
+        assert self.gpu.closed == self.ref.closed
+        if not self.gpu.closed:
+            return 0
+        got = self.gpu.grid.get_blocks(self.gpu.closed)
+        for a, g in zip(self.gpu.closed, got):
+            w = self.ref.grid[a]
+            assert np.array_equal(g[:len(w)], w), f"manifest block {a}"
+        return len(self.gpu.closed)
+
+
 class OracleExecutor:
     """The oracle on a host grid (address -> block image), memtables as
     numpy arrays. `busy` accumulates the time spent inside the oracle's sort
@@ -36,6 +89,9 @@ class OracleExecutor:
         self.busy = 0.0
         self.input_bytes = 0
         self.last: list = []
+
+    def manifest_store(self, cluster):
+        return OracleManifestStore(self.oracle, self.grid, cluster, self.bs)
 
     def _tree(self, spec):
         return self.oracle.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
@@ -93,7 +149,9 @@ class OracleExecutor:
         self.busy += time.perf_counter() - t0
         assert o.status == 0, (name, o.status)
         for a, blk in zip(c.addresses, o.blocks):
-            self.grid[int(a)] = blk
+            # the on-disk image only (grid.zig:686): a whole replay's blocks stay resident
+            size = int(blk[96:100].view(np.uint32)[0])
+            self.grid[int(a)] = blk[:size].copy()
         return o
 
     def submit(self, jobs, cluster):
@@ -114,6 +172,10 @@ class LockstepExecutor:
         self.gpu, self.ref = gpu, oracle_exec
         self.jobs_checked = 0
         self.blocks_checked = 0
+
+    def manifest_store(self, cluster):
+        self.manifest = LockstepManifestStore(self.gpu.manifest_store(cluster), self.ref.manifest_store(cluster))
+        return self.manifest
 
     def put(self, name, values):
         self.gpu.put(name, values)

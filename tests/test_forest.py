@@ -111,3 +111,47 @@ def test_small_benchmark_replay_on_the_oracle(oracle_lib):
             for s in ex.table_segments(info, acc.spec):
                 keys.extend(workloads.keys_of(s, acc.spec)[0].tolist())
     assert len(keys) > 0
+
+
+def test_replay_manifest_log_recovers_the_forest(oracle_lib):
+    """The manifest events of a replay (apply_to_manifest + remove_invisible_tables,
+    forest.py Tree.apply) through the ManifestLog: after its checkpoint,
+    ManifestLog.open's reverse scan and the chronological replay of every
+    block both recover exactly the tables in the forest's levels, at their
+    levels and snapshots (Forest.verify_tables_recovered, forest.zig:560-650),
+    and the log's extents cover every table (verify_table_extents)."""
+    from tigerbeetle_amd import manifest
+    ex = OracleExecutor(oracle_lib)
+    f = forest.Forest(ex, block_count=1 << 16, cluster=7)
+    load = benchmark_load.BenchmarkLoad(account_count=300, transfer_count=64 * 32 * 10, batch=64)
+    f.run(load.ops())
+    if f.pending is not None:   # finish the running half-bar
+        op = f.pending[1][0][1].op_min + forest.HALF - 1
+        f.compact(op)
+    log = f.manifest_log
+    assert log.stats["appends"] > 0
+    f.checkpoint_manifest()
+    blocks = [ex.grid[a] for a in log.log_addresses]
+    assert blocks
+    opened = manifest.open_log(blocks)
+    replayed = manifest.replay_log(blocks)
+    want = {}
+    for name, t in f.trees.items():
+        for level, lv in enumerate(t.levels):
+            for info in lv.tables:
+                want[info.address] = info.encode(t.spec.tree_id, level, 1, t.spec.key_size)
+    assert set(opened) == set(want) == set(log.table_extents)
+    for a, e in want.items():   # same table, level, snapshots (the label's event may be insert or update)
+        got = opened[a].copy()
+        got[126] &= 0x3f
+        e = e.copy()
+        e[126] &= 0x3f
+        assert np.array_equal(got, e), a
+    assert {int(e[96:104].view(np.uint64)[0]) for e in replayed.values()} == set(want)
+    # events by kind: inserts of outputs, updates of inputs and moves, removes of inputs
+    kinds = {}
+    for blk in blocks:
+        n = int(blk[168:172].view(np.uint32)[0])
+        for e in blk[256:256 + 128 * n].reshape(n, 128):
+            kinds[int(e[126]) >> 6] = kinds.get(int(e[126]) >> 6, 0) + 1
+    assert kinds.get(1, 0) > 0 and kinds.get(2, 0) > 0 and kinds.get(3, 0) > 0

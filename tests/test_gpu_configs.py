@@ -1,6 +1,7 @@
 """GPU parity at BASELINE.json's full sizes: whole production-sized jobs of
 configs 2, 3, 4 (a whole forest unit: 21 jobs of 4 key kinds in one batch)
-and 5 (tigerbeetle_amd/configs.py), staged exactly as bench.py stages them, compared block-for-block with the oracle; plus size-independent
+and 5 (tigerbeetle_amd/configs.py), staged exactly as bench.py stages them (every job of the benched batch),
+compared block-for-block with the oracle; plus size-independent
 properties of the output (every block's checksums verify, keys strictly
 increase across the whole output, value counts add up).
 """
@@ -25,21 +26,37 @@ def _oracle_job(oracle_lib, js, bs, addrs):
                               level_b=js.level_b, cluster=0xA5A5, snapshot_min=48, addresses=addrs)
 
 
-@pytest.mark.parametrize("config,job_ids", [(2, [0, 1]), (3, [0, 1, 6]), (4, list(range(21))), (5, [0])])
-def test_full_size_jobs_bit_exact(oracle_lib, config, job_ids):
+# Exactly the batches bench.py times (configs.DEFAULT_JOBS per GPU): config 2's
+# 28 speculated jobs (2,016 chains at once), config 3's 28 bar-end jobs with
+# their device sorts, a whole forest unit of config 4, and config 5's 27 jobs
+# (13,824 output blocks: the throughput regime — 4 pipelined job groups,
+# k_assemble, chain-only k_data_blocks over 1 MiB bodies).
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config", [2, 3, 4, 5])
+def test_full_size_jobs_bit_exact(oracle_lib, config):
     import bench
-    from tigerbeetle_amd import Engine
+    from tigerbeetle_amd import Engine, abi
     bs = 1 << 20
-    with Engine(device=0, block_size=bs, arena_bytes=2 << 30) as eng:
+    job_ids = list(range(configs.DEFAULT_JOBS[config]))
+    with Engine(device=0, block_size=bs, arena_bytes=2 << 30, profile=True) as eng:
         wl = bench.Workload(eng, config, job_ids, bs)
         wl.step(eng).release()          # twice: the memtables are re-landed and re-sorted
         b = wl.step(eng)
+        total_blocks = 0
+        kernels = b.kernel_times()
+        if config == 2:  # the latency regime with every job speculated (and held)
+            assert "partition_blocks" in kernels and "assemble" not in kernels, kernels
+            assert all(b.speculation(i) == abi.SPECULATION_HELD for i in range(len(wl.jobs)))
+        if config == 5:  # the throughput regime: pipelined groups, assembled bodies, chain-only kernel
+            assert "assemble" in kernels and "tail_wait" in kernels, kernels
         for i, (job, js) in enumerate(zip(wl.jobs, wl.specs)):
             r, infos = b.result(i)
             o = _oracle_job(oracle_lib, js, bs, job.addresses)
+            print(f"config {config} job {job_ids[i]}: {r.value_count} values, {r.block_count} blocks", flush=True)
             assert r.status == 0 and o.status == 0
             assert (r.value_count, r.block_count, r.table_count) == \
                 (o.value_count, len(o.blocks), len(o.table_infos)), (config, job_ids[i])
+            total_blocks += r.block_count
             blocks = job.output.download(r.block_count * bs).reshape(-1, bs)
             for k, (g, w) in enumerate(zip(blocks, o.blocks)):
                 assert np.array_equal(disk_image(g), disk_image(w)), (config, job_ids[i], k)
@@ -61,4 +78,7 @@ def test_full_size_jobs_bit_exact(oracle_lib, config, job_ids):
             lens = [int(blk[96:100].view(np.uint32)[0]) - 256 for blk in blocks]
             sums = eng.checksum_device(ptrs, lens)
             assert np.array_equal(sums, blocks[:, 32:48])
+            del blocks, o, vals, keys
+        if config == 5:
+            assert total_blocks > 2 * 4096, total_blocks
         b.release()

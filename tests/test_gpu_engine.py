@@ -1,0 +1,186 @@
+"""Engine-level behaviour that the per-kernel parity tests do not reach.
+
+- The static arenas (engine.hip Arena): batches and k-way merges open a
+  region at submit and close it at release. With one batch held live (the
+  adapter always has something in flight), many submit/release cycles of
+  k-way merges and batches must not grow the arenas' tops, and regions
+  released out of order are reclaimed once the ones above them are.
+- Pipelined grid batches (engine.hip submit_impl, grid mode): several
+  half-bars' batches in flight at once, submitted back to back without
+  waiting, with a storage stage (tbc_grid_put_blocks) between two submits,
+  later batches reading storage tables that earlier ones also read (the
+  first reader validates them in full, later readers must see them
+  trusted), and one corrupt storage table. Every job's blocks and TableInfos
+  are compared with the oracle; the corrupt table's job alone fails.
+- Failed grid jobs leave their outputs unverified (k_grid_mark runs after
+  the input checks, and only for clean jobs): a later reader of such an
+  output revalidates it in full, while a clean job's outputs are trusted
+  like the reference's grid cache hits (grid.zig:802-841).
+"""
+import numpy as np
+import pytest
+
+from test_gpu_grid import BS, CLUSTER, check_job, sorted_unique, storage_table
+from tigerbeetle_amd import Grid, Job, abi, trees, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _small_job(engine, spec, rng, n=20_000):
+    vals = sorted_unique(spec, n, rng)
+    buf = engine.upload(vals)
+    out = engine.alloc(4 * BS)
+    return buf, out, Job(spec, [(buf.ptr, n)], [], True, False, 1, CLUSTER, 48,
+                         np.arange(1, 5, dtype=np.uint64), out)
+
+
+def test_arena_bounded_with_a_batch_in_flight(engine):
+    spec = trees.BY_NAME["transfers.id"]
+    rng = np.random.default_rng(0xA7E)
+    base = engine.arena_usage()
+    keep0 = _small_job(engine, spec, rng)
+    held = engine.submit([keep0[2]])          # stays live for the whole loop
+    after_held = engine.arena_usage()
+    assert after_held[2] == base[2] + 2       # one device + one pinned region
+    streams = [sorted_unique(spec, 5_000, rng) for _ in range(4)]
+    bufs = [engine.upload(s) for s in streams]
+    segs = [(b.ptr, len(s)) for b, s in zip(bufs, streams)]
+    kout = engine.alloc(20_000 * 32)
+    keep1 = _small_job(engine, spec, rng)
+    peak = (0, 0)
+    for _ in range(40):
+        k = engine.kway_merge_submit(spec, segs, kout)
+        b = engine.submit([keep1[2]])
+        peak = max(peak, engine.arena_usage()[:2])
+        b.wait()
+        k.wait()
+        assert k.count() == 20_000
+        k.release()                            # released below the batch: reclaimed with it
+        b.release()
+        assert engine.arena_usage() == after_held
+    assert peak[0] < after_held[0] + (1 << 20) and peak[1] < after_held[1] + (1 << 20)
+    # Out of order: the lower region closes first, the top stays until the upper one closes.
+    b1, b2 = engine.submit([keep1[2]]), engine.submit([keep1[2]])
+    b1.wait()
+    b2.wait()
+    top2 = engine.arena_usage()
+    b1.release()
+    assert engine.arena_usage()[:2] == top2[:2]
+    b2.release()
+    assert engine.arena_usage() == after_held
+    held.wait()
+    held.release()
+    assert engine.arena_usage() == base
+
+
+def test_pipelined_grid_batches_in_flight(engine, oracle_lib):
+    rng = np.random.default_rng(0x919E)
+    grid = Grid(engine, 900)
+    sid = trees.BY_NAME["transfers.id"]
+    sacc = trees.BY_NAME["accounts.timestamp"]
+    try:
+        # Storage: S1, S2 (transfers.id, level 1), S3 (accounts, level 2); S4 corrupt.
+        uni = sorted_unique(sid, 240_000, rng)
+        part = rng.integers(0, 4, size=len(uni))
+        s1v, s2v, m1v, m2v = (uni[part == p] for p in range(4))
+        blk1, ti1 = storage_table(oracle_lib, sid, s1v, np.arange(1, 12, dtype=np.uint64))
+        blk2, ti2 = storage_table(oracle_lib, sid, s2v, np.arange(20, 31, dtype=np.uint64))
+        s3v = sorted_unique(sacc, 40_000, rng)
+        blk3, ti3 = storage_table(oracle_lib, sacc, s3v, np.arange(40, 60, dtype=np.uint64), level=2)
+        s4v = sorted_unique(sid, 30_000, rng)
+        blk4, ti4 = storage_table(oracle_lib, sid, s4v, np.arange(60, 70, dtype=np.uint64))
+        bad4 = np.stack(blk4).copy()
+        bad4[0, 256 + 77] ^= 1
+        grid.put_blocks(np.arange(1, 1 + len(blk1), dtype=np.uint64), np.stack(blk1))
+        grid.put_blocks(np.arange(20, 20 + len(blk2), dtype=np.uint64), np.stack(blk2))
+        grid.put_blocks(np.arange(60, 60 + len(bad4), dtype=np.uint64), bad4)
+        m1 = engine.upload(m1v)
+        m2 = engine.upload(m2v)
+        acc_keys = [np.sort(workloads.keys_of(s3v, sacc)[0][rng.choice(len(s3v), 9_000, replace=False)])]
+        acc_a = workloads.values_from_keys(sacc, acc_keys, rng.random(9_000) < 0.05, rng)
+        acc_buf = engine.upload(acc_a)
+
+        def grid_job(spec, segs_a, tables_a, tables_b, level_b, drop, base, count):
+            return Job(spec, segs_a, [], bool(segs_a), drop, level_b, CLUSTER, 64,
+                       np.arange(base, base + count, dtype=np.uint64), None, flags=abi.COMPACTION_GRID, grid=grid,
+                       tables_a=tables_a, tables_b=tables_b)
+
+        # Batch 1: immutable M1 into S1 (validates S1), and immutable M2 into S2.
+        j1 = [grid_job(sid, [(m1.ptr, len(m1v))], [], [ti1.ref()], 1, False, 100, 3 * 9),
+              grid_job(sid, [(m2.ptr, len(m2v))], [], [ti2.ref()], 1, False, 140, 3 * 9)]
+        b1 = engine.submit(j1)
+        # A storage read between submits (joins the running tails on the engine stream).
+        grid.put_blocks(np.arange(40, 40 + len(blk3), dtype=np.uint64), np.stack(blk3))
+        # Batch 2: S2 again (as disk A, into nothing below), and the accounts
+        # immutable into S3 at the last level.
+        j2 = [grid_job(sid, [], [ti2.ref()], [], 2, False, 200, 2 * 9),
+              grid_job(sacc, [(acc_buf.ptr, len(acc_a))], [], [ti3.ref()], 3, True, 240, 3 * 65)]
+        b2 = engine.submit(j2)
+        # Batch 3: S1 again (trusted by now), and the corrupt S4.
+        j3 = [grid_job(sid, [], [ti1.ref()], [], 2, False, 500, 2 * 9),
+              grid_job(sid, [], [ti4.ref()], [], 2, False, 540, 2 * 9)]
+        b3 = engine.submit(j3)
+        for b in (b1, b2):
+            b.wait()
+        with pytest.raises(abi.TbcError):
+            b3.wait()
+        res = [b.result(i) for b in (b1, b2, b3) for i in range(2)]
+        for b in (b1, b2, b3):
+            b.release()
+        check_job(oracle_lib, grid, sid, *res[0], m1v, True, [s1v], False, 1, 64, j1[0].addresses)
+        check_job(oracle_lib, grid, sid, *res[1], m2v, True, [s2v], False, 1, 64, j1[1].addresses)
+        check_job(oracle_lib, grid, sid, *res[2], s2v, False, [], False, 2, 64, j2[0].addresses)
+        check_job(oracle_lib, grid, sacc, *res[3], acc_a, True, [s3v], True, 3, 64, j2[1].addresses)
+        check_job(oracle_lib, grid, sid, *res[4], s1v, False, [], False, 2, 64, j3[0].addresses)
+        assert res[5][0].status == abi.TBC_ERR_BLOCK_INVALID
+    finally:
+        grid.close()
+
+
+def test_failed_job_outputs_stay_unverified(engine, oracle_lib):
+    rng = np.random.default_rng(0xF00D)
+    grid = Grid(engine, 300)
+    spec = trees.BY_NAME["transfers.id"]
+    try:
+        bad_vals = sorted_unique(spec, 50_000, rng)
+        blocks, ti = storage_table(oracle_lib, spec, bad_vals, np.arange(1, 10, dtype=np.uint64))
+        bad = np.stack(blocks).copy()
+        bad[1, 256 + 999] ^= 0x40
+        grid.put_blocks(np.arange(1, 1 + len(bad), dtype=np.uint64), bad)
+        good_vals = sorted_unique(spec, 30_000, rng)
+        gblocks, gti = storage_table(oracle_lib, spec, good_vals, np.arange(20, 30, dtype=np.uint64))
+        grid.put_blocks(np.arange(20, 20 + len(gblocks), dtype=np.uint64), np.stack(gblocks))
+
+        def job(tref, base, level=2):
+            return Job(spec, [], [], False, False, level, CLUSTER, 48, np.arange(base, base + 9, dtype=np.uint64),
+                       None, flags=abi.COMPACTION_GRID, grid=grid, tables_a=[tref])
+
+        b = engine.submit([job(ti.ref(), 50), job(gti.ref(), 70)])
+        with pytest.raises(abi.TbcError):
+            b.wait()
+        (r_bad, inf_bad), (r_good, inf_good) = b.result(0), b.result(1)
+        b.release()
+        assert r_bad.status == abi.TBC_ERR_BLOCK_INVALID and r_good.status == 0
+        from tigerbeetle_amd.tables import TableInfo
+        t_bad = TableInfo.decode(inf_bad[0], spec.key_size)
+        t_good = TableInfo.decode(inf_good[0], spec.key_size)
+        # Flip a body byte of the first data block of each output table in HBM
+        # (slot 0 of each job's reservation: addresses 50 and 70).
+        for addr in (50, 70):
+            ptr = grid.pointer(addr)
+            abi.check(abi.lib().tbc_memset_device(engine.handle, ptr + 256 + 5, 0x5A, 1), "memset")
+        # The failed job's output is unverified: its reader validates it in
+        # full and finds the body checksum broken.
+        b = engine.submit([job(t_bad.ref(), 100, 3)])
+        with pytest.raises(abi.TbcError):
+            b.wait()
+        assert b.result(0)[0].status == abi.TBC_ERR_BLOCK_INVALID
+        b.release()
+        # The clean job's output is trusted (a cache hit: header checksum,
+        # address and header fields only), as the reference's grid cache is.
+        b = engine.submit([job(t_good.ref(), 130, 3)])
+        b.wait()
+        assert b.result(0)[0].status == 0
+        b.release()
+    finally:
+        grid.close()

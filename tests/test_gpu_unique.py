@@ -94,37 +94,74 @@ def test_unique_broken_small_blocks(oracle_lib, engine_small, name):
     _run(oracle_lib, engine_small, cases, 4096, seed=12)
 
 
-def test_unique_one_repeat_at_a_block_boundary(oracle_lib, engine_small):
-    """A single repeated key exactly where a data block starts (the check that
-    crosses producers)."""
+def _repeat_at_block_start(spec, vcm, block: int, first_in_a: bool, seed: int) -> workloads.JobInputs:
+    """Inputs whose merged order (A-first tie break) has exactly one repeated
+    key, at merged positions (block*vcm - 1, block*vcm): the last value of data
+    block `block - 1` and the first of data block `block` under the
+    speculation's layout. One of the pair is in A and the other in B
+    (`first_in_a` says which comes first), so both streams stay strictly
+    increasing and only the cross-stream check at a producer's first
+    position can see the repeat."""
+    rng = np.random.default_rng(seed)
+    n = 6 * vcm + 17
+    limbs = workloads.unique_sorted_keys(spec, n, rng)
+    vals = workloads.values_from_keys(spec, limbs, np.zeros(n, dtype=bool), rng)
+    k = block * vcm                           # first merged position of `block`
+    in_a = rng.random(n) < 0.5
+    in_a[k - 1], in_a[k] = first_in_a, not first_in_a
+    dup = vals[k].copy()
+    dup[:16] = vals[k - 1][:16]               # id (the key) of the position before
+    vals[k] = dup
+    a, b = vals[in_a], vals[~in_a]
+    # B as tables of whole blocks (a table holds 5 data blocks + 3 values at 4 KiB)
+    tmax = spec.value_count_max
+    return workloads.JobInputs(spec, a, False, [b[i:i + tmax] for i in range(0, len(b), tmax)], False)
+
+
+@pytest.mark.parametrize("block,first_in_a", [(1, True), (1, False), (2, True), (4, False)])
+def test_unique_one_repeat_at_a_block_boundary(oracle_lib, engine_small, block, first_in_a):
+    """A single repeated key exactly where a data block starts: the check that
+    crosses producers (a producer's first value against its predecessor in
+    the previous block) must break the speculation, and the recomputed blocks
+    must be the reference's. Constructed, never skipped."""
     spec = _spec("transfers.id", 4096)
-    rng = np.random.default_rng(3)
-    ji = workloads.make_job_inputs(spec, rng, n_a=1000, b_table_sizes=[1000], a_immutable=False, overlap=0.0)
     vcm = engine_small.layout(spec).block_value_count_max
-    # merged position vcm*2 (block 2's first value) takes the key of position vcm*2 - 1
-    merged = np.concatenate([ji.a_values, ji.b_tables[0]])
-    keys = workloads.keys_of(merged, spec)
-    order = np.lexsort(tuple(keys))
-    p, q = order[2 * vcm - 1], order[2 * vcm]
-    src, dst = merged[p].copy(), merged[q].copy()
-    # give dst src's key (ids are the first 16 bytes): dst then equals src in key
-    dst[:16] = src[:16]
-    na = len(ji.a_values)
-    if q < na:
-        ji.a_values[q] = dst
-    else:
-        ji.b_tables[0][q - na] = dst
-    # keep each stream sorted and B strictly increasing (A/B equal keys are the repeat)
-    if (p < na) == (q < na):
-        pytest.skip("both in one stream for this seed")
-    n = len(merged)
+    ji = _repeat_at_block_start(spec, vcm, block, first_in_a, seed=3 + block)
+    n = len(ji.a_values) + sum(len(t) for t in ji.b_tables)
+    rng = np.random.default_rng(5)
     addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, n, 4096) + 3, rng, 5)
     outcome = []
     (res,), _ = gpu_run(engine_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
     r, infos, blocks = res
     o = run_oracle(oracle_lib, ji, 4096, addrs)
+    assert o.status == 0 and r.status == 0
+    assert o.value_count == n - 1             # the A copy of the repeated key wins, the B copy is dropped
     assert outcome == [BROKEN]
-    assert r.block_count == len(o.blocks)
+    assert r.value_count == o.value_count and r.block_count == len(o.blocks)
+    for g, w in zip(blocks, o.blocks):
+        assert np.array_equal(disk_image(g), disk_image(w))
+    assert np.array_equal(infos, o.table_infos)
+
+
+def test_unique_no_repeat_at_block_starts_holds(oracle_lib, engine_small):
+    """The same construction without the repeat (A/B alternate across every
+    block start): the speculation holds."""
+    spec = _spec("transfers.id", 4096)
+    vcm = engine_small.layout(spec).block_value_count_max
+    rng = np.random.default_rng(9)
+    n = 6 * vcm + 17
+    limbs = workloads.unique_sorted_keys(spec, n, rng)
+    vals = workloads.values_from_keys(spec, limbs, np.zeros(n, dtype=bool), rng)
+    in_a = np.arange(n) % 2 == 0
+    tmax = spec.value_count_max
+    b = vals[~in_a]
+    ji = workloads.JobInputs(spec, vals[in_a], False, [b[i:i + tmax] for i in range(0, len(b), tmax)], False)
+    addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, n, 4096) + 3, rng, 5)
+    outcome = []
+    (res,), _ = gpu_run(engine_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
+    r, infos, blocks = res
+    o = run_oracle(oracle_lib, ji, 4096, addrs)
+    assert outcome == [HELD] and r.block_count == len(o.blocks)
     for g, w in zip(blocks, o.blocks):
         assert np.array_equal(disk_image(g), disk_image(w))
     assert np.array_equal(infos, o.table_infos)

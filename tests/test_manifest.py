@@ -56,14 +56,144 @@ def test_pack_matches_oracle_layout():
 @pytest.mark.gpu
 @pytest.mark.parametrize("bs,n", [(4096, 1), (4096, 95), (1 << 20, 1000), (1 << 20, 20000)])
 def test_gpu_manifest_blocks_equal_oracle(bs, n):
-    from tigerbeetle_amd import Engine
-    addrs = list(range(1000, 1010))
+    """tbc_manifest_close_blocks: several blocks closed in one call (bodies in
+    parallel, the header chain in order), the first linking a given checksum."""
+    from tigerbeetle_amd import Engine, Grid
+    addrs = list(range(3, 13))
     with Engine(device=0, block_size=bs) as eng:
-        got, gsums = manifest.manifest_blocks(eng, _infos(n, n), addrs, CLUSTER, previous_checksum=7,
-                                              previous_address=3)
-    want, wsums = oracle.manifest_blocks(_infos(n, n), addrs, CLUSTER, bs, previous_checksum=7, previous_address=3)
+        grid = Grid(eng, 16)
+        try:
+            got, gsums = manifest.manifest_blocks(grid, _infos(n, n), addrs, CLUSTER, previous_checksum=7,
+                                                  previous_address=2)
+        finally:
+            grid.close()
+    want, wsums = oracle.manifest_blocks(_infos(n, n), addrs, CLUSTER, bs, previous_checksum=7, previous_address=2)
     assert gsums == wsums
     assert all(np.array_equal(g, w) for g, w in zip(got, want)) and len(got) == len(want)
+
+
+@pytest.mark.gpu
+def test_gpu_manifest_chain_links_a_block_closed_earlier():
+    """A close whose first block links the previous block by address only: the
+    engine reads that block's header checksum from the grid (no host wait)."""
+    from tigerbeetle_amd import Engine, Grid
+    bs = 4096
+    with Engine(device=0, block_size=bs) as eng:
+        grid = Grid(eng, 16)
+        try:
+            first, sums1 = manifest.manifest_blocks(grid, _infos(40, 1), [5, 6], CLUSTER)
+            images = manifest.pack_blocks(_infos(31, 2), [9, 10], CLUSTER, bs, previous_address=6)
+            manifest.close_on_grid(grid, images, [9, 10], previous_address=6, previous_checksum=None)
+            got = grid.get_blocks([9, 10])
+        finally:
+            grid.close()
+    want, _ = oracle.manifest_blocks(_infos(31, 2), [9, 10], CLUSTER, bs, previous_checksum=sums1[-1],
+                                     previous_address=6)
+    for g, w in zip(got, want):
+        assert np.array_equal(g[:len(w)], w)
+
+
+class _DictStore:
+    """The oracle's close_block into a host dict (the CPU side of the log tests)."""
+
+    def __init__(self, bs):
+        self.bs, self.grid, self.sums, self.closed = bs, {}, {}, []
+
+    def close(self, infos, address, previous_address):
+        imgs, sums = oracle.manifest_blocks(infos, [address], CLUSTER, self.bs,
+                                            previous_checksum=self.sums.get(previous_address, 0),
+                                            previous_address=previous_address)
+        self.grid[address], self.sums[address] = imgs[0], sums[0]
+        self.closed.append(address)
+
+    def read(self, address):
+        return self.grid[address]
+
+
+def _drive_log(log, rng, half_bars: int, events_per_half_bar: int):
+    """A random but valid event stream (insert, then update to invisible or a
+    move, then remove), half-bar by half-bar, as Tree.compact_end appends:
+    returns the model's live tables {address: encoded entry}."""
+    from tigerbeetle_amd.tables import EVENT_INSERT, EVENT_REMOVE, EVENT_UPDATE, TableInfo
+    live, invisible, next_addr = {}, {}, [10_000]
+    op = 32
+    for hb in range(half_bars):
+        log.compact(op)
+        for _ in range(events_per_half_bar):
+            r = rng.random()
+            if r < 0.45 or not live:
+                a = next_addr[0]
+                next_addr[0] += 1
+                lo = int(rng.integers(0, 1 << 40))
+                t = TableInfo(lo, lo + int(rng.integers(1, 1 << 20)), int(rng.integers(1, 1 << 62)) << 60 | a, a, op,
+                              (1 << 64) - 1, int(rng.integers(1, 9000)), 8, int(rng.integers(0, 7)))
+                e = t.encode(8, t.level, EVENT_INSERT, 16)
+                live[a] = (t, e)
+            elif r < 0.75:
+                a = list(live)[int(rng.integers(0, len(live)))]
+                t, _ = live[a]
+                if rng.random() < 0.3 and t.level < 6:        # a move: update at the next level
+                    t = TableInfo(t.key_min, t.key_max, t.checksum, a, t.snapshot_min, t.snapshot_max,
+                                  t.value_count, 8, t.level + 1)
+                    live[a] = (t, t.encode(8, t.level, EVENT_UPDATE, 16))
+                    e = live[a][1]
+                else:                                          # an input: snapshot_max set, then removed
+                    t = TableInfo(t.key_min, t.key_max, t.checksum, a, t.snapshot_min, op + 15, t.value_count, 8,
+                                  t.level)
+                    e = t.encode(8, t.level, EVENT_UPDATE, 16)
+                    del live[a]
+                    invisible[a] = t
+            elif invisible:
+                a = list(invisible)[int(rng.integers(0, len(invisible)))]
+                t = invisible.pop(a)
+                e = t.encode(8, t.level, EVENT_REMOVE, 16)
+            else:
+                continue
+            log.append(e)
+        log.compact_end()
+        op += 16
+    return live, invisible
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_manifest_log_compaction_and_recovery(seed):
+    """ManifestLog at test_min block size (30 entries a block) over many
+    half-bars: blocks close when full, the oldest are compacted (latest
+    extents re-appended, the rest dropped) and released; after a checkpoint,
+    opening the log newest-first (ManifestLog.open) and replaying it
+    chronologically (Forest.verify_tables_recovered's strategy 1) both give
+    exactly the model's tables, and the extents cover them (verify_table_extents)."""
+    from tigerbeetle_amd.forest import FreeSet
+    rng = np.random.default_rng(seed)
+    fs = FreeSet(1 << 16)
+    store = _DictStore(4096)
+    log = manifest.ManifestLog(store, fs, 4096)
+    assert log.entry_count_max == 30
+    live, invisible = _drive_log(log, rng, half_bars=300, events_per_half_bar=12)
+    log.checkpoint()
+    assert log.stats["blocks_compacted"] > 20 and log.stats["entries_dropped"] > 0
+    blocks = [store.grid[a] for a in log.log_addresses]
+    for b, blk in enumerate(blocks):  # the chain: each block links the one before it in the log
+        prev_a = int(blk[160:168].view(np.uint64)[0])
+        if b:
+            assert prev_a == log.log_addresses[b - 1]
+    opened = manifest.open_log(blocks)
+    replayed = manifest.replay_log(blocks)
+    want = {a: e for a, (t, e) in live.items()}
+    want.update({a: t.encode(8, t.level, 2, 16) for a, t in invisible.items()})
+    assert set(opened) == set(want) == set(log.table_extents)
+    for a, e in want.items():
+        assert np.array_equal(opened[a], e)
+    assert sorted(int(e[96:104].view(np.uint64)[0]) for e in replayed.values()) == sorted(want)
+
+
+def test_manifest_pace_production():
+    # manifest_log.zig Pace for the production forest (21 trees, 1 MiB blocks)
+    p = manifest.Pace(manifest.TREE_COUNT, manifest.TABLE_COUNT_MAX, 1, manifest.entry_count_max(1 << 20))
+    assert (p.half_bar_append_blocks_max, p.half_bar_compact_blocks_max, p.log_blocks_full_max) == (1, 2, 293)
+    assert p.log_blocks_cycle_max == 586 and p.log_blocks_max > p.log_blocks_cycle_max
+    assert p.half_bar_compact_blocks(0, 100) == 0 and p.half_bar_compact_blocks(3, 100) == 2
+    assert p.half_bar_compact_blocks(585, 100) == 2
 
 
 def test_no_entries_no_blocks():

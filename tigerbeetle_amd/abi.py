@@ -133,6 +133,8 @@ _SIGNATURES = {
     "tbc_engine_init": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.POINTER(_P)]),
     "tbc_engine_deinit": (None, [_P]),
     "tbc_tree_layout_get": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.POINTER(TreeLayout)]),
+    "tbc_engine_arena_usage": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                              ctypes.POINTER(ctypes.c_uint32)]),
     "tbc_device_alloc": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
     "tbc_device_free": (ctypes.c_int, [_P, _P]),
     "tbc_copy_to_device": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64]),
@@ -170,6 +172,8 @@ _SIGNATURES = {
     "tbc_grid_block_pointer": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
     "tbc_grid_put_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
     "tbc_grid_get_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
+    "tbc_manifest_close_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P),
+                                                 ctypes.c_uint32, ctypes.c_uint64, _P]),
     "tbc_memtable_init": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.c_uint32, ctypes.POINTER(_P)]),
     "tbc_memtable_deinit": (None, [_P]),
     "tbc_memtable_put": (ctypes.c_int, [_P, _P, ctypes.c_uint32]),

@@ -521,6 +521,64 @@ __global__ __launch_bounds__(1024) void k_checksum_batch(const uint64_t *ptrs, c
     if ((lane & 31) < 4 && mine < count) gst<uint32_t>(out + 16 * (size_t)i + 4 * (lane & 3), tag);
 }
 
+// ManifestLog.close_block (src/lsm/manifest_log.zig:876-952) of manifest
+// blocks already staged in the grid (header fields packed by the host, entries
+// in the body, zero padding): the body checksums, one message per 32-lane
+// group, in parallel ...
+__global__ __launch_bounds__(1024) void k_manifest_bodies(const uint64_t *addresses, uint32_t count,
+                                                          uint8_t *grid_base, uint32_t block_size) {
+    __shared__ uint32_t sT[kTableDwords];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (2 * wave >= count) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t mine = 2 * wave + (lane >> 5);
+    const uint32_t i = mine < count ? mine : mine - 1;
+    uint8_t *blk = grid_base + (size_t)(addresses[i] - 1) * block_size;
+    GlobalMsg m(blk + kHeaderSize, gld<uint32_t>(blk + 96) - kHeaderSize);
+    const uint32_t tag = aegis_mac32(sT, m);
+    if ((lane & 31) < 4 && mine < count) gst<uint32_t>(blk + 32 + 4 * (lane & 3), tag); // set_checksum_body
+}
+
+// ... then the header chain, in log order on one wave: each header's metadata
+// links the previous block's header checksum (the first block's comes from
+// the host, or from the header of `previous_address` in the grid, written by
+// an earlier close on this stream), then set_checksum over [16, 256).
+__global__ __launch_bounds__(64) void k_manifest_chain(const uint64_t *addresses, uint32_t count, uint8_t *grid_base,
+                                                       uint32_t block_size, uint64_t previous_address,
+                                                       const uint64_t *previous_checksum) {
+    __shared__ uint32_t sT[kTableDwords];
+    __shared__ uint32_t hdr[64];
+    load_tables(sT);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x;
+    uint32_t prev = 0; // lane c < 4: column c of the previous block's checksum
+    if (lane < 4) {
+        if (previous_checksum)
+            prev = (uint32_t)(previous_checksum[lane >> 1] >> (32 * (lane & 1)));
+        else if (previous_address)
+            prev = gld<uint32_t>(grid_base + (size_t)(previous_address - 1) * block_size + 4 * lane);
+    }
+    for (uint32_t i = 0; i < count; i++) {
+        uint8_t *blk = grid_base + (size_t)(addresses[i] - 1) * block_size;
+        hdr[lane] = gld<uint32_t>(blk + 4 * lane);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 4) {
+            hdr[32 + lane] = prev; // Metadata.previous_manifest_block_checksum
+            gst<uint32_t>(blk + 128 + 4 * lane, prev);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        LdsMsg m(hdr + 4, kHeaderSize - 16);
+        const uint32_t tag = aegis_mac32(sT, m);
+        // Lanes c < 4 of the lower group hold column c of the tag.
+        if (lane < 4) gst<uint32_t>(blk + 4 * lane, tag);
+        prev = lane < 4 ? tag : 0u;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // grid.read_block_validate (src/vsr/grid.zig:1059-1084) for a batch of
 // blocks: one wave per block, the lower 32-lane group checksums the header
 // (bytes [16, 256)), the upper group the body ([256, size)); then the checks
@@ -1785,6 +1843,18 @@ int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *grid_base, uint32_t block_size,
+                          uint64_t previous_address, const uint64_t *d_previous_checksum, void *stream) {
+    if (count == 0) return 0;
+    const uint32_t wpb = waves_per_block((count + 1) / 2);
+    hipLaunchKernelGGL(k_manifest_bodies, dim3(((count + 1) / 2 + wpb - 1) / wpb), dim3(64 * wpb), 0,
+                       (hipStream_t)stream, d_addresses, count, grid_base, block_size);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_manifest_chain, dim3(1), dim3(64), 0, (hipStream_t)stream, d_addresses, count, grid_base,
+                       block_size, previous_address, d_previous_checksum);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream) {
     if (count == 0) return 0;
@@ -1792,6 +1862,12 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
     hipLaunchKernelGGL(k_checksum_batch, dim3((count + wpb - 1) / wpb), dim3(64 * wpb), 0, (hipStream_t)stream,
                        d_ptrs, d_lens, count, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+uint32_t fused_max_chain_waves() {
+    static const uint32_t v = getenv("TBC_FUSED_MAX_WAVES") ? (uint32_t)atoi(getenv("TBC_FUSED_MAX_WAVES"))
+                                                            : kFusedMaxChainWaves; // A/B measurement only
+    return v;
 }
 
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
@@ -1815,9 +1891,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         if (mark) mark(mark_ctx, "assemble");
         return 0;
     }
-    static const uint32_t fused_max = getenv("TBC_FUSED_MAX_WAVES") ? (uint32_t)atoi(getenv("TBC_FUSED_MAX_WAVES"))
-                                                                    : kFusedMaxChainWaves; // A/B measurement only
-    if (total_dblocks && waves <= fused_max) {
+    if (total_dblocks && waves <= fused_max_chain_waves()) {
         // Latency regime: every chain is in flight at once; producers fill
         // the bodies while the chains absorb them.
         if (maybe_sparse) { // heavy-dedup jobs: bodies first, parallel (sparse_job decides on device)

@@ -27,24 +27,50 @@ using namespace tbc;
 namespace {
 
 constexpr uint64_t kDefaultArena = 256ull << 20;
-// aegis.hip kFusedMaxChainWaves: above it a batch is in the throughput regime.
-constexpr uint64_t kFusedChainWaves = 2048;
 constexpr uint64_t kPinnedArena = 64ull << 20;
 constexpr uint32_t kIndexLdsMax = 16384; // k_index_blocks LDS image
 constexpr int kMaxMarks = 16;
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+// A stack of regions: a batch or k-way merge opens one at submit and closes
+// it at release. Closing the topmost region pops it and every closed region
+// below it, so regions released out of order are reclaimed as soon as the
+// ones above them are; the top never grows past the live regions' extent.
+// (Synchronous calls take scratch above the top with alloc() and restore it.)
 struct Arena {
+    struct Region {
+        uint64_t start, end;
+        bool open;
+    };
     uint8_t *base = nullptr;
     uint64_t size = 0, top = 0;
-    uint32_t live = 0;
+    std::vector<Region> regions;
     uint8_t *alloc(uint64_t bytes) {
         uint64_t start = align_up(top, 256);
         if (start + bytes > size) return nullptr;
         top = start + bytes;
         return base + start;
     }
+    // A region of `bytes`; *end identifies it for close().
+    uint8_t *open(uint64_t bytes, uint64_t *end) {
+        const uint64_t start = top;
+        uint8_t *p = alloc(bytes);
+        if (!p) return nullptr;
+        regions.push_back(Region{start, top, true});
+        *end = top;
+        return p;
+    }
+    void close(uint64_t end) {
+        for (auto it = regions.rbegin(); it != regions.rend(); ++it)
+            if (it->open && it->end == end) {
+                it->open = false;
+                break;
+            }
+        while (!regions.empty() && !regions.back().open) regions.pop_back();
+        top = regions.empty() ? 0 : regions.back().end;
+    }
+    size_t live() const { return regions.size(); }
 };
 
 struct Layout {
@@ -220,8 +246,7 @@ static bool ensure_masks(tbc_engine *e, uint64_t words) {
 struct tbc_batch {
     tbc_engine *engine = nullptr;
     uint32_t count = 0;
-    uint8_t *dev_mark = nullptr, *host_mark = nullptr; // arena tops to restore on release
-    uint64_t dev_top = 0, host_top = 0;
+    uint64_t dev_region = 0, host_region = 0; // arena regions (Arena::open) closed on release
     JobResultDev *h_results = nullptr;
     uint8_t *h_infos = nullptr;
     std::vector<uint32_t> info_base; // per original job index
@@ -244,9 +269,8 @@ struct tbc_kway {
     tbc_engine *engine = nullptr;
     hipEvent_t done = nullptr;
     uint32_t *h_count = nullptr; // pinned: the merged value count
-    uint64_t dev_top = 0, host_top = 0;
+    uint64_t host_region = 0; // pinned arena region (device scratch is the engine's)
     bool arena = false;
-    bool host_only = false; // only the pinned arena (device scratch is the engine's)
     bool complete = false;
     tbc_status result = TBC_OK;
     uint64_t count = 0;
@@ -369,6 +393,14 @@ void tbc_engine_deinit(tbc_engine *e) {
     delete e;
 }
 
+tbc_status tbc_engine_arena_usage(const tbc_engine *e, uint64_t *dev_bytes, uint64_t *host_bytes, uint32_t *regions) {
+    if (!e || !dev_bytes || !host_bytes || !regions) return TBC_ERR_INVALID_ARGUMENT;
+    *dev_bytes = e->dev.top;
+    *host_bytes = e->host.top;
+    *regions = (uint32_t)(e->dev.live() + e->host.live());
+    return TBC_OK;
+}
+
 tbc_status tbc_grid_init(tbc_engine *e, uint64_t block_count, tbc_grid **out) {
     if (!e || !out || block_count == 0) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
@@ -433,6 +465,71 @@ tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *con
         if (!stage_d2h(e, blocks[i], g->base + (addresses[i] - 1) * e->block_size, e->block_size))
             return TBC_ERR_DEVICE;
     return TBC_OK;
+}
+
+tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *host_images,
+                                     uint32_t count, uint64_t previous_address, const uint64_t *previous_checksum) {
+    if (!g || (count && (!addresses || !host_images))) return TBC_ERR_INVALID_ARGUMENT;
+    tbc_engine *e = g->engine;
+    const uint32_t bs = e->block_size;
+    const uint32_t entry_max = (bs - kHeaderSize) / kTableInfoSize;
+    if (previous_address > g->block_count) return TBC_ERR_INVALID_ARGUMENT;
+    // The host packs the header fields (ManifestLog.acquire_block + the
+    // metadata of close_block); check them as verify_block and
+    // ManifestNode.metadata (schema.zig:534-554) will.
+    for (uint32_t i = 0; i < count; i++) {
+        const uint8_t *h = (const uint8_t *)host_images[i];
+        if (!h || addresses[i] == 0 || addresses[i] > g->block_count) return TBC_ERR_INVALID_ARGUMENT;
+        uint32_t size, entries;
+        uint64_t address, prev_address;
+        memcpy(&size, h + 96, 4);
+        memcpy(&entries, h + 168, 4);
+        memcpy(&address, h + 224, 8);
+        memcpy(&prev_address, h + 160, 8);
+        const uint64_t want_prev = i == 0 ? previous_address : addresses[i - 1];
+        if (size < kHeaderSize + kTableInfoSize || size > bs || (size - kHeaderSize) % kTableInfoSize ||
+            entries != (size - kHeaderSize) / kTableInfoSize || entries > entry_max || address != addresses[i] ||
+            prev_address != want_prev || h[110] != 20 || h[240] != 3)
+            return TBC_ERR_INVALID_ARGUMENT;
+    }
+    if (!count) return TBC_OK;
+    hipSetDevice(e->device);
+    if (!join_tails(e)) return TBC_ERR_DEVICE;
+    // Addresses and the previous checksum go through a pinned staging slot
+    // (reusable once the stream has passed this close), the images through
+    // the staging ring into their grid slots.
+    Staging &st = e->staging;
+    const uint64_t meta = 8ull * count + 16;
+    if (meta > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
+    for (uint32_t i = 0; i < count; i++) {
+        uint32_t size;
+        memcpy(&size, (const uint8_t *)host_images[i] + 96, 4);
+        if (!stage_h2d(e, g->base + (addresses[i] - 1) * bs, host_images[i], sector_ceil(size)))
+            return TBC_ERR_DEVICE;
+    }
+    const int slot = st.next;
+    st.next = (st.next + 1) % Staging::kSlots;
+    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
+    uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    memcpy(host, addresses, 8ull * count);
+    if (previous_checksum) memcpy(host + 8ull * count, previous_checksum, 16);
+    // The device copy of the descriptors lives in the slot's mirror in the
+    // device arena region of this call (freed once enqueued work is ordered
+    // before any later arena use: the region is closed after the launch and
+    // the next user of the arena is later on the same stream).
+    uint64_t region = 0;
+    uint8_t *d = e->dev.open(meta, &region);
+    if (!d) return TBC_ERR_OUT_OF_MEMORY;
+    bool ok = hipMemcpyAsync(d, host, meta, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
+              launch_manifest_close((const uint64_t *)d, count, g->base, bs, previous_address,
+                                    previous_checksum ? (const uint64_t *)(d + 8ull * count) : nullptr, e->stream) == 0 &&
+              hipEventRecord(st.ev[slot], e->stream) == hipSuccess;
+    st.used[slot] = true;
+    e->dev.close(region);
+    // Engine-written manifest blocks are trusted like compaction outputs.
+    for (uint32_t i = 0; ok && i < count; i++)
+        ok = hipMemsetAsync(g->verified + addresses[i] - 1, 1, 1, e->stream) == hipSuccess;
+    return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_memtable_init(tbc_engine *e, const tbc_tree *tree, uint32_t capacity, tbc_memtable **out) {
@@ -817,17 +914,12 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
     temp[0] = e->kway_scratch;
     temp[1] = e->kway_scratch + temp_bytes;
     uint8_t *scratch = e->kway_scratch + 2 * temp_bytes;
-    k->dev_top = e->dev.top;
-    k->host_top = e->host.top;
-    uint8_t *h = e->host.alloc(count_bytes + desc_bytes + 256);
+    uint8_t *h = e->host.open(count_bytes + desc_bytes + 256, &k->host_region);
     if (!h) {
-        e->host.top = k->host_top;
         delete k;
         return TBC_ERR_OUT_OF_MEMORY;
     }
-    e->host.live++;
     k->arena = true;
-    k->host_only = true;
     uint32_t *splits = (uint32_t *)scratch;
     uint64_t *masks = (uint64_t *)(scratch + align_up(4 * max_slots, 256));
     uint32_t *tile_cnt = (uint32_t *)((uint8_t *)masks + align_up(8 * 2 * (T / 64) * max_tiles, 256));
@@ -928,15 +1020,7 @@ void tbc_kway_release(tbc_kway *k) {
     hipSetDevice(e->device);
     if (!k->complete && k->done) hipEventSynchronize(k->done);
     if (k->done) e->event_pool.push_back(k->done);
-    if (k->arena) { // same protocol as batches: LIFO restores the tops, idle reclaims
-        if (!k->host_only) {
-            if (e->dev.live) e->dev.live--;
-            if (e->dev.live == 0) e->dev.top = 0;
-            else e->dev.top = std::min(e->dev.top, std::max(k->dev_top, e->dev.top));
-        }
-        if (e->host.live) e->host.live--;
-        if (e->host.live == 0) e->host.top = 0;
-    }
+    if (k->arena) e->host.close(k->host_region);
     delete k;
 }
 
@@ -1120,7 +1204,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // batch: every chain runs at once, so starting them before any merge is
     // what it buys (aegis.hip produce_unique).
     const bool spec_regime = !grid_mode && !pipeline && !(flags0 & TBC_COMPACTION_VALUES_ONLY) &&
-                             (uint64_t)(dblocks + 1) / 2 <= kFusedChainWaves;
+                             (uint64_t)(dblocks + 1) / 2 <= fused_max_chain_waves();
     static const bool no_spec = getenv("TBC_NO_SPECULATION") != nullptr; // A/B measurement only
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
@@ -1147,18 +1231,13 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8 + 8ull * tiles + 16 + 32, 256);
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
-    b->dev_top = e->dev.top;
-    b->host_top = e->host.top;
-    uint8_t *dbase = e->dev.alloc(sz_in + sz_splits + sz_tiles + sz_res + sz_infos);
-    uint8_t *hbase = e->host.alloc(sz_in + sz_res + sz_infos);
+    uint8_t *dbase = e->dev.open(sz_in + sz_splits + sz_tiles + sz_res + sz_infos, &b->dev_region);
+    uint8_t *hbase = dbase ? e->host.open(sz_in + sz_res + sz_infos, &b->host_region) : nullptr;
     if (!dbase || !hbase) {
-        e->dev.top = b->dev_top;
-        e->host.top = b->host_top;
+        if (dbase) e->dev.close(b->dev_region);
         delete b;
         return TBC_ERR_OUT_OF_MEMORY;
     }
-    e->dev.live++;
-    e->host.live++;
     uint8_t *d_in = dbase;
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
     SplitDesc *d_bsplits = any_unique ? d_splits + splits : nullptr;
@@ -1175,7 +1254,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // serialises tiles that then copy), so it is off unless asked for
     // (TBC_MERGE_BODIES=1, A/B measurement; parity-tested either way).
     static const bool merge_bodies_env = getenv("TBC_MERGE_BODIES") != nullptr;
-    const bool throughput = (uint64_t)(dblocks + 1) / 2 > kFusedChainWaves;
+    const bool throughput = (uint64_t)(dblocks + 1) / 2 > fused_max_chain_waves();
     const bool merge_bodies = merge_bodies_env && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
                                                    throughput);
     uint64_t *m_lb = merge_bodies ? d_lookback : nullptr;
@@ -1298,9 +1377,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && count)
             ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
                                     e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
-        // Outputs written by the engine are trusted like the reference's grid
-        // cache entries (grid.zig:802-841).
-        if (ok) ok = launch_grid_mark((const JobDesc *)d_in, (int)count, grid0->verified, T) == 0;
         for (int o = 0; ok && o < tbc_engine::kTails; o++)
             if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
         if (ok && n_checks)
@@ -1309,6 +1385,9 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                       (int)count, d_res, e->block_size, T) == 0 &&
                  launch_grid_checks(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
                                     d_res, e->block_size, T) == 0;
+        // Outputs written by the engine are trusted like the reference's grid
+        // cache entries (grid.zig:802-841), once the job's inputs checked out.
+        if (ok) ok = launch_grid_mark((const JobDesc *)d_in, (int)count, grid0->verified, d_res, T) == 0;
         mark_cb(b, "grid_check");
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
@@ -1374,11 +1453,36 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     return TBC_OK;
 }
 
-// Above this many chain waves a batch is in the throughput regime (aegis.hip
-// kFusedMaxChainWaves): it is split into job groups that pipeline (each
-// group's chains beside the next group's merge and bodies).
-constexpr uint64_t kGroupMinChainWaves = 2048;
+// Above fused_max_chain_waves() chain waves a batch is in the throughput
+// regime: it is split into job groups that pipeline (each group's chains
+// beside the next group's merge and bodies).
 constexpr uint32_t kMaxGroups = 4; // config 5: 1 -> 16.1, 2 -> 14.6, 3 -> 14.4, 4 -> 14.3, 6 -> 17.2 ms
+
+// The checks submit_impl makes of one non-grid compaction, for a batch that
+// is split into groups: every job is checked before any group is enqueued,
+// so a rejected batch touches nothing on the device.
+static tbc_status check_plain_job(const tbc_engine *e, const tbc_compaction &c, uint8_t flags0) {
+    Layout L;
+    if (!compute_layout(&c.tree, e->block_size, &L) || L.index_size > kIndexLdsMax ||
+        (c.a_immutable && c.segment_count_a > 1) || !c.output_blocks || (c.segment_count_a && !c.segments_a) ||
+        (c.segment_count_b && !c.segments_b) || (c.address_count && !c.addresses) ||
+        (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID | TBC_COMPACTION_UNIQUE_KEYS)) ||
+        ((c.flags ^ flags0) & ~TBC_COMPACTION_UNIQUE_KEYS) || (c.flags & TBC_COMPACTION_GRID))
+        return TBC_ERR_INVALID_ARGUMENT;
+    uint64_t n = 0;
+    for (int side = 0; side < 2; side++) {
+        const uint32_t ns = side == 0 ? c.segment_count_a : c.segment_count_b;
+        for (uint32_t k = 0; k < ns; k++) {
+            const tbc_segment &g = (side == 0 ? c.segments_a : c.segments_b)[k];
+            if (!g.count || !g.values || ((uintptr_t)g.values & 15)) return TBC_ERR_INVALID_ARGUMENT;
+            n += g.count;
+        }
+    }
+    if (n > 0xffff0000ull) return TBC_ERR_INVALID_ARGUMENT;
+    const uint64_t db_max = (n + L.vcm - 1) / L.vcm;
+    if (db_max + (db_max + L.dbcm - 1) / L.dbcm > c.address_count) return TBC_ERR_CAPACITY;
+    return TBC_OK;
+}
 
 tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
@@ -1398,11 +1502,12 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
             waves += (n[i] + L.vcm - 1) / L.vcm / 2;
         }
         static const uint32_t max_groups = getenv("TBC_GROUPS") ? (uint32_t)atoi(getenv("TBC_GROUPS")) : kMaxGroups;
-        static const uint64_t min_waves = getenv("TBC_FUSED_MAX_WAVES") ? (uint64_t)atoi(getenv("TBC_FUSED_MAX_WAVES"))
-                                                                       : kGroupMinChainWaves;
+        const uint64_t min_waves = fused_max_chain_waves();
         if (waves > min_waves && max_groups > 1) groups = std::min<uint32_t>(max_groups, count);
     }
     if (groups == 1) return submit_impl(e, jobs_in, count, false, out);
+    for (uint32_t i = 0; i < count; i++)
+        if (const tbc_status st = check_plain_job(e, jobs_in[i], jobs_in[0].flags); st != TBC_OK) return st;
     // Contiguous groups of about equal input (job order kept inside a group).
     uint64_t total = 0;
     for (uint32_t i = 0; i < count; i++) total += n[i];
@@ -1596,12 +1701,8 @@ void tbc_batch_release(tbc_batch *b) {
     if (b->done) e->event_pool.push_back(b->done);
     if (b->fork) e->event_pool.push_back(b->fork);
     if (b->h_results) {
-        // LIFO release restores the arena tops; otherwise reclaim when idle.
-        if (e->dev.live) e->dev.live--;
-        if (e->host.live) e->host.live--;
-        if (e->dev.live == 0) e->dev.top = 0;
-        else e->dev.top = std::min(e->dev.top, std::max(b->dev_top, e->dev.top));
-        if (e->host.live == 0) e->host.top = 0;
+        e->dev.close(b->dev_region);
+        e->host.close(b->host_region);
     }
     delete b;
 }

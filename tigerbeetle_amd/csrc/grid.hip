@@ -17,7 +17,8 @@
 //                   fields the iterators assert, to every input block (cheap);
 //   k_grid_validate (aegis.hip) runs read_block_validate on the blocks staged
 //                   from storage, on a second stream beside the compaction;
-//   k_grid_mark     trusts the batch's outputs (written by the engine itself).
+//   k_grid_mark     trusts the batch's outputs (written by the engine itself)
+//                   once its input checks passed.
 #include <hip/hip_runtime.h>
 
 #include "tbc_internal.h"
@@ -95,10 +96,16 @@ __global__ __launch_bounds__(256) void k_grid_check(const InputCheck *checks, ui
 }
 
 // Outputs of the batch's grid jobs are trusted from now on (every reserved
-// address: unused ones are never named by an index block of this batch).
-__global__ __launch_bounds__(256) void k_grid_mark(const JobDesc *jobs, int njobs, uint8_t *verified) {
+// address: unused ones are never named by an index block of this batch) —
+// after the batch's input checks, and only for jobs that ended clean: blocks
+// built from a corrupt input or by a job that hit an invariant stay
+// unverified, so a later batch naming them validates them in full.
+__global__ __launch_bounds__(256) void k_grid_mark(const JobDesc *jobs, int njobs, uint8_t *verified,
+                                                   const JobResultDev *res) {
     const JobDesc &j = jobs[blockIdx.x];
     if (!j.grid_base) return;
+    const JobResultDev &r = res[j.job_index];
+    if (r.status || r.invariant || r.block_error) return;
     for (uint32_t a = threadIdx.x; a < j.address_count; a += 256) verified[gld<uint64_t>(j.addresses + a) - 1] = 1;
 }
 
@@ -126,9 +133,11 @@ int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, void *stream) {
+int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, const JobResultDev *d_results,
+                     void *stream) {
     if (!njobs) return 0;
-    hipLaunchKernelGGL(k_grid_mark, dim3(njobs), dim3(256), 0, (hipStream_t)stream, d_jobs, njobs, d_verified);
+    hipLaunchKernelGGL(k_grid_mark, dim3(njobs), dim3(256), 0, (hipStream_t)stream, d_jobs, njobs, d_verified,
+                       d_results);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

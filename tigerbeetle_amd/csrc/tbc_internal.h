@@ -316,7 +316,15 @@ int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t
                        int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
 int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_verified, const JobDesc *d_jobs,
                          int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
-int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, void *stream);
+int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, const JobResultDev *d_results,
+                     void *stream);
+// The chain-wave count above which a batch is in the throughput regime
+// (aegis.hip; TBC_FUSED_MAX_WAVES overrides it for A/B measurement).
+uint32_t fused_max_chain_waves();
+// ManifestLog.close_block of `count` staged manifest blocks (grid addresses in
+// d_addresses): body checksums, then the header chain in order.
+int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *grid_base, uint32_t block_size,
+                          uint64_t previous_address, const uint64_t *d_previous_checksum, void *stream);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
 struct SortItem {

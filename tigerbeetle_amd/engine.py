@@ -215,6 +215,13 @@ class Batch:
               "tbc_batch_result")
         return r, infos[: r.table_count]
 
+    def check_results(self) -> None:
+        """Raise if any compaction of the (complete) batch did not end TBC_OK."""
+        for i in range(len(self.jobs)):
+            r = abi.CompactionResult()
+            check(lib().tbc_batch_result(self.handle, i, ctypes.byref(r), None, 0), "tbc_batch_result")
+            check(r.status, f"compaction {i} of the batch")
+
     def speculation(self, index: int) -> int:
         """abi.SPECULATION_NONE / _HELD / _BROKEN of compaction `index` (tbc_batch_speculation)."""
         out = ctypes.c_uint32()
@@ -298,6 +305,14 @@ class Engine:
         t = tree.ctype()
         check(lib().tbc_tree_layout_get(self.handle, ctypes.byref(t), ctypes.byref(out)), "tbc_tree_layout_get")
         return out
+
+    def arena_usage(self) -> tuple:
+        """(device bytes, pinned host bytes, open regions) of the static arenas
+        held by unreleased batches and k-way merges (tbc_engine_arena_usage)."""
+        d, h, n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()
+        check(lib().tbc_engine_arena_usage(self.handle, ctypes.byref(d), ctypes.byref(h), ctypes.byref(n)),
+              "tbc_engine_arena_usage")
+        return d.value, h.value, n.value
 
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)

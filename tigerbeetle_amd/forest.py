@@ -26,7 +26,7 @@ from dataclasses import dataclass, field, replace
 import numpy as np
 
 from . import trees
-from .tables import SNAPSHOT_LATEST, TableInfo
+from .tables import EVENT_INSERT, EVENT_REMOVE, EVENT_UPDATE, SNAPSHOT_LATEST, TableInfo
 
 LSM_LEVELS = trees.LSM_LEVELS            # config.zig:140
 GROWTH = trees.LSM_GROWTH_FACTOR         # config.zig:141
@@ -61,6 +61,7 @@ class FreeSet:
         self.acquired = np.zeros(block_count, dtype=bool)
         self.reservation_blocks = 0
         self.reservation_count = 0
+        self.released = 0
 
     def reserve(self, count: int) -> tuple:
         base = self.reservation_blocks
@@ -82,6 +83,22 @@ class FreeSet:
         assert not self.acquired[a - 1].any()
         self.acquired[a - 1] = True
 
+    def acquire_from(self, reservation: tuple) -> int:
+        """FreeSet.acquire(reservation) (free_set.zig:280-311): the first free
+        block of the reservation, now acquired (the manifest log's blocks)."""
+        base, count = reservation
+        free = np.flatnonzero(~self.acquired[base:base + count])
+        assert len(free), "reservation exhausted"
+        address = base + int(free[0]) + 1
+        self.acquired[address - 1] = True
+        return address
+
+    def release(self, address: int) -> None:
+        """FreeSet.release (free_set.zig:383-390): staged until the next
+        checkpoint, which a replay never reaches, so never reused."""
+        assert self.acquired[address - 1]
+        self.released += 1
+
     def forfeit(self) -> None:
         self.reservation_count -= 1
         if self.reservation_count == 0:
@@ -89,7 +106,9 @@ class FreeSet:
 
 
 class Level:
-    """ManifestLevel: tables ordered by (key_max, snapshot_min)."""
+    """ManifestLevel: tables ordered by (key_max, snapshot_min)
+    (manifest_level.zig:41-70); invisible tables stay until
+    remove_invisible removes them."""
 
     def __init__(self):
         self.tables: list = []
@@ -100,6 +119,46 @@ class Level:
     def insert(self, t: TableInfo) -> None:
         self.tables.append(t)
         self.tables.sort(key=lambda x: (x.key_max, x.snapshot_min))
+
+    def set_snapshot_max(self, t: TableInfo, snapshot: int) -> TableInfo:
+        """ManifestLevel.set_snapshot_max (manifest_level.zig:243-266)."""
+        assert t.snapshot_max == SNAPSHOT_LATEST and snapshot < SNAPSHOT_LATEST - 1
+        u = replace(t, snapshot_max=snapshot)
+        self.tables[self.tables.index(t)] = u
+        return u
+
+    def remove_invisible(self, key_min: int, key_max: int) -> list:
+        """The tables Manifest.remove_invisible_tables removes, in its order
+        (manifest.zig:345-386 over ManifestLevel.iterator(.invisible, &.{},
+        .descending, range), manifest_level.zig:327-520): start at the last
+        table sharing the key_max of the first table whose key_max >= the
+        range's key_max (or at the last table), walk down; skip visible tables
+        and tables starting above the range; stop at the first invisible table
+        ending below it."""
+        n = len(self.tables)
+        if n == 0:
+            return []
+        kmax = [t.key_max for t in self.tables]
+        lb = next((i for i, k in enumerate(kmax) if k >= key_max), n)
+        if lb == n:
+            start = n - 1
+        else:
+            start = lb
+            while start + 1 < n and kmax[start + 1] == kmax[lb]:
+                start += 1
+        removed = []
+        for i in range(start, -1, -1):
+            t = self.tables[i]
+            if t.snapshot_max == SNAPSHOT_LATEST:
+                continue
+            if t.key_min > key_max:
+                continue
+            if t.key_max < key_min:
+                break
+            removed.append(t)
+        for t in removed:
+            self.tables.remove(t)
+        return removed
 
     def overlapping(self, key_min: int, key_max: int, max_tables: int):
         """tables_overlapping_with_key_range (manifest_level.zig:677-731)."""
@@ -225,25 +284,39 @@ class Tree:
         self.compactions = started
         return started
 
-    def apply(self, c: Compaction) -> None:
-        """Compaction.apply_to_manifest (compaction.zig:939-973) and the
-        remove_invisible_tables calls of Tree.compact_end (tree.zig:905-960)."""
+    def apply(self, c: Compaction, log=None) -> None:
+        """Compaction.apply_to_manifest (compaction.zig:939-973) then the
+        remove_invisible_tables calls of Tree.compact_end (tree.zig:905-953),
+        appending each event to the manifest log `log` (manifest.zig:233-386):
+        updates of the inputs (A at level_b - 1, then every B table), inserts
+        of the outputs or the move's update at level_b, removes of the inputs."""
         snap_max = snapshot_max_for_table_input(c.op_min)
         lb = self.levels[c.level_b]
+        tid, ks = self.spec.tree_id, self.spec.key_size
+
+        def emit(t: TableInfo, level: int, event: int) -> None:
+            if log is not None:
+                log.append(t.encode(tid, level, event, ks))
+
         if c.move:
             la = self.levels[c.level_b - 1]
-            la.tables.remove(c.table_a)
-            lb.insert(replace(c.table_a, level=c.level_b))
-            return
-        if c.table_a is not None:
-            la = self.levels[c.level_b - 1]
-            la.tables[la.tables.index(c.table_a)] = replace(c.table_a, snapshot_max=snap_max)
-        for t in c.range_b[2]:
-            lb.tables[lb.tables.index(t)] = replace(t, snapshot_max=snap_max)
-        for t in c.outputs:
-            lb.insert(t)
-        for level in {c.level_b, c.level_b - 1} - {-1}:
-            self.levels[level].tables = [t for t in self.levels[level].tables if t.snapshot_max == SNAPSHOT_LATEST]
+            la.tables.remove(c.table_a)               # no remove event (manifest.zig:301-308)
+            moved = replace(c.table_a, level=c.level_b)
+            lb.insert(moved)
+            emit(moved, c.level_b, EVENT_UPDATE)
+        else:
+            if c.table_a is not None:
+                emit(self.levels[c.level_b - 1].set_snapshot_max(c.table_a, snap_max), c.level_b - 1, EVENT_UPDATE)
+            for t in c.range_b[2]:
+                emit(lb.set_snapshot_max(t, snap_max), c.level_b, EVENT_UPDATE)
+            for t in c.outputs:
+                lb.insert(t)
+                emit(t, c.level_b, EVENT_INSERT)
+        kmin, kmax = c.range_b[0], c.range_b[1]
+        levels = [c.level_b] if c.table_a is None else [c.level_b] + ([c.level_b - 1] if c.level_b > 0 else [])
+        for level in levels:
+            for t in self.levels[level].remove_invisible(kmin, kmax):
+                emit(t, level, EVENT_REMOVE)
 
 
 class Forest:
@@ -257,7 +330,9 @@ class Forest:
              "transfers.amount", "transfers.pending_id", "transfers.user_data_128", "transfers.user_data_64",
              "transfers.user_data_32", "transfers.timeout", "transfers.ledger", "transfers.code"]
 
-    def __init__(self, executor, block_count: int, cluster: int = 0):
+    def __init__(self, executor, block_count: int, cluster: int = 0, manifest_log: bool = True,
+                 block_size: int = 1 << 20):
+        from .manifest import ManifestLog
         self.executor = executor
         self.free_set = FreeSet(block_count)
         self.trees = {name: Tree(trees.BY_NAME[name]) for name in self.ORDER}
@@ -265,6 +340,10 @@ class Forest:
         self.pending = None       # (batch handle, [Compaction]) of the running half-bar
         self.history: list = []   # per half-bar: (op, [Compaction]) once applied
         self.swaps: list = []     # per bar end: [(tree, values, sorted)] made immutable
+        # The forest's manifest log (forest.zig:197-204), its blocks closed by
+        # the executor's store (the GPU grid, or the oracle in tests).
+        self.manifest_log = ManifestLog(executor.manifest_store(cluster), self.free_set, block_size) \
+            if manifest_log and hasattr(executor, "manifest_store") else None
 
     def put(self, name: str, values: np.ndarray) -> None:
         spec = self.trees[name].spec
@@ -280,6 +359,8 @@ class Forest:
             for name in self.ORDER:
                 for c in self.trees[name].start_half_bar(op, self.free_set):
                     started.append((name, c))
+            if self.manifest_log is not None:  # after the grooves (forest.zig:323-331)
+                self.manifest_log.compact(op)
             jobs = [(name, c) for name, c in started if not c.move]
             handle = self.executor.submit(jobs, self.cluster) if jobs else None
             self.pending = (handle, started)
@@ -288,17 +369,27 @@ class Forest:
             if handle is not None:
                 self.executor.wait(handle, [c for _, c in started if not c.move])
             odd = beat == BAR - 1
-            for name, c in started:  # immutable compactions first (tree.zig:905-927)
-                if c.table_a is None:
-                    self.trees[name].apply(c)
-                    self.trees[name].immutable_flushed = True
-                    self.executor.flushed(name)
-            for name, c in started:
+            for name, c in started:  # the blocks each compaction wrote
                 if not c.move:
                     self.free_set.acquire(c.addresses[:c.result.block_count])
+            # Grooves' compact_end in forest order, each tree's immutable
+            # compaction first, then its level compactions (tree.zig:876-953).
+            log = self.manifest_log
+            for name in self.ORDER:
+                mine = [c for n, c in started if n == name]
+                for c in mine:
+                    if c.table_a is None:
+                        self.trees[name].apply(c, log)
+                        self.trees[name].immutable_flushed = True
+                        self.executor.flushed(name)
+                for c in mine:
+                    if c.table_a is not None:
+                        self.trees[name].apply(c, log)
+            for name, c in started:
+                if not c.move:
                     self.free_set.forfeit()
-                if c.table_a is not None:
-                    self.trees[name].apply(c)
+            if log is not None and beat in (HALF - 1, BAR - 1):
+                log.compact_end()
             assert odd or not any(c.table_a is None for _, c in started)
             self.history.append((op, started))
             self.pending = None
@@ -309,6 +400,12 @@ class Forest:
             # TableMemory.sort skips a table whose puts arrived in key order
             # (table_memory.zig:110-150): only the others are sorted.
             self.executor.swap([name for name in swapped if not self.trees[name].immutable_sorted])
+
+    def checkpoint_manifest(self) -> None:
+        """ManifestLog.checkpoint (manifest_log.zig:767-781) at the end of a
+        replay: the partial block is closed, so every event is in a block."""
+        if self.manifest_log is not None:
+            self.manifest_log.checkpoint()
 
     def run(self, load_ops, progress=None) -> None:
         """Commit every op of a workload: its puts, then Forest.compact(op)."""
@@ -361,6 +458,10 @@ class GridExecutor:
         self.record: list = []
         self.archive: list = []
         self.puts_bytes = 0
+
+    def manifest_store(self, cluster: int):
+        from .manifest import GridManifestStore
+        return GridManifestStore(self.grid, cluster, self.record if self.recording else None)
 
     def _mem(self, name: str):
         if name not in self.mutable:
@@ -417,6 +518,9 @@ class GridExecutor:
         handle.wait()
         for i, c in enumerate(compactions):
             r, infos = handle.result(i)
+            if r.status != 0:  # a block error or invariant is never applied to the manifest
+                from .abi import TbcError
+                raise TbcError(r.status, f"compaction {i} ({c.tree.name}, level_b {c.level_b})")
             c.result = r
             c.outputs = [TableInfo.decode(raw, c.tree.key_size) for raw in infos]
         handle.release()

@@ -14,6 +14,8 @@ from dataclasses import dataclass
 import numpy as np
 
 SNAPSHOT_LATEST = (1 << 64) - 1  # lsm.snapshot_latest (manifest.zig:43)
+# schema.ManifestNode.Event (schema.zig:511-516)
+EVENT_INSERT, EVENT_UPDATE, EVENT_REMOVE = 1, 2, 3
 
 
 @dataclass(frozen=True)
@@ -40,6 +42,29 @@ class TableInfo:
                    value_count=int.from_bytes(b[120:124], "little"),
                    tree_id=int.from_bytes(b[124:126], "little"),
                    level=b[126] & 0x3f)
+
+    @staticmethod
+    def event_of(raw) -> int:
+        """The label's event (schema.zig:518-530) of an encoded TableInfo."""
+        return int(np.asarray(raw, dtype=np.uint8)[126]) >> 6
+
+    def encode(self, tree_id: int, level: int, event: int, key_size: int) -> np.ndarray:
+        """TreeTableInfo.encode (manifest.zig:121-149) into schema.ManifestNode.TableInfo
+        (schema.zig:489-509): keys zero-padded to 32 bytes, label = level | event << 6
+        (packed struct(u8) {level: u6, event: Event}, schema.zig:518-530)."""
+        assert 0 < tree_id and self.value_count > 0 and 0 <= level < 64 and event in (EVENT_INSERT, EVENT_UPDATE,
+                                                                                        EVENT_REMOVE)
+        b = bytearray(128)
+        b[0:key_size] = self.key_min.to_bytes(key_size, "little")
+        b[32:32 + key_size] = self.key_max.to_bytes(key_size, "little")
+        b[64:80] = self.checksum.to_bytes(16, "little")
+        b[96:104] = self.address.to_bytes(8, "little")
+        b[104:112] = self.snapshot_min.to_bytes(8, "little")
+        b[112:120] = self.snapshot_max.to_bytes(8, "little")
+        b[120:124] = self.value_count.to_bytes(4, "little")
+        b[124:126] = tree_id.to_bytes(2, "little")
+        b[126] = level | event << 6
+        return np.frombuffer(bytes(b), dtype=np.uint8)
 
     def ref(self) -> tuple:
         """(index address, index checksum, value count): a tbc_table_ref."""
