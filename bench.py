@@ -47,7 +47,7 @@ class Workload:
     memtables as one contiguous array (plus the unsorted copy they are
     re-landed from each step when the config sorts them)."""
 
-    def __init__(self, eng: Engine, config: int, job_ids: list, bs: int):
+    def __init__(self, eng: Engine, config: int, job_ids: list, bs: int, keep_host: bool = True):
         self.config = config
         self.bs = bs
         self.jobs, self.bufs, self.specs = [], [], []
@@ -104,22 +104,75 @@ class Workload:
             base_addr += reservation
             self.jobs.append(Job(spec, segs_a, segs_b, js.a_immutable, js.drop_tombstones, js.level_b, 0xA5A5, 48,
                                  addrs, out, flags=abi.COMPACTION_UNIQUE_KEYS if js.unique_keys else 0))
-            self.specs.append(js)
-            self.bufs.append(out)
             self.input_values += js.input_values
             self.input_bytes += js.input_bytes
+            if not keep_host:  # the bench needs only the shape: free the host copies as it goes
+                js = configs.JobSpec(js.tree, js.a[:0], js.a_immutable, js.a_unsorted, [], js.drop_tombstones,
+                                     js.level_b, js.unique_keys)
+            self.specs.append(js)
+            self.bufs.append(out)
             del js
 
-    def step(self, eng: Engine):
-        """One step: land + sort the bar's memtables (config 3), then the
-        compaction batch; returns the completed batch."""
+    def submit(self, eng: Engine):
+        """Land + sort the bar's memtables (config 3), then submit the
+        compaction batch (no wait)."""
         for dst, src, n in self.landings:
             eng.copy_device_async(dst, src, n)
         if self.sorts:
             eng.sort_values_batch(self.sorts)
-        b = eng.submit(self.jobs)
+        return eng.submit(self.jobs)
+
+    def step(self, eng: Engine):
+        """One step; returns the completed batch."""
+        b = self.submit(eng)
         b.wait()
         return b
+
+
+class SplitPart:
+    """This rank's key range of ONE job split across all ranks (split.py,
+    SURVEY §8(e)2): splitters from the job's data-block first keys (identical
+    on every rank, no communication), only this rank's range of A and B
+    staged, and per step compact_split — phase 1 values-only, all-gathers of
+    the survivor counts and table heads (RCCL over xGMI with the nccl
+    backend), phase 2 re-blocking the tables this rank owns."""
+
+    def __init__(self, eng: Engine, js, gid: int, rank: int, world: int, exchange, bs: int):
+        from tigerbeetle_amd import split, workloads
+        from tigerbeetle_amd.engine import stage_blocks
+        self.spec, self.gid, self.rank, self.exchange = js.tree, gid, rank, exchange
+        lay = eng.layout(js.tree)
+        vcm = lay.block_value_count_max
+        a = js.a
+        b_all = np.concatenate(js.b_tables) if js.b_tables else np.zeros((0, js.tree.value_size), np.uint8)
+        side_a = split.BlockedSide.from_values(workloads.keys_of(a, js.tree), len(a), vcm)
+        side_b = split.BlockedSide.from_values(workloads.keys_of(b_all, js.tree), len(b_all), vcm)
+        self.cuts = split.block_cuts(side_a, side_b, split.block_splitters(side_a, side_b, world))
+        (a0, b0), (a1, b1) = self.cuts[rank], self.cuts[rank + 1]
+        a_mine, b_mine = a[a0:a1], b_all[b0:b1]
+        self.bufs = []
+        if js.a_immutable:
+            abuf = eng.upload(a_mine) if len(a_mine) else None
+            segs_a = [(abuf.ptr, len(a_mine))] if abuf else []
+            if abuf:
+                self.bufs.append(abuf)
+        else:
+            abuf, segs_a = stage_blocks(eng, [workloads.split_blocks(a_mine, vcm)], js.tree.value_size, bs)
+            self.bufs.append(abuf)
+        bbuf, segs_b = stage_blocks(eng, [workloads.split_blocks(b_mine, vcm)], js.tree.value_size, bs)
+        self.bufs.append(bbuf)
+        reservation = (len(js.b_tables) + 1) * lay.data_block_count_max + len(js.b_tables) + 1
+        self.job = Job(js.tree, segs_a, segs_b, js.a_immutable, js.drop_tombstones, js.level_b, 0xA5A5, 48,
+                       np.arange(1, reservation + 1, dtype=np.uint64), None)
+        self.input_bytes = split.staged_bytes(self.cuts, rank, js.tree.value_size)
+        self.scratch: dict = {}
+        self.result = None
+
+    def run(self, eng: Engine, before_phase2=None):
+        from tigerbeetle_amd import split
+        self.result = split.compact_split(eng, self.job, self.cuts, self.exchange, self.rank, staged=True,
+                                          scratch=self.scratch, before_phase2=before_phase2)
+        return self.result
 
 
 class ReplayWorkload:
@@ -362,6 +415,9 @@ def main() -> None:
                     help="config 1: transfers of the benchmark load (default: its 10M)")
     ap.add_argument("--jobs", type=int, default=None, help="jobs per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="config 5: BASELINE's 1B values (216 jobs) divided over the GPUs (strong scaling)")
+    ap.add_argument("--no-split", action="store_true", help="config 4 at N > 1: shard whole jobs only")
     args = ap.parse_args()
     njobs = args.jobs or configs.DEFAULT_JOBS.get(args.config, 1)
 
@@ -386,13 +442,41 @@ def main() -> None:
     if args.config == 1:
         return main_config1(args, eng, rank, world, local, dist, backend, bs)
     # Weak scaling: njobs jobs per GPU; the global job set is sharded by
-    # input bytes (LPT, shard.py), no data-path collective.
-    plan = plan_shards([configs.job_bytes(args.config, j) for j in range(njobs * world)], world)
-    wl = Workload(eng, args.config, plan[rank], bs)
+    # input bytes (LPT, shard.py), no data-path collective. --strong (config
+    # 5): BASELINE's 1B values (216 jobs) fixed and divided over the ranks.
+    # Config 4 at N > 1 splits its largest pre-sorted job across all ranks
+    # by key range (SplitPart: the all-gathers run inside the timed step).
+    total_jobs = configs.STRONG_JOBS[args.config] if args.strong else njobs * world
+    job_ids = list(range(total_jobs))
+    split_id = None
+    if args.config == 4 and world > 1 and not args.no_split:
+        split_id = max((j for j in job_ids if configs.presorted(args.config, j)),
+                       key=lambda j: configs.job_bytes(args.config, j))
+        job_ids.remove(split_id)
+    by_bytes = [configs.job_bytes(args.config, j) for j in job_ids]
+    plan = plan_shards(by_bytes, world)
+    mine = [job_ids[i] for i in plan[rank]]
+    njobs = len(mine) if args.strong else njobs
+    wl = Workload(eng, args.config, mine, bs, keep_host=False)
+    part = None
+    if split_id is not None:
+        from tigerbeetle_amd.split import TorchExchange
+        part = SplitPart(eng, configs.GENERATORS[args.config](split_id), split_id, rank, world,
+                         TorchExchange(dist, f"cuda:{local}" if backend == "nccl" else None), bs)
+        wl.input_bytes += part.input_bytes
     eng.synchronize()
 
+    def step():
+        if part is None:
+            return wl.step(eng)
+        held = []
+        part.run(eng, before_phase2=lambda: held.append(wl.submit(eng)))
+        b = held[0] if held else wl.submit(eng)
+        b.wait()
+        return b
+
     for _ in range(args.warmup):
-        wl.step(eng).release()
+        step().release()
 
     def barrier():
         eng.synchronize()
@@ -409,7 +493,7 @@ def main() -> None:
     ktimes: dict = {}
     marks = []
     for _ in range(args.steps):
-        b = wl.step(eng)
+        b = step()
         marks.append(time.perf_counter())
         for k, v in b.kernel_times().items():
             ktimes[k] = ktimes.get(k, 0.0) + v
@@ -420,8 +504,10 @@ def main() -> None:
         print("step ms:", " ".join(f"{(b - a) * 1e3:.2f}" for a, b in zip([t0] + marks, marks)), file=sys.stderr)
     dt = time.perf_counter() - t0
     # Check the last step's results: every job OK, and output shape for the bytes.
-    b = wl.step(eng)
+    b = step()
     out_values = data_blocks = tables = index_bytes = 0
+    if part is not None:
+        assert part.result is not None and (part.result.result is None or part.result.result.status == 0)
     for i, js in enumerate(wl.specs):
         r, _ = b.result(i)
         assert r.status == 0, (i, r.status)
@@ -475,13 +561,14 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic (seeded tables, BASELINE config {args.config}: tigerbeetle_amd/configs.py)",
         "config": {"workload": configs.DESCRIPTION[args.config], "baseline_config": args.config,
                    "jobs_per_gpu": njobs, "input_bytes_per_gpu": wl.input_bytes, "block_size": bs,
-                   "parallelism": f"shard-by-job x{world}"},
+                   "parallelism": f"shard-by-job x{world}" + (f" + key-range split of job {split_id}"
+                                                                if split_id is not None else "")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -277,7 +277,21 @@ def job_bytes(config: int, job: int) -> int:
     return 5 * TABLE_T * trees.BY_NAME[FOREST_DEEP[k - len(FOREST_BAR)]].value_size
 
 
+def presorted(config: int, job: int) -> bool:
+    """Whether the job's A needs no device sort first (a key-range split
+    stages sorted ranges)."""
+    if config == 3:
+        return job % 7 == 6
+    if config == 4:
+        k = job % FOREST_JOBS
+        return k >= len(FOREST_BAR) or FOREST_BAR[k] in ("transfers.id", "transfers.timestamp")
+    return True
+
+
 GENERATORS = {2: config2_job, 3: config3_job, 4: config4_job, 5: config5_job}
+# --strong: the whole problem BASELINE states, divided over the GPUs (config 5:
+# 216 x 4.7M = 1.02B Account values).
+STRONG_JOBS = {2: 28, 3: 28, 4: FOREST_JOBS, 5: 216}
 DEFAULT_JOBS = {2: 28, 3: 28, 4: FOREST_JOBS, 5: 27}
 DESCRIPTION = {
     2: "transfers.id L0->L1 compaction, 28 jobs x (1 A + 8 B tables) per GPU, 64M u128 keys, 1 MiB blocks",

@@ -350,8 +350,15 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
         return TBC_ERR_OUT_OF_MEMORY;
     }
     bool ok = true;
+    // Tails (chains, index blocks, input checks, results) at the highest
+    // stream priority: their workgroups are dispatched ahead of the next
+    // batch's front on the engine stream, so a tail's short kernels (index
+    // blocks, checks) are not starved behind a merge that fills the chip.
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+    static const bool flat = getenv("TBC_FLAT_PRIORITY") != nullptr; // A/B measurement only
     for (int t = 0; ok && t < tbc_engine::kTails; t++)
-        ok = hipStreamCreateWithFlags(&e->tail[t], hipStreamNonBlocking) == hipSuccess &&
+        ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, flat ? 0 : prio_greatest) == hipSuccess &&
              hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
@@ -1165,7 +1172,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         d.address_count = c.address_count;
         d.out_blocks = grid ? nullptr : (uint8_t *)c.output_blocks;
         d.grid_base = grid ? c.grid->base : nullptr;
-        d.tile_count = (uint32_t)((n + kMergeTile - 1) / kMergeTile);
+        d.merge_tile = kMergeTile; // the staged merge's tile is set below, with the regime
         d.dblock_max = (uint32_t)db_max;
         d.table_max = (uint32_t)tables_max;
         d.job_index = i;
@@ -1173,12 +1180,28 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         addr_words += c.address_count;
         order[i] = i;
     }
+    // The staged merge (merge.hip k_merge_staged: values read once into
+    // registers, written straight to their output slots) serves every batch
+    // whose bodies are not built beside their chains: grid batches, pipelined
+    // groups, VALUES_ONLY and the throughput regime. TBC_NO_STAGED=1 (A/B
+    // measurement only) keeps the mask merge + k_assemble there.
+    uint64_t dblocks_all = 0;
+    for (uint32_t i = 0; i < count; i++) dblocks_all += hj[i].dblock_max;
+    static const bool no_staged = getenv("TBC_NO_STAGED") != nullptr;
+    const bool staged = !no_staged && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
+                                       (dblocks_all + 1) / 2 > fused_max_chain_waves());
+    for (uint32_t i = 0; i < count; i++) {
+        JobDesc &d = hj[i];
+        if (staged) d.merge_tile = staged_tile(d.value_size);
+        const uint64_t n = (uint64_t)d.a.n + d.b.n;
+        d.tile_count = (uint32_t)((n + d.merge_tile - 1) / d.merge_tile);
+    }
     // Group jobs by key kind (one kernel instantiation per kind) and assign
     // batch-wide bases in that order.
     std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hj[x].key_kind < hj[y].key_kind; });
     uint64_t all_tiles = 0;
     for (uint32_t i = 0; i < count; i++) all_tiles += hj[i].tile_count;
-    if (!ensure_masks(e, all_tiles * (2 * kMergeTile / 64))) {
+    if (!staged && !ensure_masks(e, all_tiles * (2 * kMergeTile / 64))) {
         delete b;
         return TBC_ERR_OUT_OF_MEMORY;
     }
@@ -1246,18 +1269,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     uint32_t *d_ready = d_block_tile + dblocks;
     uint64_t *d_lookback = (uint64_t *)(uintptr_t)align_up((uint64_t)(uintptr_t)(d_ready + dblocks + 2), 8);
     uint32_t *d_ticket = (uint32_t *)(d_lookback + tiles);
-    // The merge can write the bodies itself (tiles take their output offsets
-    // by look-back, merge.hip k_merge_tile<KIND, true>) instead of
-    // k_assemble walking its masks afterwards. Measured on MI355X it is not
-    // a win where it applies (config 5 alone 16.1 -> 15.1 ms, but grouped
-    // 14.3 -> 20.8 ms and the config 1 replay 75 -> 79 ms: the look-back
-    // serialises tiles that then copy), so it is off unless asked for
-    // (TBC_MERGE_BODIES=1, A/B measurement; parity-tested either way).
-    static const bool merge_bodies_env = getenv("TBC_MERGE_BODIES") != nullptr;
-    const bool throughput = (uint64_t)(dblocks + 1) / 2 > fused_max_chain_waves();
-    const bool merge_bodies = merge_bodies_env && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
-                                                   throughput);
-    uint64_t *m_lb = merge_bodies ? d_lookback : nullptr;
+    const bool merge_bodies = staged;
+    uint64_t *m_lb = staged ? d_lookback : nullptr;
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
     b->h_results = (JobResultDev *)(hbase + sz_in);

@@ -58,7 +58,7 @@ __device__ __forceinline__ const uint8_t *elem_ptr(const Stream &s, uint32_t seg
 }
 
 // --------------------------------------------------------------------------
-// Merge-path partition: for every tile boundary d = t * kMergeTile, the number
+// Merge-path partition: for every tile boundary d = t * merge_tile, the number
 // i of A elements among the first d merged elements, plus the segments that
 // hold A[max(i-1, 0)] and B[min(d-i, nb-1)] (where the tile starts reading).
 // --------------------------------------------------------------------------
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int 
     if (phase_skips(j, res, phase)) return;
     const uint32_t t = gsplit - j.split_base;
     const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
-    const uint32_t d = (uint64_t)t * kMergeTile < n ? t * kMergeTile : n;
+    const uint32_t d = (uint64_t)t * j.merge_tile < n ? t * j.merge_tile : n;
     uint32_t lo;
     switch (j.key_kind) {
     case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
@@ -207,27 +207,16 @@ template <int KL> struct TileShared {
     uint32_t wave_sums[kMergeThreads / 64];
 };
 
-// Look-back words of the assembling merge (ASM): flag in the top two bits,
-// survivors (aggregate, or inclusive prefix of the job's tiles) below.
-constexpr uint64_t kMlbAggregate = 1ull << 62, kMlbPrefix = 2ull << 62, kMlbCount = (1ull << 62) - 1;
-
-template <int KIND, bool ASM>
+template <int KIND>
 __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *order, uint32_t order_offset,
                                            const SplitDesc *splits, uint64_t *status, uint64_t *masks,
-                                           uint64_t *lookback, uint32_t *ticket, uint32_t *ready,
                                            const JobResultDev *res, uint32_t phase, uint32_t slot) {
     constexpr int KL = KeyLimbs<KIND>::value;
     __shared__ TileShared<KL> sh;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    // ASM: tiles are taken in ticket order (the order table interleaves the
-    // jobs tile by tile), so every tile a tile looks back on belongs to a
-    // workgroup that is running or done.
-    __shared__ uint32_t s_ticket;
-    if (ASM && tid == 0) s_ticket = atomicAdd(ticket, 1u);
-    if (ASM) __syncthreads();
-    const TileRef ref = order[order_offset + (ASM ? s_ticket : slot)];
+    const TileRef ref = order[order_offset + slot];
     const JobDesc &j = jobs[ref.job];
-    if (!ASM && phase_skips(j, res, phase)) return; // (speculating batches never assemble in the merge)
+    if (phase_skips(j, res, phase)) return;
     const uint32_t t = ref.tile;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * kMergeTile;
@@ -386,14 +375,9 @@ __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *o
         aw |= __shfl_xor(aw, o, 64);
     }
     uint64_t *m = masks + (size_t)(j.tile_base + t) * (2 * kMaskWords);
-    __shared__ uint64_t s_m[2 * kMaskWords];
     if (tid % kThreadsPerWord == 0) {
         gst<uint64_t>(m + tid / kThreadsPerWord, sw);
         gst<uint64_t>(m + kMaskWords + tid / kThreadsPerWord, aw);
-        if (ASM) {
-            s_m[tid / kThreadsPerWord] = sw;
-            s_m[kMaskWords + tid / kThreadsPerWord] = aw;
-        }
     }
     uint32_t sum = __builtin_popcount(sbits);
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
@@ -402,119 +386,311 @@ __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *o
     uint32_t cnt = 0;
     for (uint32_t w = 0; w < kMergeThreads / 64; w++) cnt += sh.wave_sums[w];
     if (tid == 0) gst<uint64_t>(status + j.tile_base + t, (uint64_t)cnt);
-    if constexpr (ASM) {
-        // The job's survivors before this tile: decoupled look-back, wave 0
-        // reading 64 predecessors per round trip (nearest first; before the
-        // job's first tile reads as a prefix of 0).
-        __shared__ uint32_t s_excl;
-        if (tid < 64) {
-            uint64_t *lb = lookback + j.tile_base;
-            if (tid == 0) __hip_atomic_store(&lb[t], kMlbAggregate | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t excl = 0;
-            int64_t top = (int64_t)t - 1;
-            for (uint32_t spins = 0;;) {
-                const int64_t idx = top - (int64_t)lane;
-                const uint64_t v = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                            : kMlbPrefix;
-                const uint64_t fl = v >> 62;
-                const uint64_t pre = __ballot(fl == 2);
-                const uint32_t stop = pre ? __builtin_ctzll(pre) : 64u; // nearest prefix
-                const bool mine = lane <= stop;
-                if (__ballot(mine && fl == 0)) { // a tile up to the prefix has not published yet
-                    if (++spins > (1u << 18)) break; // bounded (a broken invariant, not a hang)
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                uint64_t c = mine ? (v & kMlbCount) : 0;
-                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                excl += c;
-                if (stop < 64) break;
-                top -= 64;
-            }
-            if (tid == 0) {
-                __hip_atomic_store(&lb[t], kMlbPrefix | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_excl = (uint32_t)excl;
-            }
-        }
-        // Survivors into their output slots (k_assemble's walk, masks from LDS).
-        __shared__ uint32_t s_pre[3][kMaskWords + 1]; // survivors, A taken, B taken before word w
-        __shared__ uint64_t s_src[kMergeThreads / 64][64], s_dst[kMergeThreads / 64][64];
-        const uint32_t wv = tid >> 6;
-        const uint64_t lt = (1ull << lane) - 1;
-        auto valid_of = [&](uint32_t w) -> uint64_t {
-            const uint32_t pos0 = d0 + 64 * w;
-            return pos0 >= n ? 0ull : (n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1));
-        };
-        if (tid < kMaskWords) {
-            s_pre[0][tid + 1] = __builtin_popcountll(s_m[tid]);
-            s_pre[1][tid + 1] = __builtin_popcountll(s_m[kMaskWords + tid]);
-            s_pre[2][tid + 1] = __builtin_popcountll(valid_of(tid) & ~s_m[kMaskWords + tid]);
-        }
-        __syncthreads();
-        if (tid < 3) {
-            uint32_t acc = 0;
-            s_pre[tid][0] = 0;
-            for (uint32_t w = 1; w <= kMaskWords; w++) {
-                acc += s_pre[tid][w];
-                s_pre[tid][w] = acc;
-            }
-        }
-        __syncthreads();
-        const uint32_t out0 = s_excl;
-        const uint32_t vcm = j.vcm;
-        SegCursor ca, cb;
-        ca.init(j.a, s0.seg_a);
-        cb.init(j.b, s0.seg_b);
-        const uint32_t cpv_log = __builtin_ctz(vs >> 4);
-        for (uint32_t w = wv; w < kMaskWords; w += kMergeThreads / 64) {
-            if (d0 + 64 * w >= n) break;
-            const uint64_t smk = s_m[w], amk = s_m[kMaskWords + w];
-            const uint32_t ns = __builtin_popcountll(smk);
-            if (ns == 0) continue;
-            const uint64_t valid = valid_of(w);
-            const uint32_t ab = i0 + s_pre[1][w], bb = j0 + s_pre[2][w];
-            ca.advance(ab);
-            cb.advance(bb);
-            if ((smk >> lane) & 1) {
-                const uint32_t r = __builtin_popcountll(smk & lt);
-                const uint32_t o = out0 + s_pre[0][w] + r;
-                const uint8_t *src = ((amk >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(amk & lt), vs)
-                                                         : cb.elem(bb + __builtin_popcountll(valid & ~amk & lt), vs);
-                const uint32_t k = o / vcm;
-                s_src[wv][r] = (uint64_t)(uintptr_t)src;
-                s_dst[wv][r] = (uint64_t)(uintptr_t)(block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize +
-                                                     (size_t)(o - k * vcm) * vs);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            copy_staged(s_src[wv], s_dst[wv], ns, cpv_log);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        }
-        // Survivors landed per data block (the chains check them).
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t o = out0;
-            const uint32_t end = out0 + cnt;
-            while (o < end) {
-                const uint32_t k = o / vcm;
-                const uint32_t e = (k + 1) * vcm < end ? (k + 1) * vcm : end;
-                __hip_atomic_fetch_add(ready + j.dblock_base + k, e - o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                o = e;
-            }
-        }
-    }
 }
 
 // One merge tile per workgroup.
-template <int KIND, bool ASM>
+template <int KIND>
 __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *jobs, const TileRef *order,
                                                               uint32_t order_offset, const SplitDesc *splits,
-                                                              uint64_t *status, uint64_t *masks, uint64_t *lookback,
-                                                              uint32_t *ticket, uint32_t *ready,
+                                                              uint64_t *status, uint64_t *masks,
                                                               const JobResultDev *res, uint32_t phase) {
-    merge_tile<KIND, ASM>(jobs, order, order_offset, splits, status, masks, lookback, ticket, ready, res, phase,
-                          blockIdx.x);
+    merge_tile<KIND>(jobs, order, order_offset, splits, status, masks, res, phase, blockIdx.x);
+}
+
+// --------------------------------------------------------------------------
+// Staged merge (batches whose bodies are not built beside their chains:
+// grid batches, pipelined job groups, the throughput regime, VALUES_ONLY):
+// a tile's input values are read ONCE, into registers (up to 64 KiB per
+// workgroup, 16-byte chunks, lane groups per value: coalesced), their keys
+// go to LDS, the survivor rules decide each merged position, the tile takes
+// its output offset by decoupled look-back (tiles in ticket order, so every
+// tile looked back on is running or done), and the surviving values go from
+// registers straight to their output slots. R + W of HBM traffic, where
+// merge + k_assemble moved R + 2 W (the values re-read after the masks).
+// The last tile of a job writes its results (write_blocks' shape,
+// compaction.zig:806-850); every tile counts its survivors into the data
+// blocks they land in (checked by the chain kernel).
+// --------------------------------------------------------------------------
+constexpr uint32_t kStagedThreads = 256;
+constexpr uint32_t kStagedChunks = 16;   // 16-byte chunks per thread: 64 KiB of values per tile
+constexpr uint32_t kStagedMaxTile = 1024;
+static_assert(kStagedThreads * kStagedChunks * 16 == 65536, "64 KiB of staged values");
+
+// Byte offset of key limb l in a value (keys.h load_key's order).
+template <int KIND> __device__ __forceinline__ uint32_t key_limb_off(int l, uint32_t ts) {
+    if constexpr (KIND == kKeyTimestamp) return ts;
+    else if constexpr (KIND == kKeyIdU128) return 8u * l;
+    else if constexpr (KIND == kKeyCompositeU64) return l == 0 ? 8u : 0u;
+    else return l == 0 ? 16u : 8u * (l - 1);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kStagedThreads) void k_merge_staged(const JobDesc *jobs, const TileRef *order,
+                                                                 uint32_t order_offset, const SplitDesc *splits,
+                                                                 uint64_t *lookback, uint32_t *ticket,
+                                                                 uint32_t *ready, JobResultDev *res) {
+    constexpr int KL = KeyLimbs<KIND>::value;
+    __shared__ uint64_t s_key[KL][kStagedMaxTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
+    __shared__ uint8_t s_tomb[kStagedMaxTile + 4];
+    __shared__ uint32_t s_dst[kStagedMaxTile];         // per slot: tile-local output rank, or ~0
+    __shared__ uint32_t s_seg_pre[2][kSegWindow + 1];
+    __shared__ uint64_t s_seg_ptr[2][kSegWindow];
+    __shared__ uint32_t s_wsum[kStagedThreads / 64];
+    __shared__ uint32_t s_ticket, s_excl;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_ticket = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const TileRef ref = order[order_offset + s_ticket];
+    const JobDesc &j = jobs[ref.job];
+    const uint32_t t = ref.tile, T = j.merge_tile;
+    const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
+    const uint32_t d0 = t * T, d1 = (d0 + T) < n ? d0 + T : n;
+    const SplitDesc s0 = splits[j.split_base + t];
+    const uint32_t i0 = s0.i, i1 = splits[j.split_base + t + 1].i;
+    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t na = i1 - i0, nb = j1 - j0, slots = na + nb;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
+    const uint32_t cpv_log = __builtin_ctz(vs >> 4);
+    const bool immutable = j.a_immutable != 0, secondary = j.usage == 1, drop = j.drop_tombstones != 0;
+    const uint32_t ea = na + 2;
+
+    if (tid < 2 * (kSegWindow + 1)) {
+        const uint32_t side = tid / (kSegWindow + 1), k = tid % (kSegWindow + 1);
+        const Stream &st = side == 0 ? j.a : j.b;
+        const uint32_t seg = (side == 0 ? s0.seg_a : s0.seg_b) + k;
+        s_seg_pre[side][k] = seg <= st.nseg && st.nseg ? gld<uint32_t>(st.seg_pre + seg) : 0xffffffffu;
+        if (k < kSegWindow) s_seg_ptr[side][k] = seg < st.nseg ? gld<uint64_t>(st.seg_ptr + seg) : 0;
+    }
+    __syncthreads();
+    // Element `idx` of stream `side` (inside the tile's segment window, or found globally).
+    auto elem = [&](uint32_t side, uint32_t idx) -> const uint8_t * {
+        uint32_t k = 0;
+        while (k + 1 < kSegWindow && s_seg_pre[side][k + 1] <= idx) k++;
+        if (k + 1 == kSegWindow && s_seg_pre[side][k + 1] <= idx) {
+            const Stream &st = side == 0 ? j.a : j.b;
+            return elem_ptr(st, seg_search(st, idx), idx, vs);
+        }
+        return (const uint8_t *)s_seg_ptr[side][k] + (size_t)(idx - s_seg_pre[side][k]) * vs;
+    };
+
+    // 1. Values into registers: chunk g = slot * cpv + c (16 bytes), thread
+    //    tid holds chunks tid + 256 r. A slot e < na is A[i0 + e], else B[j0 + e - na].
+    const uint32_t chunks = slots << cpv_log;
+    u32x4 v[kStagedChunks];
+#pragma unroll
+    for (uint32_t r = 0; r < kStagedChunks; r++) {
+        const uint32_t g = tid + kStagedThreads * r;
+        if (g < chunks) {
+            const uint32_t e = g >> cpv_log, c = g & ((1u << cpv_log) - 1);
+            const uint8_t *p = e < na ? elem(0, i0 + e) : elem(1, j0 + (e - na));
+            v[r] = gld<u32x4>(p + 16 * c);
+        }
+    }
+    // Boundary keys: A[i0 - 1], A[i1], B[j1] (max when absent).
+    if (tid < 3) {
+        Key<KL> k;
+#pragma unroll
+        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
+        uint32_t tb = 0, entry = 0;
+        if (tid == 0) {
+            entry = 0;
+            if (i0 >= 1) {
+                const uint8_t *p = elem_ptr(j.a, seg_search(j.a, i0 - 1), i0 - 1, vs);
+                k = load_key<KIND>(p, ts);
+                tb = load_tomb(p, ts);
+            }
+        } else if (tid == 1) {
+            entry = na + 1;
+            if (i1 < na_all) {
+                const uint8_t *p = elem_ptr(j.a, seg_search(j.a, i1), i1, vs);
+                k = load_key<KIND>(p, ts);
+                tb = load_tomb(p, ts);
+            }
+        } else {
+            entry = ea + nb;
+            if (j1 < nb_all) k = load_key<KIND>(elem_ptr(j.b, seg_search(j.b, j1), j1, vs), ts);
+        }
+#pragma unroll
+        for (int l = 0; l < KL; l++) s_key[l][entry] = k.l[l];
+        if (entry < ea) s_tomb[entry] = (uint8_t)tb;
+    }
+    // Keys (and A tombstones) of the staged slots, from the chunks that hold them.
+#pragma unroll
+    for (uint32_t r = 0; r < kStagedChunks; r++) {
+        const uint32_t g = tid + kStagedThreads * r;
+        if (g >= chunks) continue;
+        const uint32_t e = g >> cpv_log, c = g & ((1u << cpv_log) - 1);
+        const uint32_t entry = e < na ? e + 1 : ea + (e - na);
+#pragma unroll
+        for (int l = 0; l < KL; l++) {
+            const uint32_t o = key_limb_off<KIND>(l, ts);
+            if ((o >> 4) != c) continue;
+            uint64_t w = (o & 8) ? ((uint64_t)v[r].w << 32 | v[r].z) : ((uint64_t)v[r].y << 32 | v[r].x);
+            if (l == 0 && KIND != kKeyIdU128) w &= ~kTombstoneBit;
+            s_key[l][entry] = w;
+        }
+        if (e < na && (ts >> 4) == c) {
+            const uint32_t hi = (ts & 8) ? v[r].w : v[r].y;
+            s_tomb[entry] = (uint8_t)(hi >> 31);
+        }
+    }
+    __syncthreads();
+
+    auto entry_key = [&](uint32_t e) {
+        Key<KL> k;
+#pragma unroll
+        for (int l = 0; l < KL; l++) k.l[l] = s_key[l][e];
+        return k;
+    };
+    auto run_len = [&](uint32_t ia) { // run of equal keys ending at A[ia] (secondary-index dedup)
+        const Key<KL> k = entry_key(ia - i0 + 1);
+        uint32_t len = 1;
+        int64_t idx = (int64_t)ia - 1;
+        while (idx >= 0) {
+            Key<KL> kk;
+            if (idx >= (int64_t)i0 - 1) kk = entry_key((uint32_t)(idx - ((int64_t)i0 - 1)));
+            else kk = load_key<KIND>(elem_ptr(j.a, seg_search(j.a, (uint32_t)idx), (uint32_t)idx, vs), ts);
+            if (!key_eq(kk, k)) break;
+            len++;
+            idx--;
+        }
+        return len;
+    };
+
+    // 2. Survivor rules (merge_tile's), kPer merged positions per thread.
+    const uint32_t kPer = T / kStagedThreads; // 1, 2 or 4
+    const uint32_t dd = kPer * tid < slots ? kPer * tid : slots;
+    uint32_t a, b;
+    {
+        uint32_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key_le(entry_key(1 + mid), entry_key(ea + dd - 1 - mid))) lo = mid + 1;
+            else hi = mid;
+        }
+        a = lo;
+        b = dd - lo;
+    }
+    uint32_t slot_of[4], surv_bits = 0, mine = 0;
+    for (uint32_t k = 0; k < kPer; k++) {
+        slot_of[k] = ~0u;
+        if (dd + k >= slots) continue;
+        const bool take_a = a < na && (b >= nb || key_le(entry_key(1 + a), entry_key(ea + b)));
+        bool surv;
+        if (take_a) {
+            const uint32_t ia = i0 + a, e = a + 1;
+            const Key<KL> ka = entry_key(e);
+            bool dedup = true;
+            if (immutable) {
+                dedup = !((ia + 1 < na_all) && key_eq(entry_key(e + 1), ka));
+                if (dedup && secondary) dedup = (run_len(ia) & 1) != 0;
+            }
+            const bool eq_b = (b < nb || j1 < nb_all) && key_eq(entry_key(ea + b), ka);
+            surv = dedup && !(drop && s_tomb[e]) && !(secondary && eq_b);
+            slot_of[k] = a;
+            a++;
+        } else {
+            const Key<KL> kb = entry_key(ea + b);
+            bool a_exists = (i0 + a) >= 1 && key_eq(entry_key(a), kb);
+            if (a_exists && immutable && secondary) a_exists = (run_len(i0 + a - 1) & 1) != 0;
+            surv = !a_exists;
+            slot_of[k] = na + b;
+            b++;
+        }
+        surv_bits |= (surv ? 1u : 0u) << k;
+        mine += surv ? 1u : 0u;
+    }
+    // Tile-local ranks: exclusive scan of the per-thread survivor counts.
+    uint32_t incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t woff = 0, cnt = 0;
+    for (uint32_t w = 0; w < kStagedThreads / 64; w++) {
+        woff += w < wave ? s_wsum[w] : 0u;
+        cnt += s_wsum[w];
+    }
+    uint32_t rank = woff + incl - mine;
+    for (uint32_t k = 0; k < kPer; k++) {
+        if (slot_of[k] == ~0u) continue;
+        const bool sv = (surv_bits >> k) & 1u;
+        s_dst[slot_of[k]] = sv ? rank : ~0u;
+        rank += sv ? 1u : 0u;
+    }
+
+    // 3. The job's survivors before this tile: decoupled look-back, wave 0
+    //    reading 64 predecessors per round trip (nearest first).
+    constexpr uint64_t kAgg = 1ull << 62, kPre = 2ull << 62, kCnt = (1ull << 62) - 1;
+    if (wave == 0) {
+        uint64_t *lb = lookback + j.tile_base;
+        if (lane == 0) __hip_atomic_store(&lb[t], kAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t excl = 0;
+        int64_t top = (int64_t)t - 1;
+        for (uint32_t spins = 0;;) {
+            const int64_t idx = top - (int64_t)lane;
+            const uint64_t w = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kPre;
+            const uint64_t fl = w >> 62;
+            const uint64_t pre = __ballot(fl == 2);
+            const uint32_t stop = pre ? __builtin_ctzll(pre) : 64u; // nearest inclusive prefix
+            const bool in = lane <= stop;
+            if (__ballot(in && fl == 0)) { // a tile up to the prefix has not published yet
+                if (++spins > (1u << 22)) { // bounded: report instead of hanging
+                    if (lane == 0) gst<uint32_t>(&res[j.job_index].invariant, 0xbeefu);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint64_t c = in ? (w & kCnt) : 0;
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            excl += c;
+            if (stop < 64) break;
+            top -= 64;
+        }
+        if (lane == 0) {
+            __hip_atomic_store(&lb[t], kPre | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_excl = (uint32_t)excl;
+        }
+    }
+    __syncthreads();
+    const uint32_t out0 = s_excl, vcm = j.vcm;
+
+    // 4. Survivors from registers to their output slots.
+#pragma unroll
+    for (uint32_t r = 0; r < kStagedChunks; r++) {
+        const uint32_t g = tid + kStagedThreads * r;
+        if (g >= chunks) continue;
+        const uint32_t e = g >> cpv_log, c = g & ((1u << cpv_log) - 1);
+        const uint32_t dst = s_dst[e];
+        if (dst == ~0u) continue;
+        const uint32_t o = out0 + dst, k = o / vcm;
+        gst<u32x4>(block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(o - k * vcm) * vs + 16 * c, v[r]);
+    }
+    // Survivors landed per data block (the chain kernel checks them; the
+    // reader is a later kernel in stream order, so no release fence).
+    if (tid == 0) {
+        uint32_t o = out0;
+        const uint32_t end = out0 + cnt;
+        while (o < end) {
+            const uint32_t k = o / vcm;
+            const uint32_t e = (k + 1) * vcm < end ? (k + 1) * vcm : end;
+            __hip_atomic_fetch_add(ready + j.dblock_base + k, e - o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            o = e;
+        }
+        if (t + 1 == j.tile_count) { // the job's shape (k_tile_scan's, from the inclusive prefix)
+            const uint64_t total = (uint64_t)out0 + cnt;
+            const uint32_t db = (uint32_t)((total + vcm - 1) / vcm);
+            const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
+            JobResultDev &rr = res[j.job_index];
+            rr.value_count = total;
+            rr.data_block_count = db;
+            rr.table_count = tables;
+            rr.block_count = db + tables;
+        }
+    }
 }
 
 // The recomputation phase of a speculating batch: a small grid strides over
@@ -526,8 +702,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile_redo(const JobDesc
                                                                    const JobResultDev *res, uint32_t ntiles) {
     if (*(volatile const uint32_t *)jobs[0].spec_any == 0) return;
     for (uint32_t slot = blockIdx.x; slot < ntiles; slot += gridDim.x) {
-        merge_tile<KIND, false>(jobs, order, order_offset, splits, status, masks, nullptr, nullptr, nullptr, res, 1u,
-                                slot);
+        merge_tile<KIND>(jobs, order, order_offset, splits, status, masks, res, 1u, slot);
         __syncthreads();
     }
 }
@@ -607,13 +782,12 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
         hipLaunchKernelGGL((k_merge_tile_redo<KIND>), dim3(std::min<uint32_t>(ntiles, 1024)), dim3(kMergeThreads), 0,
                            s, d_jobs, d_order, tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_res, ntiles);
     else if (ntiles && d_lookback)
-        hipLaunchKernelGGL((k_merge_tile<KIND, true>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
-                           tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket + KIND,
-                           d_ready, d_res, phase);
+        hipLaunchKernelGGL((k_merge_staged<KIND>), dim3(ntiles), dim3(kStagedThreads), 0, s, d_jobs, d_order, tile_off,
+                           (const SplitDesc *)d_splits, d_lookback, d_ticket + KIND, d_ready,
+                           const_cast<JobResultDev *>(d_res));
     else if (ntiles)
-        hipLaunchKernelGGL((k_merge_tile<KIND, false>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order,
-                           tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_lookback, d_ticket, d_ready,
-                           d_res, phase);
+        hipLaunchKernelGGL((k_merge_tile<KIND>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,
+                           (const SplitDesc *)d_splits, d_status, d_masks, d_res, phase);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -657,9 +831,11 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     }
     if (mark) mark(mark_ctx, phase ? "recompute_partition" : "merge_partition");
     if (run(phase)) return -1;
-    hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
-                       d_results, phase);
-    if (hipGetLastError() != hipSuccess) return -1;
+    if (!d_lookback) { // the staged merge writes the offsets and results itself
+        hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
+                           d_results, phase);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
     if (mark) mark(mark_ctx, phase ? "recompute_merge" : "merge");
     return 0;
 }

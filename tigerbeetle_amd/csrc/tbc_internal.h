@@ -30,6 +30,11 @@ constexpr uint64_t kTombstoneBit = 1ull << 63;
 constexpr uint32_t kMergeTile = 2048;
 static_assert(2 * (kMergeTile / 64) == 64, "one mask word per lane");
 constexpr uint32_t kMergeThreads = kMergeTile / 4;
+// Tile of the staged merge (merge.hip k_merge_staged): its values are held
+// in registers, 64 KiB per workgroup at most.
+__host__ __device__ inline uint32_t staged_tile(uint32_t value_size) {
+    return value_size <= 64 ? 1024u : 65536u / value_size;
+}
 
 enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };
 
@@ -60,7 +65,7 @@ struct JobDesc {
     Stream a, b;
     const uint64_t *addresses;
     uint32_t address_count;
-    uint32_t pad1;
+    uint32_t merge_tile; // merged positions per merge tile: kMergeTile, or staged_tile(value_size)
     uint8_t *out_blocks;
     // Batch bases (global grid indices).
     uint32_t tile_base, tile_count;      // merge tiles

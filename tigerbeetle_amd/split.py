@@ -341,13 +341,25 @@ class SplitResult:
     plan: TablePlan
 
 
-def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = False) -> SplitResult:
+def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = False, scratch: dict | None = None,
+                  before_phase2=None) -> SplitResult:
     """Run rank `rank`'s share of `job` split at `cuts` (block_cuts or
     split_points). With staged=True the job's segments hold only this rank's
     range [cuts[rank], cuts[rank+1]) of A and of B (what rank_blocks named,
-    staged on this GPU); otherwise the whole job's inputs, sliced here."""
+    staged on this GPU); otherwise the whole job's inputs, sliced here.
+    `scratch` (a dict kept by a caller that repeats the split) keeps the two
+    output arenas between calls; `before_phase2` runs after the exchange, just
+    before phase 2 is submitted (a caller enqueues its other work there)."""
     from .engine import Job
     tree, bs = job.tree, engine.block_size
+
+    def arena(name: str, nbytes: int):
+        if scratch is None:
+            return engine.alloc(nbytes)
+        buf = scratch.get(name)
+        if buf is None or buf.nbytes < nbytes:
+            buf = scratch[name] = engine.alloc(nbytes)
+        return buf
     lay = engine.layout(tree)
     vcm, dbcm, vs = lay.block_value_count_max, lay.data_block_count_max, tree.value_size
 
@@ -364,7 +376,7 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     n = (a_hi - a_lo) + (b_hi - b_lo)
     db = -(-n // vcm)
     nblocks = db + -(-db // dbcm)
-    out1 = engine.alloc(max(1, nblocks) * bs)
+    out1 = arena("phase1", max(1, nblocks) * bs)
     p1 = Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
              job.snapshot_min, np.arange(1, nblocks + 1, dtype=np.uint64), out1, flags=COMPACTION_VALUES_ONLY)
     b1 = engine.submit([p1])
@@ -379,6 +391,8 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     head = [(p, c * vs) for p, c in sub(mine, 0, plan.need[rank])]
     keep, head_ptrs = exchange.all_gather_heads(engine, head, plan.head_max * vs)
 
+    if before_phase2 is not None:
+        before_phase2()
     t0, t1 = plan.tables[rank]
     if t0 == t1:
         return SplitResult((t0, t1), None, np.zeros((0, 128), dtype=np.uint8), None, plan)
@@ -392,7 +406,7 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     addrs = np.asarray(job.addresses, dtype=np.uint64)[lo:hi]
     if len(addrs) != hi - lo:
         raise ValueError("address list shorter than the job's output")
-    out2 = engine.alloc((hi - lo) * bs)
+    out2 = arena("phase2", (hi - lo) * bs)
     p2 = Job(tree, seg2, [], False, False, job.level_b, job.cluster, job.snapshot_min, addrs, out2)
     b2 = engine.submit([p2])
     b2.wait()
@@ -401,5 +415,6 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     del keep
     if r2.status != 0 or r2.table_count != t1 - t0:
         raise RuntimeError(f"split phase 2 failed on rank {rank}: status {r2.status}")
-    out1.free()
+    if scratch is None:
+        out1.free()
     return SplitResult((t0, t1), r2, infos, out2, plan)

@@ -500,6 +500,32 @@ __global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
     }
 }
 
+// 64 lanes per message: both 32-lane halves hold the
+// same state; half 0 looks up T0/T1 of its column's bytes, half 1 T2/T3, so
+// a lane issues two table reads per update instead of four. Each half folds
+// its pair with one quad DPP (u = t_a ^ qp1(t_b)); half 1's partial belongs to
+// column c - 2, so it is rotated by qp2 and half 0 adds the round key and
+// message instead; one v_permlane32_swap exchanges the partials, and
+// swap.lo ^ swap.hi is the whole new column in both halves (no select).
+// Used with one message per wave (k_prod per_wave = 1).
+struct StepHalves {
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t, uint32_t x,
+                                                    uint32_t m) {
+        const bool hi = (threadIdx.x & 32) != 0;
+        const uint32_t base = hi ? tb.hi : tb.lo;
+        const uint32_t a0 = __builtin_amdgcn_perm(x, base, hi ? 0x03020600u : 0x03020400u);
+        const uint32_t a1 = __builtin_amdgcn_perm(x, base, hi ? 0x03020700u : 0x03020500u);
+        const uint32_t ta = lds_u32(sT, a0);
+        const uint32_t tb1 = lds_u32(sT, a1 + 128);
+        const uint32_t acc = key_valu(x) ^ m;
+        const uint32_t u = ta ^ quad_perm<1, 2, 3, 0>(tb1);
+        const uint32_t mhi = hi ? ~0u : 0u; // loop invariant: a bitwise select, no branch (v_bfi_b32)
+        const uint32_t part = (quad_perm<2, 3, 0, 1>(u) & mhi) | ((u ^ acc) & ~mhi);
+        const auto sw = __builtin_amdgcn_permlane32_swap(part, part, false, false);
+        return sw[0] ^ sw[1];
+    }
+};
+
 // Production loop (reference timing): k_checksum_batch semantics on 1 MiB bodies.
 template <class Step>
 __global__ __launch_bounds__(1024) void k_prod(const uint8_t *base, uint32_t count, uint32_t per_wave, uint8_t *out) {
@@ -623,6 +649,17 @@ int main(int argc, char **argv) {
             check(name);
         };
 
+        {
+            // 64 lanes per message: one message per wave, both halves on it.
+            const uint32_t waves = count, wpb = wpb_for(waves, 16);
+            CK(hipMemset(d_out, 0, 16ull * count));
+            const float ms = timed([&] {
+                hipLaunchKernelGGL(k_prod<StepHalves>, dim3((waves + wpb - 1) / wpb), dim3(64 * wpb), 0, 0, d_msgs,
+                                   count, 1u, d_out);
+            });
+            report("halves64", count, waves, wpb, ms);
+            check("halves64");
+        }
         run_asm(StepAsmT<2>{}, "asm-valu-split");
         run_asm(StepAsmT<3>{}, "asm-xor3");
         run_asm(StepAsmT<4>{}, "asm-xor3-1wait");
