@@ -255,12 +255,32 @@ def cpu_baseline_config1(bars: int = 11, bs: int = 1 << 20) -> dict:
     oracle.build()
     ex = OracleExecutor(oracle, bs)
     f = forest.Forest(ex, 24_000, cluster=0)
-    f.run(benchmark_load.BenchmarkLoad(transfer_count=bars * 32 * benchmark_load.BATCH).ops())
+    with pinned_core() as pin:
+        f.run(benchmark_load.BenchmarkLoad(transfer_count=bars * 32 * benchmark_load.BATCH).ops())
     return {"value": round(ex.input_bytes / ex.busy / 1e6, 1), "unit": "MB/s", "cores": 1, "kind": "port",
+            **pin.info(),
             "sample": f"config 1's first {bars} bars ({bars * 32 * benchmark_load.BATCH} transfers: "
                       f"{len(f.history)} half-bars, {ex.input_bytes / 1e6:.0f} MB of compaction input, "
                       f"{ex.busy:.1f} s in the oracle's sorts and compactions) through oracle/tbc_oracle.c "
                       f"(single thread) on {cpu_model()}"}
+
+
+class pinned_core:
+    """Pin this process to one host core while the single-threaded CPU
+    baseline runs (restored afterwards); reports the machine's CPU count and
+    the cores this process may use."""
+
+    def __enter__(self):
+        self.allowed = sorted(os.sched_getaffinity(0))
+        self.core = self.allowed[len(self.allowed) // 2]  # away from core 0's interrupt load
+        os.sched_setaffinity(0, {self.core})
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, set(self.allowed))
+
+    def info(self) -> dict:
+        return {"nproc": os.cpu_count(), "affinity_cpus": len(self.allowed), "pinned_to": self.core}
 
 
 def cpu_model() -> str:
@@ -283,6 +303,8 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
     from oracle import oracle
     oracle.build()
     total_bytes, total_t, jobs = 0, 0.0, 0
+    pin = pinned_core()
+    pin.__enter__()
     while total_t < budget_s and jobs < njobs:
         js = configs.GENERATORS[config](jobs)
         spec = js.tree
@@ -301,6 +323,7 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
         assert r.status == 0
         total_bytes += js.input_bytes
         jobs += 1
+    pin.__exit__()
     import platform
     cpu = platform.processor() or "unknown"
     try:
@@ -312,6 +335,7 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
         pass
     from oracle.oracle import lib as olib
     return {"value": round(total_bytes / total_t / 1e6, 1), "unit": "MB/s", "cores": 1, "kind": "port",
+            **pin.info(),
             "sample": f"{jobs} of {njobs} jobs ({total_bytes/1e6:.0f} MB of input) of config {config} through "
                       f"oracle/tbc_oracle.c (single thread, AES-NI={bool(olib().tbo_has_aesni())}) on {cpu}"}
 

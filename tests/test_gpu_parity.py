@@ -237,6 +237,43 @@ def test_sort_truncated_top_bytes_and_rescue(engine, oracle_lib):
         assert np.array_equal(got, want), spec.name
 
 
+def test_sort_values_many_passes(engine, oracle_lib):
+    """Tables whose keys vary in more bytes than the direct pass launches
+    cover (sort.hip kDirectPasses) and whose top bytes cluster, so the plan
+    keeps every pass (no truncation): the passes past the direct ones run in
+    k_sort_pass_rest, ordered by completion counters. Equal keys included;
+    every table bit-exact vs the oracle's stable sort, in one batch."""
+    rng = np.random.default_rng(21)
+    n = 120_001
+    tables, wants = [], []
+
+    def add(name, limbs):
+        spec = trees.BY_NAME[name]
+        vals = workloads.values_from_keys(spec, limbs, rng.random(n) < 0.05, rng)
+        t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                            spec.value_count_max, 1 << 20)
+        wants.append(oracle_lib.sort_values(t, vals))
+        tables.append((spec, engine.upload(vals, pad=16), n))
+
+    def clustered(bits_random: int, top_bytes: int):
+        x = rng.integers(0, 1 << bits_random, n, dtype=np.uint64)
+        for b in range(top_bytes):  # each byte above takes one of two values
+            x |= rng.integers(1, 3, n, dtype=np.uint64) << np.uint64(bits_random + 8 * b)
+        return x
+    # composite u128: 2 timestamp bytes + 5 field-lo bytes + 2 field-hi bytes = 9 passes
+    add("transfers.user_data_128", [rng.integers(1, 1 << 16, n, dtype=np.uint64), clustered(16, 3),
+                                    clustered(0, 2)])
+    # object tree (u64 timestamp key): 8 varying bytes, top ones clustered
+    add("transfers.timestamp", [clustered(24, 4) & np.uint64((1 << 63) - 1)])
+    # id tree: 12 varying bytes
+    add("transfers.id", [clustered(32, 4), clustered(8, 3)])
+    engine.sort_values_batch([(spec, buf, m) for spec, buf, m in tables])
+    engine.synchronize()
+    for (spec, buf, m), want in zip(tables, wants):
+        got = buf.download(m * spec.value_size).reshape(m, spec.value_size)
+        assert np.array_equal(got, want), spec.name
+
+
 @pytest.mark.parametrize("name", ["accounts.user_data_64", "transfers.debit_account_id"])
 def test_sort_composite_key_cases(engine, oracle_lib, name):
     """composite_key.zig:88-124's cases on the device's key_from_value: the

@@ -56,6 +56,7 @@ constexpr uint32_t kMaxLimbs = 3;
 constexpr uint32_t kMaxPasses = 8 * kMaxLimbs;
 constexpr uint32_t kTopBytes = 4;   // truncated sorts keep at least this many top bytes
 constexpr uint32_t kRunMax = 64;    // longest run of equal top bytes k_sort_fixup orders
+constexpr uint32_t kDirectPasses = 6; // passes with a launch each; the rest share k_sort_pass_rest
 
 // Look-back words (64-bit): the pass launch's epoch in the top half (words
 // of earlier launches read as "not published", so the buffer is zeroed once,
@@ -351,32 +352,65 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
 // workgroup's LDS does not grow with the key width (5 workgroups per CU).
 // A table's last pass moves the values themselves (values[dst] =
 // copy[index]) instead of keys and indices: the gather is fused into it.
-__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
-                                                            const uint32_t *tile_seg, const uint32_t *tile_order,
-                                                            uint32_t p, uint32_t ntiles,
-                                                            uint32_t N, uint64_t *keys0, uint64_t *keys1,
-                                                            uint32_t *idx0, uint32_t *idx1, const uint32_t *bins,
-                                                            uint64_t *status, uint32_t epoch,
-                                                            uint32_t *tile_counter) {
+struct PassShared {
+    uint32_t tile;
+    uint32_t wcnt[kSortWaves][kRadix]; // per wave: running, then total counts
+    uint32_t start[kRadix];            // local start of each digit in the tile
+    uint32_t excl[kRadix];             // items of the digit in the table's earlier tiles
+    uint32_t wsum[kSortWaves];
+    uint64_t key[kSortTile];           // one limb at a time
+    uint32_t idx[kSortTile];
+    uint8_t dig[kSortTile];
+};
+
+// Pass p over the tiles taken from tile_counter[p] (ticket order), until
+// they run out. `done` (the rest kernel only): every finished tile adds one
+// to done[p] after an agent-scope release, and before its first tile of pass
+// p a workgroup waits for done[p - 1] == ntiles and acquires (the pass reads
+// what every tile of the previous pass wrote, on any XCD).
+__device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *segs, const uint32_t *tile_seg,
+                                                const uint32_t *tile_order, uint32_t p, uint32_t ntiles, uint32_t N,
+                                                uint64_t *keys0, uint64_t *keys1, uint32_t *idx0, uint32_t *idx1,
+                                                const uint32_t *bins, uint64_t *status, uint32_t epoch,
+                                                uint32_t *tile_counter, uint32_t *done) {
     constexpr uint32_t R = kSortRounds;
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_wcnt[kSortWaves][kRadix]; // per wave: running, then total counts
-    __shared__ uint32_t s_start[kRadix];            // local start of each digit in the tile
-    __shared__ uint32_t s_excl[kRadix];             // items of the digit in the table's earlier tiles
-    __shared__ uint32_t s_wsum[kSortWaves];
-    __shared__ uint64_t s_key[kSortTile];           // one limb at a time
-    __shared__ uint32_t s_idx[kSortTile];
-    __shared__ uint8_t s_dig[kSortTile];
+    auto &s_tile = sh.tile;
+    auto &s_wcnt = sh.wcnt;
+    auto &s_start = sh.start;
+    auto &s_excl = sh.excl;
+    auto &s_wsum = sh.wsum;
+    auto &s_key = sh.key;
+    auto &s_idx = sh.idx;
+    auto &s_dig = sh.dig;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (!((batch->active >> p) & 1u)) return; // uniform: no table has this many passes
     const uint64_t ep = (uint64_t)epoch << 32;
     const uint64_t lt_mask = (1ull << lane) - 1;
-    for (;;) {
+    // The first pass of the rest kernel follows a kernel boundary: nothing to wait for.
+    bool waited = done == nullptr || p == kDirectPasses;
+    for (bool first = true;; first = false) {
+        // Every wave releases its own stores of the previous tile (at agent
+        // scope: waits for them and writes the XCD's L2 back) before the
+        // tile is counted as done.
+        if (!first && done) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __syncthreads(); // the previous tile's LDS readers are done
+        if (!first && done && tid == 0)
+            __hip_atomic_fetch_add(&done[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0) s_tile = atomicAdd(&tile_counter[p], 1u);
         for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
         __syncthreads();
         if (s_tile >= ntiles) return;
+        if (!waited) { // rest kernel: every tile of pass p - 1 is complete and visible
+            if (tid == 0) {
+                for (uint32_t spins = 0; __hip_atomic_load(&done[p - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                                             ntiles;) {
+                    if (++spins > (1u << 26)) break; // bounded (a broken invariant, not a hang)
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            __syncthreads();
+            waited = true;
+        }
         const uint32_t t = tile_order[s_tile];
         const uint32_t sg = tile_seg[t];
         const SortSeg &S = segs[sg];
@@ -548,6 +582,43 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs,
                 if (j < m) gst<uint64_t>(kdst + (size_t)(limb + l) * N + dst[q], s_key[j]);
             }
         }
+    }
+}
+
+// One launch per pass below kDirectPasses: the kernel boundary orders the
+// passes. A pass no table needs returns at once.
+__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
+                                                            const uint32_t *tile_seg, const uint32_t *tile_order,
+                                                            uint32_t p, uint32_t ntiles,
+                                                            uint32_t N, uint64_t *keys0, uint64_t *keys1,
+                                                            uint32_t *idx0, uint32_t *idx1, const uint32_t *bins,
+                                                            uint64_t *status, uint32_t epoch,
+                                                            uint32_t *tile_counter) {
+    __shared__ PassShared sh;
+    if (!((batch->active >> p) & 1u)) return; // uniform: no table has this many passes
+    sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, N, keys0, keys1, idx0, idx1, bins, status, epoch,
+                    tile_counter, nullptr);
+}
+
+// Passes [kDirectPasses, kMaxPasses) in ONE launch (most batches need none:
+// a truncated sort keeps at least 4 bytes, an in-order prefix is skipped):
+// workgroups take pass p's tiles after pass p - 1's tickets ran out, so a
+// tile only ever waits on tiles already taken by running workgroups (no
+// grid barrier, no residency assumption), and the completion counters with
+// agent-scope release/acquire order the passes across XCDs. Each pass takes
+// a fresh look-back epoch.
+__global__ __launch_bounds__(kSortThreads) void k_sort_pass_rest(const SortSeg *segs, const SortBatch *batch,
+                                                                 const uint32_t *tile_seg, const uint32_t *tile_order,
+                                                                 uint32_t ntiles, uint32_t N, uint64_t *keys0,
+                                                                 uint64_t *keys1, uint32_t *idx0, uint32_t *idx1,
+                                                                 const uint32_t *bins, uint64_t *status,
+                                                                 uint32_t epoch0, uint32_t *tile_counter,
+                                                                 uint32_t *done) {
+    __shared__ PassShared sh;
+    for (uint32_t p = kDirectPasses; p < kMaxPasses; p++) {
+        if (!((batch->active >> p) & 1u)) return; // passes run as a prefix: none beyond either
+        sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, N, keys0, keys1, idx0, idx1, bins, status,
+                        epoch0 + (p - kDirectPasses), tile_counter, done);
     }
 }
 
@@ -746,8 +817,8 @@ static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
     o += align256(4 * tiles);
     s.hist = o; // zeroed per batch: hist, counters, batch
     o += align256(4ull * nseg * kMaxPasses * kRadix);
-    s.counters = o;
-    o += align256(4ull * kMaxPasses);
+    s.counters = o; // per pass: tile tickets, then (rest kernel) completed tiles
+    o += align256(8ull * kMaxPasses);
     s.batch = o;
     o += align256(sizeof(SortBatch));
     s.bins = o;
@@ -855,10 +926,18 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         resident = (uint32_t)(per_cu * cus);
     }
     const uint32_t pgrid = ntiles < resident ? ntiles : resident;
-    for (uint32_t p = 0; p < 8 * max_kl; p++) {
+    const uint32_t passes = 8 * max_kl;
+    for (uint32_t p = 0; p < passes && p < kDirectPasses; p++) {
         if (*epoch == 0) *epoch = 1; // 0 is the zeroed buffer's
         hipLaunchKernelGGL(k_sort_pass, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, d_order, p,
                            ntiles, N, keys0, keys1, idx0, idx1, bins, status, (*epoch)++, counters);
+    }
+    if (passes > kDirectPasses) {
+        if (*epoch == 0 || *epoch + kMaxPasses < *epoch) *epoch = 1; // a fresh epoch per pass, none 0
+        hipLaunchKernelGGL(k_sort_pass_rest, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, d_order,
+                           ntiles, N, keys0, keys1, idx0, idx1, bins, status, *epoch, counters,
+                           counters + kMaxPasses);
+        *epoch += kMaxPasses;
     }
     hipLaunchKernelGGL(k_sort_fixup, dim3(ntiles), dim3(256), 0, s, d_segs, (const uint32_t *)d_tile,
                        (const uint32_t *)idx0, (const uint32_t *)idx1);
