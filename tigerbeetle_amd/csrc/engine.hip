@@ -155,6 +155,19 @@ struct tbc_engine {
     // merges run in stream order, so one growable buffer serves them all.
     uint8_t *kway_scratch = nullptr;
     uint64_t kway_scratch_size = 0;
+    // Memtable sorts run on their own stream, after everything enqueued on
+    // the engine stream before them; later engine-stream work waits for a
+    // sort only if it touches that sort's tables (wait_sorts) — so a bar-end
+    // sort overlaps the next half-bar's level compactions, which do not read
+    // memtables — and conservatively where it cannot tell (join_sorts).
+    hipStream_t sort_stream = nullptr;
+    hipEvent_t sort_last = nullptr; // recorded after every sort batch
+    bool sort_recorded = false;
+    struct PendingSort {
+        std::vector<std::pair<uint64_t, uint64_t>> ranges; // [lo, hi) of the sorted tables
+        hipEvent_t done;
+    };
+    std::vector<PendingSort> pending_sorts;
 };
 
 struct tbc_grid {
@@ -306,12 +319,44 @@ static void mark_cb(void *ctx, const char *name) {
     b->mark_names[b->nmarks++] = name;
 }
 
+// Engine-stream work after a sort waits for it when it touches its tables.
+static void retire_sorts(tbc_engine *e) {
+    auto &ps = e->pending_sorts;
+    for (size_t i = 0; i < ps.size();) {
+        if (hipEventQuery(ps[i].done) == hipSuccess) {
+            e->event_pool.push_back(ps[i].done);
+            ps.erase(ps.begin() + (long)i);
+        } else {
+            i++;
+        }
+    }
+}
+
+static bool wait_sorts(tbc_engine *e, uint64_t lo, uint64_t hi) {
+    for (const auto &p : e->pending_sorts)
+        for (const auto &r : p.ranges)
+            if (lo < r.second && r.first < hi) {
+                if (hipStreamWaitEvent(e->stream, p.done, 0) != hipSuccess) return false;
+                break;
+            }
+    return true;
+}
+
+static bool wait_sorts_ptr(tbc_engine *e, const void *p, uint64_t bytes) {
+    return e->pending_sorts.empty() || wait_sorts(e, (uint64_t)(uintptr_t)p, (uint64_t)(uintptr_t)p + bytes);
+}
+
+// Work that may read any device memory waits for every sort enqueued so far.
+static bool join_sorts(tbc_engine *e) {
+    return !e->sort_recorded || hipStreamWaitEvent(e->stream, e->sort_last, 0) == hipSuccess;
+}
+
 // Later work on the engine stream that touches grid blocks (staging blocks in
 // or out, synchronous checks) waits for every batch tail enqueued so far.
 static bool join_tails(tbc_engine *e) {
     for (int t = 0; t < tbc_engine::kTails; t++)
         if (hipStreamWaitEvent(e->stream, e->tail_ev[t], 0) != hipSuccess) return false;
-    return true;
+    return join_sorts(e);
 }
 
 extern "C" {
@@ -362,6 +407,8 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
              hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&e->sort_stream, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&e->sort_last, hipEventDisableTiming) == hipSuccess;
     for (int s = 0; ok && s < Staging::kSlots; s++)
         ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
     // The merge's mask buffer, sized up front for batches of up to 2^28
@@ -382,7 +429,11 @@ void tbc_engine_deinit(tbc_engine *e) {
     hipStreamSynchronize(e->stream);
     for (int t = 0; t < tbc_engine::kTails; t++)
         if (e->tail[t]) hipStreamSynchronize(e->tail[t]);
+    if (e->sort_stream) hipStreamSynchronize(e->sort_stream);
+    for (auto &p : e->pending_sorts) e->event_pool.push_back(p.done);
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
+    if (e->sort_last) hipEventDestroy(e->sort_last);
+    if (e->sort_stream) hipStreamDestroy(e->sort_stream);
     for (int s = 0; s < Staging::kSlots; s++)
         if (e->staging.ev[s]) hipEventDestroy(e->staging.ev[s]);
     if (e->staging.base) hipHostFree(e->staging.base);
@@ -564,6 +615,7 @@ void tbc_memtable_deinit(tbc_memtable *m) {
     if (!m) return;
     hipSetDevice(m->engine->device);
     hipStreamSynchronize(m->engine->stream);
+    if (m->engine->sort_stream) hipStreamSynchronize(m->engine->sort_stream);
     hipFree(m->values);
     delete m;
 }
@@ -574,7 +626,9 @@ tbc_status tbc_memtable_put(tbc_memtable *m, const void *values, uint32_t count)
     if (!count) return TBC_OK;
     hipSetDevice(m->engine->device);
     const uint64_t vs = m->tree.value_size;
-    if (!stage_h2d(m->engine, m->values + m->count * vs, values, count * vs)) return TBC_ERR_DEVICE;
+    if (!wait_sorts_ptr(m->engine, m->values + m->count * vs, count * vs) ||
+        !stage_h2d(m->engine, m->values + m->count * vs, values, count * vs))
+        return TBC_ERR_DEVICE;
     m->count += count;
     return TBC_OK;
 }
@@ -623,7 +677,8 @@ tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+    if (!wait_sorts_ptr(e, dst, bytes) || hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+        return TBC_ERR_DEVICE;
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
@@ -631,13 +686,15 @@ tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t 
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+    if (!wait_sorts_ptr(e, src, bytes) || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        return TBC_ERR_DEVICE;
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_copy_device_async(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
     if (!e || (bytes && (!dst || !src))) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
+    if (!wait_sorts_ptr(e, dst, bytes) || !wait_sorts_ptr(e, src, bytes)) return TBC_ERR_DEVICE;
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, e->stream) == hipSuccess ? TBC_OK
                                                                                           : TBC_ERR_DEVICE;
 }
@@ -646,7 +703,8 @@ tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+    if (!wait_sorts_ptr(e, dst, bytes) || hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess)
+        return TBC_ERR_DEVICE;
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
@@ -655,6 +713,8 @@ tbc_status tbc_synchronize(tbc_engine *e) {
     hipSetDevice(e->device);
     bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
     for (int t = 0; t < tbc_engine::kTails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
+    ok = ok && hipStreamSynchronize(e->sort_stream) == hipSuccess;
+    retire_sorts(e);
     return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
 
@@ -743,11 +803,14 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
         items[k] = SortItem{j.values, j.count, j.tree.value_size, j.tree.timestamp_offset, j.tree.key_kind};
     }
     hipSetDevice(e->device);
+    static const bool same_stream = getenv("TBC_SORT_SAME_STREAM") != nullptr; // A/B measurement only
+    hipStream_t ss = same_stream ? e->stream : e->sort_stream;
     const uint64_t need = sort_scratch_bytes(items.data(), count);
     const uint64_t host_need = sort_host_bytes(items.data(), count);
     if (host_need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
     if (need > e->sort_scratch_size) { // grows once per larger bar (a stream drain)
-        if (hipStreamSynchronize(e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (hipStreamSynchronize(e->stream) != hipSuccess || hipStreamSynchronize(e->sort_stream) != hipSuccess)
+            return TBC_ERR_DEVICE;
         if (e->sort_scratch) hipFree(e->sort_scratch);
         e->sort_scratch = nullptr;
         e->sort_scratch_size = 0;
@@ -760,7 +823,8 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     }
     const uint64_t words = sort_status_words(items.data(), count);
     if (words > e->sort_status_words) {
-        if (hipStreamSynchronize(e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (hipStreamSynchronize(e->stream) != hipSuccess || hipStreamSynchronize(e->sort_stream) != hipSuccess)
+            return TBC_ERR_DEVICE;
         if (e->sort_status) hipFree(e->sort_status);
         e->sort_status = nullptr;
         e->sort_status_words = 0;
@@ -769,7 +833,9 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
             e->sort_status = nullptr;
             return TBC_ERR_OUT_OF_MEMORY;
         }
-        if (hipMemsetAsync(e->sort_status, 0, 8 * want, e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (hipMemsetAsync(e->sort_status, 0, 8 * want, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            return TBC_ERR_DEVICE;
         e->sort_status_words = want;
     }
     // The descriptors go through a pinned staging slot, reusable once the
@@ -779,10 +845,31 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     st.next = (st.next + 1) % Staging::kSlots;
     if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
     uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    retire_sorts(e);
+    if (ss != e->stream) { // after everything enqueued so far (the tables' puts and landings)
+        hipEvent_t fork = take_event(e);
+        const bool ok = fork && hipEventRecord(fork, e->stream) == hipSuccess &&
+                        hipStreamWaitEvent(ss, fork, 0) == hipSuccess;
+        if (fork) e->event_pool.push_back(fork); // the wait holds the recording it saw
+        if (!ok) return TBC_ERR_DEVICE;
+    }
     int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, e->sort_status,
-                               e->sort_status_words, &e->sort_epoch, host, e->stream);
-    if (hipEventRecord(st.ev[slot], e->stream) != hipSuccess) rc = -1;
+                               e->sort_status_words, &e->sort_epoch, host, ss);
+    if (hipEventRecord(st.ev[slot], ss) != hipSuccess) rc = -1;
     st.used[slot] = true;
+    if (ss != e->stream && rc == 0) {
+        tbc_engine::PendingSort ps;
+        ps.done = take_event(e);
+        for (uint32_t k = 0; k < count; k++)
+            if (jobs[k].count)
+                ps.ranges.push_back({(uint64_t)(uintptr_t)jobs[k].values,
+                                     (uint64_t)(uintptr_t)jobs[k].values + (uint64_t)jobs[k].count * jobs[k].tree.value_size});
+        if (!ps.done || hipEventRecord(ps.done, ss) != hipSuccess || hipEventRecord(e->sort_last, ss) != hipSuccess)
+            rc = -1;
+        else
+            e->pending_sorts.push_back(ps);
+        e->sort_recorded = true;
+    }
     return rc == 0 ? TBC_OK : TBC_ERR_DEVICE;
 }
 
@@ -802,7 +889,7 @@ tbc_status tbc_sort_values_async(tbc_engine *e, const tbc_tree *tree, void *valu
 tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
     tbc_status st = tbc_sort_values_async(e, tree, values, count);
     if (st != TBC_OK) return st;
-    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    return tbc_synchronize(e);
 }
 
 // Host image of kway.hip's KPair (kway_pair_bytes() checks the size).
@@ -828,6 +915,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
     if (n >= 0x7fffffffull) return TBC_ERR_INVALID_ARGUMENT;
     if (n && !out_values) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
+    if (!join_sorts(e)) return TBC_ERR_DEVICE; // the streams may be tables a sort still writes
     tbc_kway *k = new (std::nothrow) tbc_kway();
     if (!k) return TBC_ERR_OUT_OF_MEMORY;
     k->engine = e;
@@ -1361,7 +1449,16 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     e->event_pool.pop_back();
 
     hipStream_t s = e->stream;
-    bool ok = hipMemcpyAsync(d_in, h_in, sz_in, hipMemcpyHostToDevice, s) == hipSuccess;
+    bool ok = true;
+    // Inputs a sort is still writing (a bar's memtables): wait for that sort.
+    retire_sorts(e);
+    if (!e->pending_sorts.empty())
+        for (uint32_t i = 0; ok && i < count; i++)
+            for (int side = 0; ok && side < 2; side++)
+                for (const auto &g : seg_in[2 * (size_t)i + side])
+                    if (g.first && !(ok = wait_sorts(e, g.first, g.first + (uint64_t)g.second * hj[i].value_size)))
+                        break;
+    ok = ok && hipMemcpyAsync(d_in, h_in, sz_in, hipMemcpyHostToDevice, s) == hipSuccess;
     // Tile status, block tiles and results start zeroed (contiguous).
     ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");
