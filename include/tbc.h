@@ -298,8 +298,8 @@ tbc_status tbc_sort_values_async(tbc_engine *engine, const tbc_tree *tree, void 
  * tree; the batch is the same work without a launch train per tree). Same
  * semantics per table as tbc_sort_values; tables that are already sorted are
  * left untouched. Enqueued on the engine stream with no host wait: the digit
- * plan (which bytes vary, which passes run) is computed and read on the
- * device (sort.hip k_sort_plan). */
+ * plan (which key bits vary, which passes run) is computed and read on the
+ * device (sort.hip k_sort_layout / k_sort_plan). */
 typedef struct tbc_sort_job {
     tbc_tree tree;
     void *values;   /* device pointer, 16-byte aligned */

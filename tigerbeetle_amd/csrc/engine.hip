@@ -395,15 +395,16 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
         return TBC_ERR_OUT_OF_MEMORY;
     }
     bool ok = true;
-    // Tails (chains, index blocks, input checks, results) at the highest
-    // stream priority: their workgroups are dispatched ahead of the next
-    // batch's front on the engine stream, so a tail's short kernels (index
-    // blocks, checks) are not starved behind a merge that fills the chip.
+    // Tails (chains, index blocks, input checks, results) at the engine
+    // stream's priority. Round 3 measured the highest tail priority (its
+    // workgroups dispatched ahead of the next front) on one box: config 1
+    // 130 -> 108 ms and config 5 15.0 -> 14.4 ms with equal priorities (the
+    // fronts are the critical path); TBC_TAIL_PRIORITY=1 (A/B only) restores it.
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-    static const bool flat = getenv("TBC_FLAT_PRIORITY") != nullptr; // A/B measurement only
+    static const bool high = getenv("TBC_TAIL_PRIORITY") != nullptr; // A/B measurement only
     for (int t = 0; ok && t < tbc_engine::kTails; t++)
-        ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, flat ? 0 : prio_greatest) == hipSuccess &&
+        ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, high ? prio_greatest : 0) == hipSuccess &&
              hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
@@ -803,8 +804,13 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
         items[k] = SortItem{j.values, j.count, j.tree.value_size, j.tree.timestamp_offset, j.tree.key_kind};
     }
     hipSetDevice(e->device);
-    static const bool same_stream = getenv("TBC_SORT_SAME_STREAM") != nullptr; // A/B measurement only
-    hipStream_t ss = same_stream ? e->stream : e->sort_stream;
+    // The bar-end sort runs on the engine stream. A sort stream of its own
+    // (opt-in, TBC_SORT_STREAM=1) lets it overlap the next half-bar's level
+    // compactions, but with GPU_MAX_HW_QUEUES=4 (the box's default) a fifth
+    // stream shares a hardware queue with a tail and inherits its order:
+    // round 3 measured config 1 130 vs 75 ms and config 3 4.28 vs 3.78 ms.
+    static const bool own_stream = getenv("TBC_SORT_STREAM") != nullptr; // A/B measurement only
+    hipStream_t ss = own_stream ? e->sort_stream : e->stream;
     const uint64_t need = sort_scratch_bytes(items.data(), count);
     const uint64_t host_need = sort_host_bytes(items.data(), count);
     if (host_need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
@@ -1269,15 +1275,19 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         order[i] = i;
     }
     // The staged merge (merge.hip k_merge_staged: values read once into
-    // registers, written straight to their output slots) serves every batch
-    // whose bodies are not built beside their chains: grid batches, pipelined
-    // groups, VALUES_ONLY and the throughput regime. TBC_NO_STAGED=1 (A/B
-    // measurement only) keeps the mask merge + k_assemble there.
+    // registers, written straight to their output slots) can serve every
+    // batch whose bodies are not built beside their chains: grid batches,
+    // pipelined groups, VALUES_ONLY and the throughput regime. It moves R + W
+    // where the mask merge + k_assemble move R + 2 W, but measured slower
+    // (round 3, one box: config 5 19.9 vs 15.0 ms, its four fronts 16.7 vs
+    // 10.8 ms of kernel time; its tiles hold 64 KiB of registers each and
+    // serialise on the look-back beside the chain workgroups), so it is
+    // opt-in: TBC_STAGED=1 (A/B measurement and its parity tests).
     uint64_t dblocks_all = 0;
     for (uint32_t i = 0; i < count; i++) dblocks_all += hj[i].dblock_max;
-    static const bool no_staged = getenv("TBC_NO_STAGED") != nullptr;
-    const bool staged = !no_staged && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
-                                       (dblocks_all + 1) / 2 > fused_max_chain_waves());
+    static const bool staged_on = getenv("TBC_STAGED") != nullptr;
+    const bool staged = staged_on && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
+                                      (dblocks_all + 1) / 2 > fused_max_chain_waves());
     for (uint32_t i = 0; i < count; i++) {
         JobDesc &d = hj[i];
         if (staged) d.merge_tile = staged_tile(d.value_size);

@@ -6,40 +6,47 @@
 // keeps the LAST of a run of equal keys (compaction.zig:519-522).
 //
 // A batch of memtables (every tree's at the bar end) is sorted by one
-// enqueued launch sequence that never waits on the host. Items are sorted
-// as (packed key, index) pairs by a stable LSD radix sort with 8-bit digits:
+// enqueued launch sequence that never waits on the host. Every item is ONE
+// 64-bit word: the key bits that vary over its table (packed), above the
+// item's index in the table. The words are distinct, so any order of them is
+// the stable order of the keys; a stable LSD radix sort with 8-bit digits
+// over the packed bits moves 8 bytes per item per pass:
 //
-//   k_sort_extract  per tile of 2,048 items: a copy of the values (the
+//   k_sort_extract  per tile of 4,096 items: a copy of the values (the
 //                   gather's source), OR/AND of every key limb, and whether
 //                   the table is out of order at all;
-//   k_sort_layout   per table: the key bytes that vary over the table, in
-//                   significance order; the rest cannot decide any order, so
-//                   the packed key (those bytes only, 8 per limb) orders the
-//                   table exactly as its key does (config 3's composite u128
-//                   keys: 24 key bytes, 6 varying -> one 64-bit limb);
-//   k_sort_pack     per tile: packed keys + indices, the digit histograms of
-//                   every packed byte, and which low-order prefixes of the
-//                   packed key the table is already in order on;
+//   k_sort_layout   per table: the key bits that vary over the table as at
+//                   most 8 runs of bits, most significant first (the others
+//                   cannot decide any order), and the index width; config 3's
+//                   composite u128 keys (account id, timestamp) pack into
+//                   ~34 bits above an 18-bit index;
+//   k_sort_pack     per tile: the words, the digit histograms of every packed
+//                   digit, and which low-order digit prefixes the table is
+//                   already in order on;
 //   k_sort_plan     per table: LSD passes run from the least significant
-//                   byte up, so the bytes of a prefix the table is already
+//                   digit up, so the digits of a prefix the table is already
 //                   in order on (a secondary index put in timestamp order)
 //                   cannot change the stable order and are skipped; each
-//                   remaining pass's source buffer; every digit's start;
-//   k_sort_pass x P one launch per potential pass (P = 8 per key limb of the
-//                   batch's widest key), persistent workgroups; a pass no
-//                   table needs returns at once. Onesweep: each tile ranks
-//                   its items by digit (wave match ballots + per-wave counts:
-//                   stable), publishes its digit counts, looks back over the
-//                   tiles before it in its table for their prefix (decoupled
+//                   remaining pass's digit; every digit's start;
+//   k_sort_pass x P persistent workgroups (tickets); a pass no table needs
+//                   returns at once. Onesweep: each tile ranks its items by
+//                   digit (wave match ballots + per-wave counts: stable),
+//                   publishes its digit counts, looks back over the tiles
+//                   before it in its table for their prefix (decoupled
 //                   look-back), and writes the tile out through LDS so each
-//                   digit's run is contiguous; a table's last pass moves
-//                   the values themselves (values[i] = copy[idx[i]]).
+//                   digit's run is contiguous;
+//   k_sort_finish   values[i] = copy[index of sorted word i] (a gather with
+//                   every workgroup's loads in flight, apart from the passes'
+//                   register and LDS footprint).
 //
 // Tiles never straddle tables, so a table's passes are independent of the
 // others' (a segmented sort with no table digit). Tables whose puts arrived
-// in order are left untouched (table_memory.zig:141).
+// in order are left untouched (table_memory.zig:141). Keys wider than the
+// word holds are sorted on their top bits and each run of equal top bits is
+// ordered by the full key (k_sort_finish; k_sort_rescue if a run is long).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -49,13 +56,15 @@ namespace tbc {
 
 constexpr uint32_t kSortThreads = 256;
 constexpr uint32_t kSortWaves = kSortThreads / 64;
-constexpr uint32_t kSortRounds = 8;
-constexpr uint32_t kSortTile = kSortThreads * kSortRounds; // 2,048 items
+constexpr uint32_t kSortRounds = 16;
+constexpr uint32_t kSortTile = kSortThreads * kSortRounds; // 4,096 items
 constexpr uint32_t kRadix = 256;
 constexpr uint32_t kMaxLimbs = 3;
-constexpr uint32_t kMaxPasses = 8 * kMaxLimbs;
-constexpr uint32_t kTopBytes = 4;   // truncated sorts keep at least this many top bytes
-constexpr uint32_t kRunMax = 64;    // longest run of equal top bytes k_sort_fixup orders
+constexpr uint32_t kMaxPasses = 8;  // 8-bit digits of a 64-bit word
+constexpr uint32_t kMaxBytes = 8 * kMaxLimbs;
+constexpr uint32_t kMaxRuns = 8;    // bit runs of a packed key
+constexpr uint32_t kTopDigits = 4;  // truncated sorts keep at least this many top digits
+constexpr uint32_t kRunMax = 64;    // longest run of equal top bits k_sort_finish orders
 constexpr uint32_t kDirectPasses = 6; // passes with a launch each; the rest share k_sort_pass_rest
 
 // Look-back words (64-bit): the pass launch's epoch in the top half (words
@@ -73,16 +82,22 @@ struct SortSeg {
     uint32_t kl; // key limbs of the table's key kind
     uint32_t item_base, tile_base, tiles;
     uint32_t unsorted;  // some adjacent pair is out of key order (extract)
-    uint32_t nbytes;    // varying key bytes = packed key bytes (layout)
-    uint32_t viol;      // bit b: out of order on packed bytes [0, b] (pack)
+    uint32_t ib;        // index bits: word = packed key << ib | index (layout)
+    uint32_t kbits;     // packed key bits (<= 64 - ib)
+    uint32_t trunc;     // the key varies in more bits than the word holds: its lowest were dropped
+    uint32_t ndig;      // 8-bit digits of the packed key (0: in order, untouched)
+    uint32_t nruns;
+    uint32_t run[kMaxRuns]; // limb | source bit << 8 | width << 16 | packed bit << 24
+    uint32_t nbytes;    // varying key bytes (k_sort_rescue's full sort)
+    uint32_t viol;      // bit j: out of order on packed digits [0, j] (pack)
     uint32_t active;    // bit p: pass p moves this table's items (plan)
-    uint32_t src_bits;  // bit p: pass p reads buffer 1
-    uint32_t final_buf; // buffer the last pass would have written
-    uint32_t skip;      // packed bytes [0, skip): the table is in order on them
-    uint32_t top;       // truncated: passes cover only packed bytes [top, nbytes) (0: not truncated)
-    uint32_t overflow;  // truncated and a run of equal top bytes too long to fix up: rescued
-    uint32_t nact;      // passes of the table: pass q sorts on packed byte act[q]
-    uint8_t byte_src[kMaxPasses]; // packed byte j = key byte byte_src[j] (limb * 8 + byte)
+    uint32_t final_buf; // buffer the last pass wrote
+    uint32_t skip;      // digits [0, skip): the table is in order on them
+    uint32_t top;       // fixup compares packed digits [top, ndig)
+    uint32_t fix;       // runs of equal sorted bits are ordered by k_sort_finish
+    uint32_t overflow;  // such a run too long to fix up: rescued
+    uint32_t nact;      // passes of the table: pass q sorts on digit act[q]
+    uint8_t byte_src[kMaxBytes]; // rescue: packed byte j = key byte byte_src[j] (limb * 8 + byte)
     uint8_t act[kMaxPasses];
 };
 
@@ -98,6 +113,19 @@ __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t
     case kKeyCompositeU64: k[0] = gld<uint64_t>(v + 8) & ~kTombstoneBit; k[1] = gld<uint64_t>(v); break;
     default: k[0] = gld<uint64_t>(v + 16) & ~kTombstoneBit; k[1] = gld<uint64_t>(v); k[2] = gld<uint64_t>(v + 8); break;
     }
+}
+
+__host__ __device__ __forceinline__ uint64_t low_mask(uint32_t bits) { return bits >= 64 ? ~0ull : (1ull << bits) - 1; }
+
+// The packed key: every run's bits at its packed position.
+__device__ __forceinline__ uint64_t pack_bits(const uint32_t *runs, uint32_t nr, const uint64_t k[3]) {
+    uint64_t p = 0;
+    for (uint32_t r = 0; r < nr; r++) {
+        const uint32_t d = runs[r], limb = d & 3, src = (d >> 8) & 63, w = (d >> 16) & 127, at = d >> 24;
+        const uint64_t x = limb == 0 ? k[0] : limb == 1 ? k[1] : k[2];
+        p |= ((x >> src) & low_mask(w)) << at;
+    }
+    return p;
 }
 
 // hist / bins layout: [segment][pass][digit] u32.
@@ -120,7 +148,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     __shared__ uint32_t s_uns;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t sg = tile_seg[blockIdx.x];
-    const SortSeg S = segs[sg];
+    const SortSeg S = segs[sg]; // a copy: the stores below may not alias it
+    const uint32_t n = S.n, vs = S.vs, kl = S.kl;
     const uint32_t lt = blockIdx.x - S.tile_base;
     if (tid == 0) s_uns = 0;
     __syncthreads();
@@ -128,27 +157,27 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     uint32_t uns = 0;
     for (uint32_t r = 0; r < kSortRounds; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-        if (lt * kSortTile + r * kSortThreads >= S.n) break; // wave-uniform (whole row past the end)
-        const bool in = li < S.n;
+        if (lt * kSortTile + r * kSortThreads >= n) break; // wave-uniform (whole row past the end)
+        const bool in = li < n;
         uint64_t k[3], kn[3];
         row_keys(S, li, in, k, kn);
         if (!in) continue;
-        for (uint32_t b = 0; b < S.vs; b += 128) { // up to 8 loads in flight before their stores
+        for (uint32_t b = 0; b < vs; b += 128) { // up to 8 loads in flight before their stores
             u32x4 v[8];
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
-                if (b + 16 * q < S.vs) v[q] = gld<u32x4>(S.values + (size_t)li * S.vs + b + 16 * q);
+                if (b + 16 * q < vs) v[q] = gld<u32x4>(S.values + (size_t)li * vs + b + 16 * q);
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
-                if (b + 16 * q < S.vs) gst<u32x4>(S.copy + (size_t)li * S.vs + b + 16 * q, v[q]);
+                if (b + 16 * q < vs) gst<u32x4>(S.copy + (size_t)li * vs + b + 16 * q, v[q]);
         }
-        for (uint32_t l = 0; l < S.kl; l++) {
+        for (uint32_t l = 0; l < kl; l++) {
             o[l] |= k[l];
             a[l] &= k[l];
         }
-        if (li + 1 < S.n) {
+        if (li + 1 < n) {
             int cmp = 0;
-            for (uint32_t l = 0; l < S.kl; l++)
+            for (uint32_t l = 0; l < kl; l++)
                 if (k[l] != kn[l]) cmp = k[l] > kn[l] ? 1 : -1;
             uns |= cmp > 0 ? 1u : 0u;
         }
@@ -165,7 +194,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     }
     if (uns) atomicOr(&s_uns, 1u);
     __syncthreads();
-    if (tid < S.kl) {
+    if (tid < kl) {
         uint64_t oo = 0, aa = ~0ull;
         for (uint32_t w = 0; w < kSortWaves; w++) {
             oo |= s_or[tid][w];
@@ -177,25 +206,79 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     if (tid == 0 && s_uns) atomicOr(&segs[sg].unsorted, 1u);
 }
 
-// Layout: one thread per table — its varying key bytes, least significant first.
-__global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs, uint32_t nseg) {
-    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
-    if (s >= nseg) return;
-    SortSeg &S = segs[s];
+// Layout: one workgroup (its first thread) per table. The varying bits of every limb, most
+// significant limb and bit first, as runs of consecutive bits; while there
+// are more than kMaxRuns, the two same-limb runs with the smallest gap merge
+// (the constant bits between them are kept: they cannot decide any order).
+// The word holds 64 - ib key bits: beyond that, the lowest are dropped
+// (trunc) and k_sort_finish orders the resulting runs of equal words.
+__global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs) {
+    __shared__ uint8_t rl[kMaxLimbs * 32], rs[kMaxLimbs * 32], rw[kMaxLimbs * 32]; // LDS, not scratch
+    if (threadIdx.x) return;
+    SortSeg &S = segs[blockIdx.x];
+    S.nbytes = S.ndig = S.nruns = 0;
+    if (!S.unsorted) return;
     uint32_t nb = 0;
-    if (S.unsorted)
-        for (uint32_t l = 0; l < S.kl; l++)
-            for (uint32_t b = 0; b < 8; b++)
-                if (((S.key_or[l] ^ S.key_and[l]) >> (8 * b)) & 255) S.byte_src[nb++] = (uint8_t)(8 * l + b);
+    for (uint32_t l = 0; l < S.kl; l++)
+        for (uint32_t b = 0; b < 8; b++)
+            if (((S.key_or[l] ^ S.key_and[l]) >> (8 * b)) & 255) S.byte_src[nb++] = (uint8_t)(8 * l + b);
     S.nbytes = nb;
-}
-
-__device__ __forceinline__ void pack_key(const uint8_t *map, uint32_t nb, const uint64_t k[3], uint64_t pk[3]) {
-    pk[0] = pk[1] = pk[2] = 0;
-    for (uint32_t j = 0; j < nb; j++) {
-        const uint32_t src = map[j];
-        pk[j >> 3] |= ((k[src >> 3] >> (8 * (src & 7))) & 255ull) << (8 * (j & 7));
+    // Runs (limb, lowest bit, width), most significant first.
+    uint32_t nr = 0;
+    for (int l = (int)S.kl - 1; l >= 0; l--) {
+        uint64_t m = S.key_or[l] ^ S.key_and[l];
+        while (m) {
+            const uint32_t hi = 63 - __builtin_clzll(m);
+            const uint64_t gaps = ~m & low_mask(hi + 1); // clear bits at or below hi
+            const uint32_t lo = gaps ? 64 - __builtin_clzll(gaps) : 0;
+            rl[nr] = (uint8_t)l;
+            rs[nr] = (uint8_t)lo;
+            rw[nr] = (uint8_t)(hi - lo + 1);
+            nr++;
+            m &= low_mask(lo);
+        }
     }
+    while (nr > kMaxRuns) {
+        uint32_t best = 0, gap = ~0u;
+        for (uint32_t r = 0; r + 1 < nr; r++)
+            if (rl[r] == rl[r + 1] && rs[r] - (rs[r + 1] + rw[r + 1]) < gap) {
+                gap = rs[r] - (rs[r + 1] + rw[r + 1]);
+                best = r;
+            }
+        if (gap == ~0u) break; // cannot happen with <= 3 limbs (some limb has 3 runs)
+        rw[best] = (uint8_t)(rs[best] + rw[best] - rs[best + 1]);
+        rs[best] = rs[best + 1];
+        for (uint32_t r = best + 1; r + 1 < nr; r++) {
+            rl[r] = rl[r + 1];
+            rs[r] = rs[r + 1];
+            rw[r] = rw[r + 1];
+        }
+        nr--;
+    }
+    const uint32_t ib = 32 - __builtin_clz(S.n - 1); // S.n >= 2
+    uint32_t v = 0;
+    for (uint32_t r = 0; r < nr; r++) v += rw[r];
+    S.trunc = 0;
+    while (v > 64 - ib) { // drop the lowest bits
+        S.trunc = 1;
+        const uint32_t cut = v - (64 - ib);
+        if (rw[nr - 1] <= cut) {
+            v -= rw[--nr];
+        } else {
+            rs[nr - 1] = (uint8_t)(rs[nr - 1] + cut);
+            rw[nr - 1] = (uint8_t)(rw[nr - 1] - cut);
+            v -= cut;
+        }
+    }
+    uint32_t at = v;
+    for (uint32_t r = 0; r < nr; r++) {
+        at -= rw[r];
+        S.run[r] = rl[r] | (uint32_t)rs[r] << 8 | (uint32_t)rw[r] << 16 | at << 24;
+    }
+    S.nruns = nr;
+    S.ib = ib;
+    S.kbits = v;
+    S.ndig = (v + 7) / 8;
 }
 
 // One wave's 64 digits into an LDS histogram row: a digit shared by the
@@ -221,81 +304,73 @@ __device__ __forceinline__ void hist_add(uint32_t *row, uint32_t d, bool in) {
 }
 
 // Pack: one workgroup per tile of an unsorted table.
-__global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const uint32_t *tile_seg, uint32_t N,
-                                                            uint64_t *keys, uint32_t *idx, uint32_t *hist) {
+__global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const uint32_t *tile_seg,
+                                                            uint64_t *words, uint32_t *hist) {
     __shared__ uint32_t s_hist[kMaxPasses][kRadix];
+    __shared__ uint32_t s_run[kMaxRuns]; // read per item: LDS, not scratch
     __shared__ uint32_t s_viol;
     const uint32_t tid = threadIdx.x;
     const uint32_t sg = tile_seg[blockIdx.x];
-    const SortSeg S = segs[sg];
-    const uint32_t nb = S.nbytes;
-    if (!nb) return; // uniform: a sorted table
-    __shared__ uint8_t s_map[kMaxPasses]; // the byte map is read per item: LDS, not scratch
-    const uint32_t pl = (nb + 7) >> 3;
-    for (uint32_t j = 0; j < nb; j++) s_hist[j][tid] = 0;
-    if (tid < kMaxPasses) s_map[tid] = segs[sg].byte_src[tid];
+    const SortSeg S = segs[sg]; // a copy: the stores below may not alias it
+    const uint32_t nd = S.ndig, nr = S.nruns, ib = S.ib, n = S.n;
+    if (!nd) return; // uniform: a sorted table
+    for (uint32_t j = 0; j < nd; j++) s_hist[j][tid] = 0;
+    if (tid < kMaxRuns) s_run[tid] = S.run[tid];
     if (tid == 0) s_viol = 0;
     __syncthreads();
     const uint32_t lt = blockIdx.x - S.tile_base;
     uint32_t viol = 0;
     for (uint32_t r = 0; r < kSortRounds; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-        if (lt * kSortTile + r * kSortThreads >= S.n) break; // uniform
-        const bool in = li < S.n;
-        uint64_t k[3], kn[3], pk[3], pn[3];
+        if (lt * kSortTile + r * kSortThreads >= n) break; // uniform
+        const bool in = li < n;
+        uint64_t k[3], kn[3];
         row_keys(S, li, in, k, kn);
-        pack_key(s_map, nb, k, pk);
-        const uint32_t i = S.item_base + li;
-        if (in) {
-            for (uint32_t l = 0; l < pl; l++) keys[(size_t)l * N + i] = pk[l];
-            idx[i] = i;
-        }
-        for (uint32_t j = 0; j < nb; j++) hist_add(s_hist[j], (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u, in);
-        if (in && li + 1 < S.n) {
-            pack_key(s_map, nb, kn, pn);
-            int cmp = 0; // order of (item, next) on packed bytes [0, j]
-            for (uint32_t j = 0; j < nb; j++) {
-                const uint32_t x = (uint32_t)(pk[j >> 3] >> (8 * (j & 7))) & 255u;
-                const uint32_t y = (uint32_t)(pn[j >> 3] >> (8 * (j & 7))) & 255u;
-                if (x != y) cmp = x > y ? 1 : -1;
-                if (cmp > 0) viol |= 1u << j;
+        const uint64_t p = pack_bits(s_run, nr, k);
+        if (in) gst<uint64_t>(words + S.item_base + li, p << ib | li);
+        for (uint32_t j = 0; j < nd; j++) hist_add(s_hist[j], (uint32_t)(p >> (8 * j)) & 255u, in);
+        if (in && li + 1 < n) {
+            const uint64_t q = pack_bits(s_run, nr, kn);
+            for (uint32_t j = 0; j < nd; j++) { // out of order on digits [0, j]: the low 8(j+1) bits
+                const uint64_t m = low_mask(8 * (j + 1));
+                if ((p & m) > (q & m)) viol |= 1u << j;
             }
         }
     }
     if (viol) atomicOr(&s_viol, viol);
     __syncthreads();
     uint32_t *h = seg_hist(hist, sg);
-    for (uint32_t j = 0; j < nb; j++)
+    for (uint32_t j = 0; j < nd; j++)
         if (s_hist[j][tid]) atomicAdd(&h[j * kRadix + tid], s_hist[j][tid]);
     if (tid == 0 && s_viol) atomicOr(&segs[sg].viol, s_viol);
 }
 
-// Plan: one workgroup per table. Passes [skip, nbytes) run, where the table
-// is already in order on packed bytes [0, skip) (the largest such prefix);
-// then the digit starts of those passes.
+// Plan: one workgroup per table. Passes [skip, ndig) run, where the table
+// is already in order on digits [0, skip) (the largest such prefix); then
+// the digit starts of those passes.
 __global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *batch, const uint32_t *hist,
                                                       uint32_t *bins) {
     const uint32_t s = blockIdx.x, d = threadIdx.x, lane = d & 63, wave = d >> 6;
     __shared__ uint32_t wsum[kRadix / 64];
     SortSeg &S = segs[s];
-    const uint32_t nb = S.nbytes;
+    const uint32_t nd = S.ndig;
     uint32_t skip = 0;
-    for (uint32_t j = 1; j < nb; j++)
+    for (uint32_t j = 1; j < nd; j++)
         if (!((S.viol >> (j - 1)) & 1u)) skip = j;
-    // Many varying bytes (random u64/u128 fields): sort on the top bytes
-    // only (at least kTopBytes, 10 bits beyond log2 n) and let k_sort_fixup
-    // order each run of equal top bytes by the full key -- when the top
-    // bytes' histograms predict short runs: n x prod(largest digit share)
-    // <= 1 if the bytes were independent. Clustered keys (config 3's Zipf
+    // Many varying digits (random u64/u128 fields): sort on the top digits
+    // only (at least kTopDigits, 10 bits beyond log2 n) and let k_sort_finish
+    // order each run of equal top digits by the full key -- when the top
+    // digits' histograms predict short runs: n x prod(largest digit share)
+    // <= 1 if the digits were independent. Clustered keys (config 3's Zipf
     // accounts) keep every pass; a misprediction costs k_sort_rescue.
     const uint32_t *h = hist + (size_t)s * kMaxPasses * kRadix;
     const uint32_t log2n = 32 - __builtin_clz(S.n | 1);
-    const uint32_t top_bytes = (log2n + 10 + 7) / 8 > kTopBytes ? (log2n + 10 + 7) / 8 : kTopBytes;
+    const uint32_t top_digits = (log2n + 10 + 7) / 8 > kTopDigits ? (log2n + 10 + 7) / 8 : kTopDigits;
     uint32_t first = skip;
-    if (nb - skip > top_bytes) {
+    if (nd - skip > top_digits) {
         __shared__ uint32_t wmax[kRadix / 64];
         float est = (float)S.n;
-        for (uint32_t b = nb - top_bytes; b < nb; b++) {
+        for (uint32_t b = nd - top_digits; b < nd; b++) {
             uint32_t mx = h[b * kRadix + d];
             for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
             if (lane == 0) wmax[wave] = mx;
@@ -304,19 +379,20 @@ __global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *
             __syncthreads();
             est *= (float)mx / (float)S.n;
         }
-        if (est <= 1.0f) first = nb - top_bytes;
+        if (est <= 1.0f) first = nd - top_digits;
     }
     uint32_t active = 0;
-    for (uint32_t p = first; p < nb; p++) active |= 1u << p;
+    for (uint32_t p = first; p < nd; p++) active |= 1u << p;
     __syncthreads(); // every thread has read viol before thread 0 writes the plan
     if (d == 0) {
         S.active = active;
-        S.nact = nb - first;
-        for (uint32_t q = 0; q < nb - first; q++) S.act[q] = (uint8_t)(first + q);
-        S.final_buf = (nb - first) & 1u;
+        S.nact = nd - first;
+        for (uint32_t q = 0; q < nd - first; q++) S.act[q] = (uint8_t)(first + q);
+        S.final_buf = (nd - first) & 1u;
         S.skip = skip;
         S.top = first > skip ? first : 0;
-        if (nb > first) atomicOr(&batch->active, (1u << (nb - first)) - 1u); // pass q runs if some table has > q
+        S.fix = (first > skip || S.trunc) ? 1u : 0u;
+        if (nd > first) atomicOr(&batch->active, (1u << (nd - first)) - 1u); // pass q runs if some table has > q
     }
     uint32_t *out = bins + (size_t)s * kMaxPasses * kRadix;
     for (uint32_t m = active; m; m &= m - 1) {
@@ -337,7 +413,7 @@ __global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *
 }
 
 // --------------------------------------------------------------------------
-// One onesweep pass (digit = packed byte p: byte p & 7 of packed limb p >> 3).
+// One onesweep pass (digit = packed digit act[p] of the table's words).
 // --------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -346,20 +422,18 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Persistent workgroups take tiles in arrival order (dynamic ids): every
+// Persistent workgroups take tiles in ticket order when they are free: every
 // tile one looks back on was taken by a workgroup that is running or done.
-// The tile is reordered through LDS one key limb at a time (16 KiB), so the
-// workgroup's LDS does not grow with the key width (5 workgroups per CU).
-// A table's last pass moves the values themselves (values[dst] =
-// copy[index]) instead of keys and indices: the gather is fused into it.
+// (Taking the next ticket one tile ahead, to hide its round trip, measured
+// slower: config 3's passes 58 vs 44 us, as a reserved tile's successors
+// wait on it for a whole tile.)
 struct PassShared {
-    uint32_t tile;
+    uint32_t next;
     uint32_t wcnt[kSortWaves][kRadix]; // per wave: running, then total counts
     uint32_t start[kRadix];            // local start of each digit in the tile
-    uint32_t excl[kRadix];             // items of the digit in the table's earlier tiles
+    uint32_t off[kRadix];              // destination of the digit's tile-local position 0 (mod 2^32)
     uint32_t wsum[kSortWaves];
-    uint64_t key[kSortTile];           // one limb at a time
-    uint32_t idx[kSortTile];
+    uint64_t word[kSortTile];
     uint8_t dig[kSortTile];
 };
 
@@ -369,36 +443,33 @@ struct PassShared {
 // p a workgroup waits for done[p - 1] == ntiles and acquires (the pass reads
 // what every tile of the previous pass wrote, on any XCD).
 __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *segs, const uint32_t *tile_seg,
-                                                const uint32_t *tile_order, uint32_t p, uint32_t ntiles, uint32_t N,
-                                                uint64_t *keys0, uint64_t *keys1, uint32_t *idx0, uint32_t *idx1,
-                                                const uint32_t *bins, uint64_t *status, uint32_t epoch,
-                                                uint32_t *tile_counter, uint32_t *done) {
+                                                const uint32_t *tile_order, uint32_t p, uint32_t ntiles,
+                                                uint64_t *words0, uint64_t *words1, const uint32_t *bins,
+                                                uint64_t *status, uint32_t epoch, uint32_t *tile_counter,
+                                                uint32_t *done) {
     constexpr uint32_t R = kSortRounds;
-    auto &s_tile = sh.tile;
-    auto &s_wcnt = sh.wcnt;
-    auto &s_start = sh.start;
-    auto &s_excl = sh.excl;
-    auto &s_wsum = sh.wsum;
-    auto &s_key = sh.key;
-    auto &s_idx = sh.idx;
-    auto &s_dig = sh.dig;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t ep = (uint64_t)epoch << 32;
     const uint64_t lt_mask = (1ull << lane) - 1;
     // The first pass of the rest kernel follows a kernel boundary: nothing to wait for.
     bool waited = done == nullptr || p == kDirectPasses;
+    const bool from1 = (p & 1u) != 0; // passes alternate buffers, the first reads buffer 0
+    const uint64_t *src = from1 ? words1 : words0;
+    uint64_t *dstw = from1 ? words0 : words1;
     for (bool first = true;; first = false) {
         // Every wave releases its own stores of the previous tile (at agent
         // scope: waits for them and writes the XCD's L2 back) before the
         // tile is counted as done.
         if (!first && done) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __syncthreads(); // the previous tile's LDS readers are done
+        __syncthreads(); // the previous tile's LDS readers are done; sh.next is written
         if (!first && done && tid == 0)
             __hip_atomic_fetch_add(&done[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) s_tile = atomicAdd(&tile_counter[p], 1u);
-        for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
+        if (tid == 0) sh.next = atomicAdd(&tile_counter[p], 1u);
         __syncthreads();
-        if (s_tile >= ntiles) return;
+        const uint32_t tile = sh.next;
+        if (tile >= ntiles) return; // uniform
+        for (uint32_t i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&sh.wcnt[0][0])[i] = 0;
+        __syncthreads(); // every thread has read sh.next
         if (!waited) { // rest kernel: every tile of pass p - 1 is complete and visible
             if (tid == 0) {
                 for (uint32_t spins = 0; __hip_atomic_load(&done[p - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -411,39 +482,33 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
             __syncthreads();
             waited = true;
         }
-        const uint32_t t = tile_order[s_tile];
+        const uint32_t t = tile_order[tile];
         const uint32_t sg = tile_seg[t];
         const SortSeg &S = segs[sg];
         const uint32_t nact = S.nact;
         if (p >= nact) continue; // uniform: the table's passes are done (or it is in order)
-        const bool last = p + 1 == nact && S.top == 0; // truncated tables finish in k_sort_fixup
-        const uint32_t pb = S.act[p];                   // this pass's packed byte for the table
-        const uint32_t limb = pb >> 3, shift = 8 * (pb & 7);
+        const uint32_t pd = S.act[p];              // this pass's digit for the table
+        const uint32_t shift = S.ib + 8 * pd;
         const uint32_t lt = t - S.tile_base;
         const uint32_t base = S.item_base + lt * kSortTile;
         const uint32_t m = (S.n - lt * kSortTile) < kSortTile ? (S.n - lt * kSortTile) : kSortTile;
-        const uint32_t live = ((S.nbytes + 7) >> 3) - limb; // packed limbs [limb, ..) still move
-        const bool from1 = (p & 1u) != 0; // passes alternate buffers, the first reads buffer 0
-        const uint64_t *ksrc = from1 ? keys1 : keys0;
-        uint64_t *kdst = from1 ? keys0 : keys1;
-        const uint32_t *isrc = from1 ? idx1 : idx0;
-        uint32_t *idst = from1 ? idx0 : idx1;
+        const uint32_t bin_d = bins[((size_t)sg * kMaxPasses + pd) * kRadix + tid]; // thread = digit (below)
 
-        // Wave w owns items [512 w, 512 w + 512) of the tile, 64 per round in
-        // lane order: stable rank = (earlier waves) + (earlier rounds of this
-        // wave, counted in s_wcnt) + (earlier lanes with the same digit).
-        uint32_t rank[R], dig[R], ix[R];
-        uint64_t k[R][kMaxLimbs];
+        // Wave w owns items [1024 w, 1024 w + 1024) of the tile, 64 per round
+        // in lane order: stable rank = (earlier waves) + (earlier rounds of
+        // this wave, counted in wcnt) + (earlier lanes with the same digit).
+        uint32_t rd[R]; // rank << 8 | digit
+        uint64_t w[R];
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = wave * (64 * R) + r * 64 + lane;
+            w[r] = e < m ? gld<uint64_t>(src + base + e) : 0ull;
+        }
 #pragma unroll
         for (uint32_t r = 0; r < R; r++) {
             const uint32_t e = wave * (64 * R) + r * 64 + lane;
             const bool in = e < m;
-#pragma unroll
-            for (uint32_t l = 0; l < kMaxLimbs; l++)
-                k[r][l] = in && l < live ? gld<uint64_t>(ksrc + (size_t)(limb + l) * N + base + e) : 0ull;
-            ix[r] = in ? gld<uint32_t>(isrc + base + e) : 0u;
-            const uint32_t d = in ? (uint32_t)(k[r][0] >> shift) & 255u : 0u;
-            dig[r] = d;
+            const uint32_t d = in ? (uint32_t)(w[r] >> shift) & 255u : 0u;
             uint64_t peers = __ballot(in);
 #pragma unroll
             for (uint32_t b = 0; b < 8; b++) {
@@ -451,13 +516,13 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
                 peers &= ((d >> b) & 1u) ? bal : ~bal;
             }
             const uint32_t before = __builtin_popcountll(peers & lt_mask);
-            const uint32_t prior = in ? s_wcnt[wave][d] : 0u;
+            const uint32_t prior = in ? sh.wcnt[wave][d] : 0u;
             __builtin_amdgcn_wave_barrier();
-            if (in && before == 0) s_wcnt[wave][d] = prior + (uint32_t)__builtin_popcountll(peers);
+            if (in && before == 0) sh.wcnt[wave][d] = prior + (uint32_t)__builtin_popcountll(peers);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            rank[r] = prior + before;
+            rd[r] = (prior + before) << 8 | d;
         }
         __syncthreads();
         // Per digit (thread d): counts of the tile, exclusive prefix over
@@ -465,9 +530,9 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
         const uint32_t d = tid;
         uint32_t cnt = 0, wpre[kSortWaves];
 #pragma unroll
-        for (uint32_t w = 0; w < kSortWaves; w++) {
-            wpre[w] = cnt;
-            cnt += s_wcnt[w][d];
+        for (uint32_t v = 0; v < kSortWaves; v++) {
+            wpre[v] = cnt;
+            cnt += sh.wcnt[v][d];
         }
         {
             uint32_t incl = cnt;
@@ -475,15 +540,27 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
                 const uint32_t y = __shfl_up(incl, o, 64);
                 if (lane >= (uint32_t)o) incl += y;
             }
-            if (lane == 63) s_wsum[wave] = incl;
+            if (lane == 63) sh.wsum[wave] = incl;
             __syncthreads();
             uint32_t off = 0;
-            for (uint32_t w = 0; w < wave; w++) off += s_wsum[w];
-            s_start[d] = off + incl - cnt;
+            for (uint32_t v = 0; v < wave; v++) off += sh.wsum[v];
+            sh.start[d] = off + incl - cnt;
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t w = 0; w < kSortWaves; w++) s_wcnt[w][d] = wpre[w]; // becomes the wave's offset
+        for (uint32_t v = 0; v < kSortWaves; v++) sh.wcnt[v][d] = wpre[v]; // becomes the wave's offset
+        __syncthreads(); // every digit's wave offsets are in place
+        // Tile-local sorted position of every item; words and digits into LDS.
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t e = wave * (64 * R) + r * 64 + lane;
+            if (e < m) {
+                const uint32_t dg = rd[r] & 255u;
+                const uint32_t pos = sh.start[dg] + sh.wcnt[wave][dg] + (rd[r] >> 8);
+                sh.word[pos] = w[r];
+                sh.dig[pos] = (uint8_t)dg;
+            }
+        }
         // Decoupled look-back over the table's earlier tiles, one digit per thread.
         uint32_t excl = 0;
         if (lt == 0) {
@@ -498,21 +575,21 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
             for (uint32_t spins = 0;;) {
                 uint64_t v[kLook];
 #pragma unroll
-                for (uint32_t w = 0; w < kLook; w++)
-                    v[w] = pred >= S.tile_base + w ? lb_load(&status[(size_t)(pred - w) * kRadix + d]) : 0ull;
-                bool done = false, stall = false;
+                for (uint32_t i = 0; i < kLook; i++)
+                    v[i] = pred >= S.tile_base + i ? lb_load(&status[(size_t)(pred - i) * kRadix + d]) : 0ull;
+                bool fin = false, stall = false;
 #pragma unroll
-                for (uint32_t w = 0; w < kLook; w++) {
-                    if (done || stall) continue;
-                    if ((v[w] >> 32) != epoch || !(v[w] & (3ull << 30))) { // not published by this pass yet
+                for (uint32_t i = 0; i < kLook; i++) {
+                    if (fin || stall) continue;
+                    if ((v[i] >> 32) != epoch || !(v[i] & (3ull << 30))) { // not published by this pass yet
                         stall = true;
-                        pred -= w;
+                        pred -= i;
                         continue;
                     }
-                    excl += (uint32_t)(v[w] & kCountMask);
-                    if ((v[w] & (3ull << 30)) == kFlagPrefix || pred - w == S.tile_base) done = true;
+                    excl += (uint32_t)(v[i] & kCountMask);
+                    if ((v[i] & (3ull << 30)) == kFlagPrefix || pred - i == S.tile_base) fin = true;
                 }
-                if (done) break;
+                if (fin) break;
                 if (stall) {
                     if (++spins > (1u << 24)) break; // bounded (a broken invariant, not a hang)
                     __builtin_amdgcn_s_sleep(1);
@@ -522,127 +599,67 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
             }
             lb_store(&status[(size_t)t * kRadix + d], ep | kFlagPrefix | (excl + cnt));
         }
-        s_excl[d] = excl;
-        __syncthreads();
-        // Tile-local sorted position of every item; indices and digits into LDS.
-        uint32_t pos[R];
-#pragma unroll
-        for (uint32_t r = 0; r < R; r++) {
-            const uint32_t e = wave * (64 * R) + r * 64 + lane;
-            pos[r] = s_start[dig[r]] + s_wcnt[wave][dig[r]] + rank[r];
-            if (e < m) {
-                s_idx[pos[r]] = ix[r];
-                s_dig[pos[r]] = (uint8_t)dig[r];
-            }
-        }
-        __syncthreads();
-        // Destination of sorted position j = tid + 256 q: each digit's run
+        sh.off[d] = bin_d + excl - sh.start[d];
+        __syncthreads(); // every digit's destination is in place
+        // Sorted position j (digit dj) goes to off[dj] + j: each digit's run
         // lands contiguously.
-        const uint32_t *bin = bins + ((size_t)sg * kMaxPasses + pb) * kRadix;
-        uint32_t dst[R];
-#pragma unroll
+#pragma unroll 4
         for (uint32_t q = 0; q < R; q++) {
             const uint32_t j = tid + kSortThreads * q;
-            const uint32_t dj = j < m ? s_dig[j] : 0u;
-            dst[q] = bin[dj] + s_excl[dj] + (j - s_start[dj]);
-        }
-        if (last) {
-            // values[dst] = copy[index]: 16 bytes per lane, a lane group per value.
-            const uint32_t cpv = S.vs >> 4, vpr = kSortThreads / cpv; // values per row of the workgroup
-            for (uint32_t j0 = 0; j0 < m; j0 += vpr) {
-                const uint32_t j = j0 + tid / cpv, part = tid % cpv;
-                if (j < m) {
-                    const uint32_t dj = s_dig[j];
-                    const uint32_t to = bin[dj] + s_excl[dj] + (j - s_start[dj]) - S.item_base;
-                    const uint32_t from = s_idx[j] - S.item_base;
-                    gst<u32x4>(S.values + (size_t)to * S.vs + 16 * part,
-                               gld<u32x4>(S.copy + (size_t)from * S.vs + 16 * part));
-                }
-            }
-            continue;
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < R; q++) {
-            const uint32_t j = tid + kSortThreads * q;
-            if (j < m) gst<uint32_t>(idst + dst[q], s_idx[j]);
-        }
-#pragma unroll
-        for (uint32_t l = 0; l < kMaxLimbs; l++) { // unrolled: k[r][l] stays in registers
-            if (l >= live) break;
-            __syncthreads(); // the previous limb's readers are done
-#pragma unroll
-            for (uint32_t r = 0; r < R; r++) {
-                const uint32_t e = wave * (64 * R) + r * 64 + lane;
-                if (e < m) s_key[pos[r]] = k[r][l];
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t q = 0; q < R; q++) {
-                const uint32_t j = tid + kSortThreads * q;
-                if (j < m) gst<uint64_t>(kdst + (size_t)(limb + l) * N + dst[q], s_key[j]);
-            }
+            if (j < m) gst<uint64_t>(dstw + sh.off[sh.dig[j]] + j, sh.word[j]);
         }
     }
 }
 
 // One launch per pass below kDirectPasses: the kernel boundary orders the
 // passes. A pass no table needs returns at once.
-__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
+__global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
                                                             const uint32_t *tile_seg, const uint32_t *tile_order,
-                                                            uint32_t p, uint32_t ntiles,
-                                                            uint32_t N, uint64_t *keys0, uint64_t *keys1,
-                                                            uint32_t *idx0, uint32_t *idx1, const uint32_t *bins,
-                                                            uint64_t *status, uint32_t epoch,
-                                                            uint32_t *tile_counter) {
+                                                            uint32_t p, uint32_t ntiles, uint64_t *words0,
+                                                            uint64_t *words1, const uint32_t *bins, uint64_t *status,
+                                                            uint32_t epoch, uint32_t *tile_counter) {
     __shared__ PassShared sh;
     if (!((batch->active >> p) & 1u)) return; // uniform: no table has this many passes
-    sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, N, keys0, keys1, idx0, idx1, bins, status, epoch,
-                    tile_counter, nullptr);
+    sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, words0, words1, bins, status, epoch, tile_counter,
+                    nullptr);
 }
 
 // Passes [kDirectPasses, kMaxPasses) in ONE launch (most batches need none:
-// a truncated sort keeps at least 4 bytes, an in-order prefix is skipped):
+// a truncated sort keeps at least 4 digits, an in-order prefix is skipped):
 // workgroups take pass p's tiles after pass p - 1's tickets ran out, so a
 // tile only ever waits on tiles already taken by running workgroups (no
 // grid barrier, no residency assumption), and the completion counters with
 // agent-scope release/acquire order the passes across XCDs. Each pass takes
 // a fresh look-back epoch.
-__global__ __launch_bounds__(kSortThreads) void k_sort_pass_rest(const SortSeg *segs, const SortBatch *batch,
+__global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass_rest(const SortSeg *segs, const SortBatch *batch,
                                                                  const uint32_t *tile_seg, const uint32_t *tile_order,
-                                                                 uint32_t ntiles, uint32_t N, uint64_t *keys0,
-                                                                 uint64_t *keys1, uint32_t *idx0, uint32_t *idx1,
+                                                                 uint32_t ntiles, uint64_t *words0, uint64_t *words1,
                                                                  const uint32_t *bins, uint64_t *status,
                                                                  uint32_t epoch0, uint32_t *tile_counter,
                                                                  uint32_t *done) {
     __shared__ PassShared sh;
     for (uint32_t p = kDirectPasses; p < kMaxPasses; p++) {
         if (!((batch->active >> p) & 1u)) return; // passes run as a prefix: none beyond either
-        sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, N, keys0, keys1, idx0, idx1, bins, status,
+        sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, words0, words1, bins, status,
                         epoch0 + (p - kDirectPasses), tile_counter, done);
+        // Its last tile's stores are released and counted before the next pass.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
     }
 }
 
 // --------------------------------------------------------------------------
-// Truncated tables: the passes ordered the items by their top packed bytes
-// (stable); each run of equal top bytes is put in full-key order here (ties
-// by put order, i.e. by item index: stability), and every value is written.
-// One thread per sorted position; keys are re-read from the put-order copy.
-// A run longer than kRunMax marks the table for k_sort_rescue.
+// Finish: every sorted table's values from its sorted words, 1,024 sorted
+// positions per workgroup. Exact tables gather: values[i] = copy[index of
+// word i] (reads at random, writes in order; eight values' loads in flight
+// per lane before their stores). Fixed-up tables (truncated words, or passes
+// on the top digits only): the passes ordered the words by their digits
+// [top, ndig) (stable); each run of equal such digits is put in full-key order
+// (ties by put order, i.e. by item index: stability), one thread per sorted
+// position, runs found on the sorted words, keys re-read from the put-order
+// copy; a run longer than kRunMax marks the table for k_sort_rescue.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void packed_of(const SortSeg &S, const uint8_t *map, uint32_t item, uint64_t pk[3]) {
-    uint64_t k[3];
-    key_of(S.kind, S.copy + (size_t)item * S.vs, S.ts_off, k);
-    pack_key(map, S.nbytes, k, pk);
-}
-
-__device__ __forceinline__ bool top_eq(const uint64_t a[3], const uint64_t b[3], uint32_t top) {
-    // packed bytes [top, 24): limbs above top's limb whole, top's limb from byte top % 8
-    const uint32_t l0 = top >> 3, sh = 8 * (top & 7);
-    if ((a[l0] >> sh) != (b[l0] >> sh)) return false;
-    for (uint32_t l = l0 + 1; l < 3; l++)
-        if (a[l] != b[l]) return false;
-    return true;
-}
+constexpr uint32_t kFinishItems = 1024;
 
 __device__ __forceinline__ bool key_before(const uint64_t a[3], uint32_t ia, const uint64_t b[3], uint32_t ib) {
     for (int l = 2; l >= 0; l--)
@@ -650,75 +667,95 @@ __device__ __forceinline__ bool key_before(const uint64_t a[3], uint32_t ia, con
     return ia < ib;
 }
 
-__global__ __launch_bounds__(256) void k_sort_fixup(SortSeg *segs, const uint32_t *tile_seg, const uint32_t *idx0,
-                                                    const uint32_t *idx1) {
-    __shared__ uint8_t s_map[kMaxPasses];
-    const uint32_t sg = tile_seg[blockIdx.x];
+__global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32_t *tile_seg, const uint64_t *words0,
+                                                     const uint64_t *words1) {
+    const uint32_t tile = blockIdx.x / (kSortTile / kFinishItems);
+    const uint32_t sg = tile_seg[tile];
     const SortSeg S = segs[sg];
-    if (!S.top) return; // uniform: not truncated
-    if (threadIdx.x < kMaxPasses) s_map[threadIdx.x] = segs[sg].byte_src[threadIdx.x];
-    __syncthreads();
-    const uint32_t *idx = (S.final_buf ? idx1 : idx0) + S.item_base; // table-local sorted order
-    const uint32_t first = (blockIdx.x - S.tile_base) * kSortTile;
-    for (uint32_t r = 0; r < kSortRounds; r++) {
-        const uint32_t i = first + r * kSortThreads + threadIdx.x;
-        if (i >= S.n) break;
-        const uint32_t me = idx[i] - S.item_base;
-        uint64_t pk[3];
-        packed_of(S, s_map, me, pk);
-        // run bounds [lo, hi) of equal top bytes around i
+    if (!S.nact) return; // uniform: in order, untouched
+    const uint64_t *wv = (S.final_buf ? words1 : words0) + S.item_base; // the table's sorted words
+    const uint64_t imask = low_mask(S.ib);
+    const uint32_t n = S.n, vs = S.vs, tid = threadIdx.x;
+    const uint32_t first = (tile - S.tile_base) * kSortTile + (blockIdx.x % (kSortTile / kFinishItems)) * kFinishItems;
+    if (first >= n) return;
+    const uint32_t last = first + kFinishItems < n ? first + kFinishItems : n;
+    if (!S.fix) {
+        const uint32_t cpv = vs >> 4, vpr = 256 / cpv; // values per row of the workgroup
+        const uint32_t jl = tid / cpv, part = tid % cpv;
+        if (jl >= vpr) return;
+        for (uint32_t j0 = first; j0 < last; j0 += 8 * vpr) {
+            u32x4 v[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t j = j0 + q * vpr + jl;
+                if (j < last) v[q] = gld<u32x4>(S.copy + (size_t)(uint32_t)(wv[j] & imask) * vs + 16 * part);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t j = j0 + q * vpr + jl;
+                if (j < last) gst<u32x4>(S.values + (size_t)j * vs + 16 * part, v[q]);
+            }
+        }
+        return;
+    }
+    const uint32_t sh = S.ib + 8 * S.top;
+    for (uint32_t i = first + tid; i < last; i += 256) {
+        const uint64_t wi = wv[i], ti = wi >> sh;
+        // run bounds [lo, hi) of equal top digits around i
         uint32_t lo = i, hi = i + 1;
-        bool too_long = false;
-        while (lo > 0) {
-            uint64_t q[3];
-            packed_of(S, s_map, idx[lo - 1] - S.item_base, q);
-            if (!top_eq(q, pk, S.top)) break;
-            if (i - --lo >= kRunMax) { too_long = true; break; }
-        }
-        while (!too_long && hi < S.n) {
-            uint64_t q[3];
-            packed_of(S, s_map, idx[hi] - S.item_base, q);
-            if (!top_eq(q, pk, S.top)) break;
-            if (++hi - lo > kRunMax) too_long = true;
-        }
-        if (too_long) {
+        while (lo > 0 && (wv[lo - 1] >> sh) == ti && i - lo < kRunMax) lo--;
+        while (hi < n && (wv[hi] >> sh) == ti && hi - lo <= kRunMax) hi++;
+        if (hi - lo > kRunMax) {
             atomicOr(&segs[sg].overflow, 1u);
             continue;
         }
+        const uint32_t me = (uint32_t)(wi & imask);
+        uint64_t k[3];
+        key_of(S.kind, S.copy + (size_t)me * vs, S.ts_off, k);
         uint32_t rank = 0;
         for (uint32_t j = lo; j < hi; j++) {
             if (j == i) continue;
-            const uint32_t other = idx[j] - S.item_base;
+            const uint32_t other = (uint32_t)(wv[j] & imask);
             uint64_t q[3];
-            packed_of(S, s_map, other, q);
-            rank += key_before(q, other, pk, me) ? 1u : 0u;
+            key_of(S.kind, S.copy + (size_t)other * vs, S.ts_off, q);
+            rank += key_before(q, other, k, me) ? 1u : 0u;
         }
         const uint32_t to = lo + rank;
-        for (uint32_t b = 0; b < S.vs; b += 16)
-            gst<u32x4>(S.values + (size_t)to * S.vs + b, gld<u32x4>(S.copy + (size_t)me * S.vs + b));
+        for (uint32_t b = 0; b < vs; b += 16)
+            gst<u32x4>(S.values + (size_t)to * vs + b, gld<u32x4>(S.copy + (size_t)me * vs + b));
     }
 }
 
-// A truncated table whose top bytes left a run too long to fix up (rare:
-// keys clustered in their top bytes): one workgroup sorts it again, all its
+// A fixed-up table whose top bits left a run too long to fix up (rare: keys
+// clustered in their top bits): one workgroup sorts it again, all its
 // varying bytes, LSD from the put-order copy, stable (ranks by wave match
 // ballots within 256-item chunks in order), then writes every value. Slow
-// but correct; the common case never launches work here.
+// but correct; the common case never launches work here. Packed keys of up
+// to three limbs (`keys`, N words per limb) and indices (`idx`) are its own.
+__device__ __forceinline__ void pack_bytes(const uint8_t *map, uint32_t nb, const uint64_t k[3], uint64_t pk[3]) {
+    pk[0] = pk[1] = pk[2] = 0;
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t src = map[j];
+        pk[j >> 3] |= ((k[src >> 3] >> (8 * (src & 7))) & 255ull) << (8 * (j & 7));
+    }
+}
+
 __global__ __launch_bounds__(256) void k_sort_rescue(SortSeg *segs, uint32_t N, uint64_t *keys0, uint64_t *keys1,
                                                      uint32_t *idx0, uint32_t *idx1) {
-    __shared__ uint8_t s_map[kMaxPasses];
+    __shared__ uint8_t s_map[kMaxBytes];
     __shared__ uint32_t s_off[kRadix];
     __shared__ uint32_t s_wc[4][kRadix];
     __shared__ uint32_t s_wsum[4];
     const SortSeg S = segs[blockIdx.x];
     if (!S.overflow) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid < kMaxPasses) s_map[tid] = segs[blockIdx.x].byte_src[tid];
+    if (tid < kMaxBytes) s_map[tid] = segs[blockIdx.x].byte_src[tid];
     __syncthreads();
     const uint32_t nb = S.nbytes, pl = (nb + 7) >> 3, base = S.item_base;
     for (uint32_t i = tid; i < S.n; i += 256) {
-        uint64_t pk[3];
-        packed_of(S, s_map, i, pk);
+        uint64_t k[3], pk[3];
+        key_of(S.kind, S.copy + (size_t)i * S.vs, S.ts_off, k);
+        pack_bytes(s_map, nb, k, pk);
         for (uint32_t l = 0; l < pl; l++) keys0[(size_t)l * N + base + i] = pk[l];
         idx0[base + i] = i;
     }
@@ -726,7 +763,7 @@ __global__ __launch_bounds__(256) void k_sort_rescue(SortSeg *segs, uint32_t N, 
     uint64_t *ks = keys0, *kd = keys1;
     uint32_t *is = idx0, *id = idx1;
     const uint64_t lt = (1ull << lane) - 1;
-    for (uint32_t p = S.skip; p < nb; p++) {
+    for (uint32_t p = 0; p < nb; p++) {
         const uint32_t limb = p >> 3, sh = 8 * (p & 7);
         s_off[tid] = 0;
         __syncthreads();
@@ -792,9 +829,10 @@ static uint64_t align256(uint64_t x) { return (x + 255) / 256 * 256; }
 
 // Scratch layout (sort_scratch_bytes must match launch_sort_batch). The
 // look-back words live in their own buffer (sort_status_words): epochs are
-// only unique there.
+// only unique there. `words` (two buffers of N) are the passes'; the rescue
+// keys (two buffers of N per key limb) and indices are k_sort_rescue's.
 struct SortScratch {
-    uint64_t segs, tile_seg, tile_order, hist, counters, batch, bins, keys, idx, copies, total;
+    uint64_t segs, tile_seg, tile_order, hist, counters, batch, bins, words, keys, idx, copies, total;
 };
 
 static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
@@ -823,6 +861,8 @@ static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
     o += align256(sizeof(SortBatch));
     s.bins = o;
     o += align256(4ull * nseg * kMaxPasses * kRadix);
+    s.words = o;
+    o += 2 * align256(8 * N);
     s.keys = o;
     o += 2 * align256(8 * N * kl);
     s.idx = o;
@@ -861,7 +901,7 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     SortSeg *hsegs = (SortSeg *)(hbase + L.segs);
     uint32_t *htile = (uint32_t *)(hbase + L.tile_seg);
     uint32_t N = 0, nseg = 0, ntiles = 0;
-    uint32_t max_kl = 0;
+    uint32_t max_kl = 0, max_pass = 0;
     uint64_t copy_off = L.copies;
     for (uint32_t j = 0; j < count; j++) {
         const SortItem &it = items[j];
@@ -883,6 +923,11 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         ntiles += g.tiles;
         N += it.n;
         max_kl = max_kl > g.kl ? max_kl : g.kl;
+        // The most passes the table's words can need: its key bits, at most
+        // 64 minus the index bits, in 8-bit digits.
+        const uint32_t ib = 32 - __builtin_clz(it.n - 1);
+        const uint32_t kb = 64 * g.kl < 64 - ib ? 64 * g.kl : 64 - ib;
+        max_pass = max_pass > (kb + 7) / 8 ? max_pass : (kb + 7) / 8;
         hsegs[nseg++] = g;
     }
     if (!nseg) return 0;
@@ -900,6 +945,7 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     SortSeg *d_segs = (SortSeg *)(base + L.segs);
     uint32_t *d_tile = (uint32_t *)(base + L.tile_seg);
     const uint32_t *d_order = (const uint32_t *)(base + L.tile_order);
+    uint64_t *words0 = (uint64_t *)(base + L.words), *words1 = (uint64_t *)(base + L.words + align256(8ull * N));
     const uint64_t klw = align256(8ull * N * max_kl);
     uint64_t *keys0 = (uint64_t *)(base + L.keys), *keys1 = (uint64_t *)(base + L.keys + klw);
     uint32_t *idx0 = (uint32_t *)(base + L.idx), *idx1 = (uint32_t *)(base + L.idx + align256(4ull * N));
@@ -910,12 +956,12 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         hipMemsetAsync(hist, 0, L.bins - L.hist, s) != hipSuccess)
         return -1;
     hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile);
-    hipLaunchKernelGGL(k_sort_layout, dim3((nseg + 63) / 64), dim3(64), 0, s, d_segs, nseg);
-    hipLaunchKernelGGL(k_sort_pack, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, N, keys0, idx0, hist);
+    hipLaunchKernelGGL(k_sort_layout, dim3(nseg), dim3(64), 0, s, d_segs);
+    hipLaunchKernelGGL(k_sort_pack, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, words0, hist);
     hipLaunchKernelGGL(k_sort_plan, dim3(nseg), dim3(kRadix), 0, s, d_segs, d_batch, hist, bins);
-    // Persistent: as many workgroups as are resident at once (VGPRs allow
-    // three per CU): more would only start after the tiles run out, and an
-    // idle pass (no table has that many bytes) costs its launch alone.
+    // Persistent: as many workgroups as are resident at once: more would
+    // only start after the tiles run out, and an idle pass (no table has
+    // that many digits) costs its launch alone.
     static uint32_t resident = 0;
     if (!resident) {
         int per_cu = 0, dev = 0, cus = 0;
@@ -926,21 +972,20 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         resident = (uint32_t)(per_cu * cus);
     }
     const uint32_t pgrid = ntiles < resident ? ntiles : resident;
-    const uint32_t passes = 8 * max_kl;
+    const uint32_t passes = max_pass < kMaxPasses ? max_pass : kMaxPasses;
     for (uint32_t p = 0; p < passes && p < kDirectPasses; p++) {
         if (*epoch == 0) *epoch = 1; // 0 is the zeroed buffer's
         hipLaunchKernelGGL(k_sort_pass, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, d_order, p,
-                           ntiles, N, keys0, keys1, idx0, idx1, bins, status, (*epoch)++, counters);
+                           ntiles, words0, words1, bins, status, (*epoch)++, counters);
     }
     if (passes > kDirectPasses) {
         if (*epoch == 0 || *epoch + kMaxPasses < *epoch) *epoch = 1; // a fresh epoch per pass, none 0
         hipLaunchKernelGGL(k_sort_pass_rest, dim3(pgrid), dim3(kSortThreads), 0, s, d_segs, d_batch, d_tile, d_order,
-                           ntiles, N, keys0, keys1, idx0, idx1, bins, status, *epoch, counters,
-                           counters + kMaxPasses);
+                           ntiles, words0, words1, bins, status, *epoch, counters, counters + kMaxPasses);
         *epoch += kMaxPasses;
     }
-    hipLaunchKernelGGL(k_sort_fixup, dim3(ntiles), dim3(256), 0, s, d_segs, (const uint32_t *)d_tile,
-                       (const uint32_t *)idx0, (const uint32_t *)idx1);
+    hipLaunchKernelGGL(k_sort_finish, dim3(ntiles * (kSortTile / kFinishItems)), dim3(256), 0, s, d_segs,
+                       (const uint32_t *)d_tile, (const uint64_t *)words0, (const uint64_t *)words1);
     hipLaunchKernelGGL(k_sort_rescue, dim3(nseg), dim3(256), 0, s, d_segs, N, keys0, keys1, idx0, idx1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
