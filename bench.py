@@ -55,6 +55,10 @@ class Workload:
         self.input_values = 0
         self.input_bytes = 0
         self.sort_bytes = 0
+        self.out_bytes = 0
+        self.job_args = []
+        self.jobs_alt: list = []
+        self.flip = 0
         base_addr = 1
         for gid in job_ids:
             js = configs.GENERATORS[config](gid)
@@ -102,8 +106,12 @@ class Workload:
             out = eng.alloc(reservation * bs)
             addrs = np.arange(base_addr, base_addr + reservation, dtype=np.uint64)
             base_addr += reservation
+            flags = abi.COMPACTION_UNIQUE_KEYS if js.unique_keys else 0
             self.jobs.append(Job(spec, segs_a, segs_b, js.a_immutable, js.drop_tombstones, js.level_b, 0xA5A5, 48,
-                                 addrs, out, flags=abi.COMPACTION_UNIQUE_KEYS if js.unique_keys else 0))
+                                 addrs, out, flags=flags))
+            self.out_bytes += reservation * bs
+            self.job_args.append((spec, segs_a, segs_b, js.a_immutable, js.drop_tombstones, js.level_b, addrs, flags,
+                                  reservation * bs))
             self.input_values += js.input_values
             self.input_bytes += js.input_bytes
             if not keep_host:  # the bench needs only the shape: free the host copies as it goes
@@ -113,14 +121,31 @@ class Workload:
             self.bufs.append(out)
             del js
 
+    def double_buffer(self, eng: Engine, limit: int = 64 << 30) -> bool:
+        """A second set of output blocks, so that consecutive steps write
+        different blocks and step k+1's fronts may run beside step k's
+        chains (the engine makes a batch wait for an earlier tail only when
+        their outputs alias). Skipped above `limit` bytes of outputs."""
+        if self.out_bytes > limit or self.jobs_alt:
+            return bool(self.jobs_alt)
+        for spec, segs_a, segs_b, a_imm, drop, level_b, addrs, flags, nbytes in self.job_args:
+            out = eng.alloc(nbytes)
+            self.bufs.append(out)
+            self.jobs_alt.append(Job(spec, segs_a, segs_b, a_imm, drop, level_b, 0xA5A5, 48, addrs, out,
+                                     flags=flags))
+        return True
+
     def submit(self, eng: Engine):
         """Land + sort the bar's memtables (config 3), then submit the
-        compaction batch (no wait)."""
-        for dst, src, n in self.landings:
-            eng.copy_device_async(dst, src, n)
+        compaction batch (no wait). With double_buffer(), steps alternate
+        between the two output sets."""
+        if self.landings:
+            eng.copy_device_batch(self.landings)
         if self.sorts:
             eng.sort_values_batch(self.sorts)
-        return eng.submit(self.jobs)
+        jobs = self.jobs_alt if (self.jobs_alt and self.flip) else self.jobs
+        self.flip ^= 1
+        return eng.submit(jobs)
 
     def step(self, eng: Engine):
         """One step; returns the completed batch."""
@@ -228,8 +253,7 @@ class ReplayWorkload:
         for kind, *rest in self.executor.record:
             if kind == "sort":
                 jobs, landings = rest
-                for dst, src, n in landings:
-                    eng.copy_device_async(dst, src, n)
+                eng.copy_device_batch(landings)
                 eng.sort_values_batch(jobs)
             elif kind == "manifest":  # ManifestLog.close_block on the device (manifest.py)
                 images, addresses, prev = rest
@@ -442,6 +466,9 @@ def main() -> None:
     ap.add_argument("--strong", action="store_true",
                     help="config 5: BASELINE's 1B values (216 jobs) divided over the GPUs (strong scaling)")
     ap.add_argument("--no-split", action="store_true", help="config 4 at N > 1: shard whole jobs only")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="wait for each step before submitting the next (default: step k+1 is enqueued before "
+                         "step k is waited for, so the host's submit and wake-up do not idle the GPU)")
     args = ap.parse_args()
     njobs = args.jobs or configs.DEFAULT_JOBS.get(args.config, 1)
 
@@ -490,12 +517,16 @@ def main() -> None:
         wl.input_bytes += part.input_bytes
     eng.synchronize()
 
-    def step():
+    def submit():
+        """Enqueue one step; returns its batch (not waited for)."""
         if part is None:
-            return wl.step(eng)
+            return wl.submit(eng)
         held = []
         part.run(eng, before_phase2=lambda: held.append(wl.submit(eng)))
-        b = held[0] if held else wl.submit(eng)
+        return held[0] if held else wl.submit(eng)
+
+    def step():
+        b = submit()
         b.wait()
         return b
 
@@ -516,12 +547,33 @@ def main() -> None:
     t0 = time.perf_counter()
     ktimes: dict = {}
     marks = []
-    for _ in range(args.steps):
-        b = step()
+
+    def finish(b):
+        b.wait()
         marks.append(time.perf_counter())
         for k, v in b.kernel_times().items():
             ktimes[k] = ktimes.get(k, 0.0) + v
         b.release()
+
+    # Steps run back to back on the engine's streams (the same work each
+    # step, every step's results checked below for the last one). Overlapped:
+    # step k+1 is enqueued before step k is waited for (each batch has its
+    # own arena region and results; stream order keeps the shared outputs
+    # and mask buffer consistent), so the device never idles for the host.
+    # A split step (config 4, N > 1) exchanges between its phases: sequential.
+    overlap = not args.no_overlap and part is None
+    doubled = overlap and wl.double_buffer(eng)
+    pending = None
+    for _ in range(args.steps):
+        b = submit()
+        if not overlap:
+            finish(b)
+            continue
+        if pending is not None:
+            finish(pending)
+        pending = b
+    if pending is not None:
+        finish(pending)
     barrier()
     gc.enable()
     if os.environ.get("TBC_BENCH_TRACE"):
@@ -592,7 +644,8 @@ def main() -> None:
         "config": {"workload": configs.DESCRIPTION[args.config], "baseline_config": args.config,
                    "jobs_per_gpu": njobs, "input_bytes_per_gpu": wl.input_bytes, "block_size": bs,
                    "parallelism": f"shard-by-job x{world}" + (f" + key-range split of job {split_id}"
-                                                                if split_id is not None else "")},
+                                                                if split_id is not None else ""),
+                   "steps_overlapped": overlap, "outputs_double_buffered": doubled},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -257,6 +257,16 @@ tbc_status tbc_copy_to_host(tbc_engine *engine, void *dst, const void *src, uint
 /* Device-to-device copy enqueued on the engine stream (no host wait): e.g.
  * landing a bar's mutable table next to the sort that consumes it. */
 tbc_status tbc_copy_device_async(tbc_engine *engine, void *dst, const void *src, uint64_t bytes);
+/* Many device-to-device copies in ONE launch on the engine stream (no host
+ * wait): e.g. landing every memtable of a bar at once. Copies whose
+ * addresses and size are multiples of 16 bytes go to one kernel; any other
+ * is a copy of its own, in order. The copies must not overlap each other. */
+typedef struct tbc_copy {
+    void *dst;
+    const void *src;
+    uint64_t bytes;
+} tbc_copy;
+tbc_status tbc_copy_device_batch(tbc_engine *engine, const tbc_copy *copies, uint32_t count);
 tbc_status tbc_memset_device(tbc_engine *engine, void *dst, int value, uint64_t bytes);
 tbc_status tbc_synchronize(tbc_engine *engine);
 

@@ -1,0 +1,76 @@
+"""Batches submitted back to back without waiting (as bench.py's timed loop
+does): the second batch writes the same caller-provided output blocks the
+first one's tail streams (chains, in the throughput regime's pipelined
+groups) may still be reading, so its fronts must start after those tails
+(engine.hip tbc_compaction_submit). The outputs must end as the oracle's
+compaction of the SECOND batch's inputs, headers included."""
+import numpy as np
+import pytest
+
+from helpers import disk_image, run_oracle
+from tigerbeetle_amd import trees, workloads
+from tigerbeetle_amd.engine import Job, stage_blocks
+
+BS = 4096
+
+
+def _cases():
+    T = trees.BY_NAME
+    cases = []
+    for i, name in enumerate(["transfers.id", "accounts.timestamp", "transfers.debit_account_id", "accounts.ledger",
+                              "posted.timestamp", "transfers.id", "account_history.timestamp", "transfers.amount"]):
+        base = T[name]
+        spec = trees.with_table_size(base, 6 * (BS - 256) // base.value_size + 1)
+        n = 125 * (BS - 256) // base.value_size
+        cases.append((spec, dict(n_a=n, b_table_sizes=[n // 2] * 7, a_immutable=i % 2 == 1, dup_frac=0.1 * (i % 2),
+                                 tomb_frac=0.05 * (i % 3 != 2), drop_tombstones=i % 4 == 3, overlap=0.2)))
+    return cases
+
+
+def _jobs(engine, inputs, addrs, outs, keep):
+    jobs = []
+    for ji, a, out in zip(inputs, addrs, outs):
+        vcm = engine.layout(ji.tree).block_value_count_max
+        if ji.a_immutable:
+            abuf = engine.upload(ji.a_values)
+            segs_a = [(abuf.ptr, len(ji.a_values))]
+        else:
+            abuf, segs_a = stage_blocks(engine, [workloads.split_blocks(ji.a_values, vcm)], ji.tree.value_size, BS)
+        bbuf, segs_b = stage_blocks(engine, [workloads.split_blocks(t, vcm) for t in ji.b_tables],
+                                    ji.tree.value_size, BS)
+        keep += [abuf, bbuf]
+        jobs.append(Job(ji.tree, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48, a, out))
+    return jobs
+
+
+@pytest.mark.gpu
+def test_back_to_back_batches_share_outputs(engine_small, oracle_lib):
+    cases = _cases()
+    rng1, rng2, rng_a = np.random.default_rng(301), np.random.default_rng(302), np.random.default_rng(303)
+    first = [workloads.make_job_inputs(spec, rng1, **kw) for spec, kw in cases]
+    second = [workloads.make_job_inputs(spec, rng2, **kw) for spec, kw in cases]
+    addrs, outs = [], []
+    for (spec, kw), ji in zip(cases, first):
+        n = len(ji.a_values) + sum(len(t) for t in ji.b_tables)
+        a = workloads.addresses_for(workloads.worst_case_blocks(spec, 2 * n, BS) + 3, rng_a, 1, 0.1)
+        addrs.append(np.asarray(a, dtype=np.uint64))
+        out = engine_small.alloc(len(a) * BS)
+        out.zero()
+        outs.append(out)
+    assert sum(workloads.worst_case_blocks(s, kw["n_a"] * 9 // 2, BS) for s, kw in cases) > 4096  # pipelined groups
+    keep = []
+    b1 = engine_small.submit(_jobs(engine_small, first, addrs, outs, keep))
+    b2 = engine_small.submit(_jobs(engine_small, second, addrs, outs, keep))
+    b1.wait()
+    b2.wait()
+    for i, (ji, a, out) in enumerate(zip(second, addrs, outs)):
+        r, infos = b2.result(i)
+        o = run_oracle(oracle_lib, ji, BS, a)
+        assert r.status == 0 and o.status == 0
+        assert r.block_count == len(o.blocks)
+        got = out.download(r.block_count * BS).reshape(-1, BS)
+        for k, (g, w) in enumerate(zip(got, o.blocks)):
+            assert np.array_equal(disk_image(g), disk_image(w)), (ji.tree.name, k)
+        assert np.array_equal(infos, o.table_infos)
+    b1.release()
+    b2.release()

@@ -86,6 +86,10 @@ class SortJob(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class Copy(ctypes.Structure):
+    _fields_ = [("dst", ctypes.c_void_p), ("src", ctypes.c_void_p), ("bytes", ctypes.c_uint64)]
+
+
 class TableRef(ctypes.Structure):
     _fields_ = [("address", ctypes.c_uint64), ("checksum", ctypes.c_uint64 * 2), ("value_count", ctypes.c_uint64)]
 
@@ -144,6 +148,7 @@ _SIGNATURES = {
     "tbc_checksum_batch": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_uint32, _P]),
     "tbc_copy_device_async": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64]),
+    "tbc_copy_device_batch": (ctypes.c_int, [_P, ctypes.POINTER(Copy), ctypes.c_uint32]),
     "tbc_blocks_validate": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint32, _P]),
     "tbc_sort_values": (ctypes.c_int, [_P, ctypes.POINTER(Tree), _P, ctypes.c_uint32]),
     "tbc_sort_values_async": (ctypes.c_int, [_P, ctypes.POINTER(Tree), _P, ctypes.c_uint32]),

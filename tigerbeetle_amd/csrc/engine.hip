@@ -129,10 +129,22 @@ struct tbc_engine {
     // blocks, input checks and results run on one of them, after its front
     // (merge + bodies) on `stream`; the next batch's front does not wait
     // for them, so consecutive batches' AEGIS chains share the chip. Main +
-    // tails = 4 streams, HIP's hardware queues per process.
-    static constexpr int kTails = 3;
-    hipStream_t tail[kTails] = {};
-    hipEvent_t tail_ev[kTails] = {}; // the last batch finished on each tail
+    // tails = one stream per hardware queue of the process
+    // (GPU_MAX_HW_QUEUES, HIP's default 4): a stream sharing a queue would
+    // inherit another's order.
+    static constexpr int kMaxTails = 8;
+    int ntails = 3;
+    hipStream_t tail[kMaxTails] = {};
+    hipEvent_t tail_ev[kMaxTails] = {}; // the last batch finished on each tail
+    // Caller-provided output ranges [lo, hi) of non-grid batches whose tails
+    // may still read them, with an event recorded after each such tail: a
+    // later batch writing into one of them waits for that event
+    // (tbc_compaction_submit).
+    struct TailOutputs {
+        hipEvent_t done;
+        std::vector<std::pair<uint64_t, uint64_t>> ranges;
+    };
+    std::vector<TailOutputs> tail_out;
     int next_tail = 0;
     Arena dev, host;
     Staging staging;
@@ -153,6 +165,8 @@ struct tbc_engine {
     uint32_t sort_epoch = 1;
     // k-way merge scratch (level outputs, splits, masks, counts, descriptors):
     // merges run in stream order, so one growable buffer serves them all.
+    uint8_t *copy_desc = nullptr; // tbc_copy_device_batch descriptors (device, grown once)
+    uint64_t copy_desc_size = 0;
     uint8_t *kway_scratch = nullptr;
     uint64_t kway_scratch_size = 0;
     // Memtable sorts run on their own stream, after everything enqueued on
@@ -354,7 +368,7 @@ static bool join_sorts(tbc_engine *e) {
 // Later work on the engine stream that touches grid blocks (staging blocks in
 // or out, synchronous checks) waits for every batch tail enqueued so far.
 static bool join_tails(tbc_engine *e) {
-    for (int t = 0; t < tbc_engine::kTails; t++)
+    for (int t = 0; t < e->ntails; t++)
         if (hipStreamWaitEvent(e->stream, e->tail_ev[t], 0) != hipSuccess) return false;
     return join_sorts(e);
 }
@@ -379,7 +393,12 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     e->flags = config->flags;
     e->dev.size = config->arena_bytes ? config->arena_bytes : kDefaultArena;
     e->host.size = kPinnedArena;
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    // TBC_FRONT_PRIORITY=1 (A/B measurement only): the engine stream (fronts,
+    // sorts) at the highest stream priority, the tails' chains filling in.
+    int lo_prio = 0, hi_prio = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) hi_prio = 0;
+    if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, getenv("TBC_FRONT_PRIORITY") ? hi_prio : 0) !=
+        hipSuccess) {
         delete e;
         return TBC_ERR_DEVICE;
     }
@@ -403,13 +422,22 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
     static const bool high = getenv("TBC_TAIL_PRIORITY") != nullptr; // A/B measurement only
-    for (int t = 0; ok && t < tbc_engine::kTails; t++)
+    {
+        const char *q = getenv("GPU_MAX_HW_QUEUES"), *t = getenv("TBC_TAILS");
+        const int queues = q && atoi(q) > 0 ? atoi(q) : 4;
+        const int want = t && atoi(t) > 0 ? atoi(t) : queues - 1;
+        e->ntails = want < 1 ? 1 : (want > tbc_engine::kMaxTails ? tbc_engine::kMaxTails : want);
+    }
+    for (int t = 0; ok && t < e->ntails; t++)
         ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, high ? prio_greatest : 0) == hipSuccess &&
              hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
-    ok = ok && hipStreamCreateWithFlags(&e->sort_stream, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&e->sort_last, hipEventDisableTiming) == hipSuccess;
+    // The sort stream exists only when asked for (TBC_SORT_STREAM=1): a
+    // stream beyond the hardware queues shares one with another stream.
+    if (getenv("TBC_SORT_STREAM"))
+        ok = ok && hipStreamCreateWithFlags(&e->sort_stream, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&e->sort_last, hipEventDisableTiming) == hipSuccess;
     for (int s = 0; ok && s < Staging::kSlots; s++)
         ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
     // The merge's mask buffer, sized up front for batches of up to 2^28
@@ -428,10 +456,11 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (!e) return;
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
-    for (int t = 0; t < tbc_engine::kTails; t++)
+    for (int t = 0; t < e->ntails; t++)
         if (e->tail[t]) hipStreamSynchronize(e->tail[t]);
     if (e->sort_stream) hipStreamSynchronize(e->sort_stream);
     for (auto &p : e->pending_sorts) e->event_pool.push_back(p.done);
+    for (auto &t : e->tail_out) e->event_pool.push_back(t.done);
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
     if (e->sort_last) hipEventDestroy(e->sort_last);
     if (e->sort_stream) hipStreamDestroy(e->sort_stream);
@@ -444,7 +473,8 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (e->sort_scratch) hipFree(e->sort_scratch);
     if (e->sort_status) hipFree(e->sort_status);
     if (e->kway_scratch) hipFree(e->kway_scratch);
-    for (int t = 0; t < tbc_engine::kTails; t++) {
+    if (e->copy_desc) hipFree(e->copy_desc);
+    for (int t = 0; t < e->ntails; t++) {
         if (e->tail_ev[t]) hipEventDestroy(e->tail_ev[t]);
         if (e->tail[t]) hipStreamDestroy(e->tail[t]);
     }
@@ -700,6 +730,55 @@ tbc_status tbc_copy_device_async(tbc_engine *e, void *dst, const void *src, uint
                                                                                           : TBC_ERR_DEVICE;
 }
 
+tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t count) {
+    if (!e || (count && !copies)) return TBC_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < count; i++)
+        if (copies[i].bytes && (!copies[i].dst || !copies[i].src)) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    std::vector<CopyItem> items;
+    uint64_t chunks = 0;
+    const uint64_t cb = copy_chunk_bytes();
+    for (uint32_t i = 0; i < count; i++) {
+        const tbc_copy &c = copies[i];
+        if (!c.bytes) continue;
+        if (!wait_sorts_ptr(e, c.dst, c.bytes) || !wait_sorts_ptr(e, c.src, c.bytes)) return TBC_ERR_DEVICE;
+        if (((uintptr_t)c.dst | (uintptr_t)c.src | c.bytes) & 15) { // unaligned: a copy of its own, in order
+            if (hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, e->stream) != hipSuccess)
+                return TBC_ERR_DEVICE;
+            continue;
+        }
+        items.push_back(CopyItem{c.dst, c.src, c.bytes, (uint32_t)chunks, 0});
+        chunks += (c.bytes + cb - 1) / cb;
+        if (chunks > 0x7fffffffu) return TBC_ERR_INVALID_ARGUMENT;
+    }
+    if (items.empty()) return TBC_OK;
+    const uint64_t need = sizeof(CopyItem) * items.size();
+    if (need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
+    if (need > e->copy_desc_size) { // grows once (a stream drain)
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (e->copy_desc) hipFree(e->copy_desc);
+        e->copy_desc = nullptr;
+        e->copy_desc_size = 0;
+        const uint64_t want = align_up(need, 1ull << 16);
+        if (hipMalloc((void **)&e->copy_desc, want) != hipSuccess) return TBC_ERR_OUT_OF_MEMORY;
+        e->copy_desc_size = want;
+    }
+    // The descriptors go through a pinned staging slot, reusable once the
+    // stream has passed this copy.
+    Staging &st = e->staging;
+    const int slot = st.next;
+    st.next = (st.next + 1) % Staging::kSlots;
+    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
+    uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    memcpy(host, items.data(), need);
+    bool ok = hipMemcpyAsync(e->copy_desc, host, need, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
+              launch_copy_batch((const CopyItem *)e->copy_desc, (uint32_t)items.size(), (uint32_t)chunks,
+                                e->stream) == 0;
+    ok = hipEventRecord(st.ev[slot], e->stream) == hipSuccess && ok;
+    st.used[slot] = true;
+    return ok ? TBC_OK : TBC_ERR_DEVICE;
+}
+
 tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
@@ -713,8 +792,8 @@ tbc_status tbc_synchronize(tbc_engine *e) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
-    for (int t = 0; t < tbc_engine::kTails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
-    ok = ok && hipStreamSynchronize(e->sort_stream) == hipSuccess;
+    for (int t = 0; t < e->ntails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
+    ok = ok && (!e->sort_stream || hipStreamSynchronize(e->sort_stream) == hipSuccess);
     retire_sorts(e);
     return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
@@ -815,7 +894,7 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     const uint64_t host_need = sort_host_bytes(items.data(), count);
     if (host_need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
     if (need > e->sort_scratch_size) { // grows once per larger bar (a stream drain)
-        if (hipStreamSynchronize(e->stream) != hipSuccess || hipStreamSynchronize(e->sort_stream) != hipSuccess)
+        if (hipStreamSynchronize(e->stream) != hipSuccess || (e->sort_stream && hipStreamSynchronize(e->sort_stream) != hipSuccess))
             return TBC_ERR_DEVICE;
         if (e->sort_scratch) hipFree(e->sort_scratch);
         e->sort_scratch = nullptr;
@@ -829,7 +908,7 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     }
     const uint64_t words = sort_status_words(items.data(), count);
     if (words > e->sort_status_words) {
-        if (hipStreamSynchronize(e->stream) != hipSuccess || hipStreamSynchronize(e->sort_stream) != hipSuccess)
+        if (hipStreamSynchronize(e->stream) != hipSuccess || (e->sort_stream && hipStreamSynchronize(e->sort_stream) != hipSuccess))
             return TBC_ERR_DEVICE;
         if (e->sort_status) hipFree(e->sort_status);
         e->sort_status = nullptr;
@@ -1002,6 +1081,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
             return TBC_ERR_DEVICE;
         }
         if (e->kway_scratch) hipFree(e->kway_scratch);
+    if (e->copy_desc) hipFree(e->copy_desc);
         e->kway_scratch = nullptr;
         e->kway_scratch_size = 0;
         const uint64_t want = align_up(need + need / 8, 1ull << 24);
@@ -1488,7 +1568,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
         const int ti = e->next_tail;
-        e->next_tail = (e->next_tail + 1) % tbc_engine::kTails;
+        e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
         b->fork = take_event(e);
         ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
@@ -1497,7 +1577,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && count)
             ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
                                     e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
-        for (int o = 0; ok && o < tbc_engine::kTails; o++)
+        for (int o = 0; ok && o < e->ntails; o++)
             if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
         if (ok && n_checks)
             ok = launch_grid_expect(d_resolve, (uint32_t)resolve.size(), d_checks, T) == 0 &&
@@ -1522,7 +1602,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
         const int ti = e->next_tail;
-        e->next_tail = (e->next_tail + 1) % tbc_engine::kTails;
+        e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
         b->fork = take_event(e);
         ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
@@ -1533,6 +1613,17 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                     e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+        if (ok) {
+            tbc_engine::TailOutputs to;
+            to.done = take_event(e);
+            ok = to.done && hipEventRecord(to.done, T) == hipSuccess;
+            for (uint32_t i = 0; ok && i < count; i++) {
+                const uint64_t lo = (uint64_t)(uintptr_t)jobs_in[i].output_blocks;
+                to.ranges.push_back({lo, lo + (uint64_t)jobs_in[i].address_count * e->block_size});
+            }
+            if (ok) e->tail_out.push_back(std::move(to));
+            else if (to.done) e->event_pool.push_back(to.done);
+        }
     } else if (any_unique) {
         // Speculated jobs: their block splits and results first, then the
         // merge of the others, then ONE block pass for all (speculated
@@ -1606,6 +1697,34 @@ static tbc_status check_plain_job(const tbc_engine *e, const tbc_compaction &c, 
 
 tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
+    // A batch with caller-provided output blocks may write blocks an earlier
+    // batch's tail (its chains) still reads, when the caller reuses them
+    // while that batch is in flight: its fronts then start after that tail.
+    // Batches into other blocks overlap earlier tails, as grid batches (whose
+    // outputs are freshly acquired addresses) always do.
+    if (count && !(jobs_in[0].flags & TBC_COMPACTION_GRID)) {
+        hipSetDevice(e->device);
+        auto &pend = e->tail_out;
+        for (size_t k = 0; k < pend.size();) {
+            if (hipEventQuery(pend[k].done) == hipSuccess) { // that tail is done with its outputs
+                e->event_pool.push_back(pend[k].done);
+                pend.erase(pend.begin() + (long)k);
+                continue;
+            }
+            bool alias = false;
+            for (uint32_t i = 0; i < count && !alias; i++) {
+                const uint64_t lo = (uint64_t)(uintptr_t)jobs_in[i].output_blocks;
+                const uint64_t hi = lo + (uint64_t)jobs_in[i].address_count * e->block_size;
+                for (const auto &r : pend[k].ranges)
+                    if (lo < r.second && r.first < hi) {
+                        alias = true;
+                        break;
+                    }
+            }
+            if (alias && hipStreamWaitEvent(e->stream, pend[k].done, 0) != hipSuccess) return TBC_ERR_DEVICE;
+            k++;
+        }
+    }
     static const bool no_groups = getenv("TBC_NO_GROUPS") != nullptr; // A/B measurement only
     uint32_t groups = 1;
     std::vector<uint64_t> n(count, 0);

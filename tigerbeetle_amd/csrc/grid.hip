@@ -141,4 +141,41 @@ int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, cons
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// tbc_copy_device_batch: many device-to-device copies (16-byte aligned,
+// multiples of 16 bytes) in one launch. One workgroup per 64 KiB chunk:
+// every lane's sixteen 16-byte loads are issued before its stores.
+constexpr uint32_t kCopyChunk = 65536;
+
+__global__ __launch_bounds__(256) void k_copy_batch(const CopyItem *items, uint32_t count) {
+    uint32_t lo = 0, hi = count; // the copy whose chunk range holds this workgroup's chunk
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (items[mid].chunk0 <= blockIdx.x) lo = mid;
+        else hi = mid;
+    }
+    const CopyItem it = items[lo];
+    const uint64_t off = (uint64_t)(blockIdx.x - it.chunk0) * kCopyChunk;
+    const uint64_t n = it.bytes - off < kCopyChunk ? it.bytes - off : kCopyChunk;
+    const uint8_t *src = (const uint8_t *)it.src + off;
+    uint8_t *dst = (uint8_t *)it.dst + off;
+    u32x4 v[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+        const uint64_t o = 16 * ((uint64_t)threadIdx.x + 256 * r);
+        if (o < n) v[r] = gld<u32x4>(src + o);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+        const uint64_t o = 16 * ((uint64_t)threadIdx.x + 256 * r);
+        if (o < n) gst<u32x4>(dst + o, v[r]);
+    }
+}
+
+int launch_copy_batch(const CopyItem *d_items, uint32_t count, uint32_t chunks, void *stream) {
+    if (!count || !chunks) return 0;
+    hipLaunchKernelGGL(k_copy_batch, dim3(chunks), dim3(256), 0, (hipStream_t)stream, d_items, count);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+uint64_t copy_chunk_bytes() { return kCopyChunk; }
+
 } // namespace tbc

@@ -332,6 +332,15 @@ int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *
                           uint64_t previous_address, const uint64_t *d_previous_checksum, void *stream);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
+// One copy of tbc_copy_device_batch: chunks [chunk0, chunk0 + ceil(bytes / copy_chunk_bytes())).
+struct CopyItem {
+    void *dst;
+    const void *src;
+    uint64_t bytes;
+    uint32_t chunk0, pad;
+};
+int launch_copy_batch(const CopyItem *d_items, uint32_t count, uint32_t chunks, void *stream);
+uint64_t copy_chunk_bytes();
 struct SortItem {
     void *values;
     uint32_t n, value_size, timestamp_offset, key_kind;

@@ -373,6 +373,14 @@ class Engine:
     def copy_device_async(self, dst: int, src: int, nbytes: int) -> None:
         check(lib().tbc_copy_device_async(self.handle, dst, src, nbytes), "tbc_copy_device_async")
 
+    def copy_device_batch(self, copies: list) -> None:
+        """tbc_copy_device_batch: [(dst, src, nbytes)] device copies in one
+        launch on the engine stream (no host wait)."""
+        arr = (abi.Copy * max(1, len(copies)))()
+        for i, (d, s, n) in enumerate(copies):
+            arr[i].dst, arr[i].src, arr[i].bytes = d, s, n
+        check(lib().tbc_copy_device_batch(self.handle, arr, len(copies)), "tbc_copy_device_batch")
+
     def sort_values_batch(self, tables: list) -> None:
         """Bar end: [(TreeSpec, DeviceBuffer | device ptr, count)] sorted by one
         segmented launch sequence (tbc_sort_values_batch), enqueued on the

@@ -38,8 +38,7 @@ for gid in range(njobs):
 
 
 def land():
-    for dst, src, n, _, _ in landings:
-        eng.copy_device_async(dst, src, n)
+    eng.copy_device_batch([(dst, src, n) for dst, src, n, _, _ in landings])
 
 
 def timed(fn, reps):
