@@ -14,9 +14,13 @@ arrays at a time) to keep host memory bounded at the 1B-value scale.
             L0 tables; 1% of the bar's puts are removed again (half inside the
             bar -> put/remove pairs cancel in fill_immutable_values, half
             removing an older put that lives in B -> both dropped by the
-            secondary-index merge rule). Every 7th job is the sequential
-            transfers.timestamp object tree (Transfer, 128 B): already sorted,
-            no B, a pure flush.
+            secondary-index merge rule). Two jobs in every 7 are the
+            sequential leg: the same index trees with an
+            increasing field and monotone timestamps (job % 7 == 5: the
+            memtable arrives sorted and its keys lie above every older table,
+            so it flushes with no B and the deeper levels move), and the
+            transfers.timestamp object tree (Transfer, 128 B; job % 7 == 6),
+            likewise a pure flush.
   config 4  full groove compaction (one forest unit per GPU, 21 jobs): the
             bar-end immutable->L0 compaction of the 11 trees a create_transfers
             bar feeds (10 transfer trees — pending_id/timeout are 0 and not
@@ -128,6 +132,14 @@ def config3_job(job: int, n_b_tables: int = 8) -> JobSpec:
         a = workloads.values_from_keys(spec, [ts], np.zeros(TABLE_T, dtype=bool), rng)
         return JobSpec(spec, a, True, False, [], False, 0, unique_keys=True)
     spec = trees.BY_NAME["transfers.debit_account_id" if job % 2 == 0 else "transfers.credit_account_id"]
+    if job % 7 == 5:
+        # Sequential secondary index: each new account's transfers in order
+        # (four per account), fields above every older table's: the
+        # memtable is already in key order and overlaps no L0 table.
+        ts = bar_ts0 + np.arange(TABLE_T, dtype=np.uint64)
+        field = np.uint64(1 + (job + n_b_tables) * TABLE_T) + np.arange(TABLE_T, dtype=np.uint64) // np.uint64(4)
+        a = _composite128(field, ts, np.zeros(TABLE_T, dtype=bool))
+        return JobSpec(spec, a, True, False, [], False, 0, unique_keys=True)
     # B: 8 L0 tables of older puts (timestamps before this bar), sorted, cut.
     nb = n_b_tables * TABLE_T
     b_ts = np.uint64(1) + rng.choice(int(bar_ts0) - 1, size=nb, replace=False).astype(np.uint64)
@@ -265,7 +277,7 @@ def job_bytes(config: int, job: int) -> int:
     if config == 2:
         return 9 * TABLE_T * 32
     if config == 3:
-        return TABLE_T * (128 if job % 7 == 6 else 9 * 32)
+        return TABLE_T * (128 if job % 7 == 6 else 32 if job % 7 == 5 else 9 * 32)
     if config == 5:
         return 9 * TABLE_A_TS * 128
     k = job % FOREST_JOBS
@@ -281,7 +293,7 @@ def presorted(config: int, job: int) -> bool:
     """Whether the job's A needs no device sort first (a key-range split
     stages sorted ranges)."""
     if config == 3:
-        return job % 7 == 6
+        return job % 7 in (5, 6)
     if config == 4:
         k = job % FOREST_JOBS
         return k >= len(FOREST_BAR) or FOREST_BAR[k] in ("transfers.id", "transfers.timestamp")
@@ -296,7 +308,8 @@ DEFAULT_JOBS = {2: 28, 3: 28, 4: FOREST_JOBS, 5: 27}
 DESCRIPTION = {
     2: "transfers.id L0->L1 compaction, 28 jobs x (1 A + 8 B tables) per GPU, 64M u128 keys, 1 MiB blocks",
     3: "bar end of transfers.debit/credit_account_id (Zipf 1.1 over 10k accounts, unsorted memtable sorted on "
-       "device, 1% put/remove pairs) + sequential transfers.timestamp flushes, 28 jobs per GPU",
+       "device, 1% put/remove pairs) + sequential legs (index trees with increasing fields, transfers.timestamp: "
+       "already sorted flushes), 28 jobs per GPU",
     4: "full groove compaction: bar-end immutable->L0 of the 11 trees a create_transfers bar feeds (+ on-device "
        "memtable sorts) and one L1->L2 job per transfer tree, 21 jobs of 4 key kinds per GPU, sharded by bytes",
     5: "accounts.timestamp last-level compaction (Account 128 B, 1% tombstones dropped), 27 jobs x 4.7M values "
