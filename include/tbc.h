@@ -343,7 +343,10 @@ tbc_status tbc_kway_merge(tbc_engine *engine, const tbc_tree *tree, const tbc_se
 
 /* ---- compaction ------------------------------------------------------------- */
 /* Enqueue `count` independent compactions (one half-bar's jobs) as one batch.
- * All input/output device memory must stay valid until the batch completes. */
+ * All input/output device memory must stay valid until the batch completes.
+ * Batches may be submitted without waiting for earlier ones: a batch whose
+ * output blocks overlap those of an earlier batch still being checksummed
+ * waits for it on the device; other batches run beside it. */
 tbc_status tbc_compaction_submit(tbc_engine *engine, const tbc_compaction *compactions, uint32_t count,
                                  tbc_batch **out_batch);
 /* Non-blocking: TBC_PENDING while running, then TBC_OK or the first error. */
