@@ -27,7 +27,7 @@ def _cases():
     return cases
 
 
-def _jobs(engine, inputs, addrs, outs, keep):
+def _jobs(engine, inputs, addrs, outs, keep, bs=BS, flags=0):
     jobs = []
     for ji, a, out in zip(inputs, addrs, outs):
         vcm = engine.layout(ji.tree).block_value_count_max
@@ -35,11 +35,12 @@ def _jobs(engine, inputs, addrs, outs, keep):
             abuf = engine.upload(ji.a_values)
             segs_a = [(abuf.ptr, len(ji.a_values))]
         else:
-            abuf, segs_a = stage_blocks(engine, [workloads.split_blocks(ji.a_values, vcm)], ji.tree.value_size, BS)
+            abuf, segs_a = stage_blocks(engine, [workloads.split_blocks(ji.a_values, vcm)], ji.tree.value_size, bs)
         bbuf, segs_b = stage_blocks(engine, [workloads.split_blocks(t, vcm) for t in ji.b_tables],
-                                    ji.tree.value_size, BS)
+                                    ji.tree.value_size, bs)
         keep += [abuf, bbuf]
-        jobs.append(Job(ji.tree, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48, a, out))
+        jobs.append(Job(ji.tree, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48, a, out,
+                        flags=flags))
     return jobs
 
 
@@ -69,6 +70,44 @@ def test_back_to_back_batches_share_outputs(engine_small, oracle_lib):
         assert r.status == 0 and o.status == 0
         assert r.block_count == len(o.blocks)
         got = out.download(r.block_count * BS).reshape(-1, BS)
+        for k, (g, w) in enumerate(zip(got, o.blocks)):
+            assert np.array_equal(disk_image(g), disk_image(w)), (ji.tree.name, k)
+        assert np.array_equal(infos, o.table_infos)
+    b1.release()
+    b2.release()
+
+
+@pytest.mark.gpu
+def test_back_to_back_speculated_batches_share_outputs(engine, oracle_lib):
+    """The latency regime: a UNIQUE_KEYS batch's index blocks and results run
+    on a tail stream; a second batch into the same output blocks must wait
+    for them (its data blocks, then its own index blocks, are the final ones)."""
+    from tigerbeetle_amd import abi
+    bs = 1 << 20
+    names = ["transfers.id", "transfers.timestamp", "transfers.debit_account_id", "transfers.amount"]
+    rng1, rng2, rng_a = np.random.default_rng(311), np.random.default_rng(312), np.random.default_rng(313)
+    kw = dict(n_a=60_000, b_table_sizes=[50_000, 40_000], a_immutable=False, overlap=0.3)
+    first = [workloads.make_job_inputs(trees.BY_NAME[n], rng1, **kw) for n in names]
+    second = [workloads.make_job_inputs(trees.BY_NAME[n], rng2, **kw) for n in names]
+    addrs, outs = [], []
+    for n in names:
+        a = workloads.addresses_for(workloads.worst_case_blocks(trees.BY_NAME[n], 150_000, bs) + 3, rng_a, 1, 0.1)
+        addrs.append(np.asarray(a, dtype=np.uint64))
+        out = engine.alloc(len(a) * bs)
+        out.zero()
+        outs.append(out)
+    keep = []
+    fl = abi.COMPACTION_UNIQUE_KEYS
+    b1 = engine.submit(_jobs(engine, first, addrs, outs, keep, bs, fl))
+    b2 = engine.submit(_jobs(engine, second, addrs, outs, keep, bs, fl))
+    b1.wait()
+    b2.wait()
+    for i, (ji, a, out) in enumerate(zip(second, addrs, outs)):
+        r, infos = b2.result(i)
+        o = run_oracle(oracle_lib, ji, bs, a)
+        assert r.status == 0 and o.status == 0
+        assert r.block_count == len(o.blocks)
+        got = out.download(r.block_count * bs).reshape(-1, bs)
         for k, (g, w) in enumerate(zip(got, o.blocks)):
             assert np.array_equal(disk_image(g), disk_image(w)), (ji.tree.name, k)
         assert np.array_equal(infos, o.table_infos)

@@ -1952,6 +1952,14 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
     return 0;
 }
 
+int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
+                        uint8_t *d_infos, void *stream) {
+    if (!total_tables) return 0;
+    hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, (hipStream_t)stream, d_jobs, njobs,
+                       d_results, d_infos);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Pipelined batch, front (engine stream, in order with every later batch's
 // front): every body assembled, and the output index blocks' data addresses.
 int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks,

@@ -1407,6 +1407,10 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     const bool spec_regime = !grid_mode && !pipeline && !(flags0 & TBC_COMPACTION_VALUES_ONLY) &&
                              (uint64_t)(dblocks + 1) / 2 <= fused_max_chain_waves();
     static const bool no_spec = getenv("TBC_NO_SPECULATION") != nullptr; // A/B measurement only
+    // The speculated batch's index blocks and results on a tail stream
+    // (round 3, one box: config 2 2.276/2.251 -> 2.235/2.222 ms, configs 3
+    // and 4 within noise); TBC_NO_TAIL_FORK=1 keeps them on the engine stream.
+    static const bool no_tail_fork = getenv("TBC_NO_TAIL_FORK") != nullptr; // A/B measurement only
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
@@ -1624,12 +1628,50 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             if (ok) e->tail_out.push_back(std::move(to));
             else if (to.done) e->event_pool.push_back(to.done);
         }
-    } else if (any_unique) {
+    } else if (any_unique && !no_tail_fork) {
         // Speculated jobs: their block splits and results first, then the
         // merge of the others, then ONE block pass for all (speculated
         // producers merge their blocks themselves), then the recomputation of
         // broken speculations (every kernel leaves at once when none broke),
         // then the index blocks.
+        const JobDesc *dj = (const JobDesc *)d_in;
+        ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
+        mark_cb(b, "partition_blocks");
+        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
+                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
+        ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
+                                 d_block_tile, d_splits, false, maybe_sparse, s, mark_cb, b, false, d_bsplits, 0,
+                                 false) == 0;
+        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
+                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+        ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
+                                 d_block_tile, d_splits, false, true, s, mark_cb, b, false, d_bsplits, 1, false) == 0;
+        // The index blocks and the results go to a tail stream, so the next
+        // batch's front starts as soon as this batch's data blocks (and any
+        // recomputation, which uses the engine's mask buffer) are done. A
+        // later batch into the same output blocks waits for this tail.
+        const int ti = e->next_tail;
+        e->next_tail = (e->next_tail + 1) % e->ntails;
+        hipStream_t T = e->tail[ti];
+        b->fork = take_event(e);
+        ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
+        b->mark_stream = T;
+        ok = ok && launch_index_blocks(dj, (int)count, tables, d_res, d_infos, T) == 0;
+        mark_cb(b, "index_blocks");
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+        if (ok) {
+            tbc_engine::TailOutputs to;
+            to.done = take_event(e);
+            ok = to.done && hipEventRecord(to.done, T) == hipSuccess;
+            for (uint32_t i = 0; ok && i < count; i++) {
+                const uint64_t lo = (uint64_t)(uintptr_t)jobs_in[i].output_blocks;
+                to.ranges.push_back({lo, lo + (uint64_t)jobs_in[i].address_count * e->block_size});
+            }
+            if (ok) e->tail_out.push_back(std::move(to));
+            else if (to.done) e->event_pool.push_back(to.done);
+        }
+    } else if (any_unique) { // the speculated path with everything on the engine stream (A/B only)
         const JobDesc *dj = (const JobDesc *)d_in;
         ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
         mark_cb(b, "partition_blocks");

@@ -317,6 +317,8 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
                        JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
                        void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
+                        uint8_t *d_infos, void *stream);
 int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t *d_verified, const JobDesc *d_jobs,
                        int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
 int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_verified, const JobDesc *d_jobs,
