@@ -129,6 +129,92 @@ def test_two_half_bars_chained_through_the_grid(engine, oracle_lib):
         grid.close()
 
 
+def test_grid_batches_in_flight_together(engine, oracle_lib):
+    """Three grid batches submitted back to back with a put_blocks between
+    them and no wait: batch 2 reads batch 1's first output table (its fronts
+    find the data blocks through the index block batch 1's front laid out
+    early; its input checks wait for batch 1's tail), batch 3 reads a storage
+    table batch 1 also reads. Expected outputs come from the oracle before
+    anything is submitted (the output TableInfo batch 2 names is the
+    oracle's)."""
+    rng = np.random.default_rng(0x3B47)
+    grid = Grid(engine, 700)
+    spec_id = trees.BY_NAME["transfers.id"]
+    spec_acc = trees.BY_NAME["accounts.timestamp"]
+    mem = None
+    try:
+        universe = sorted_unique(spec_id, 160_000, rng)
+        pick = np.zeros(len(universe), bool)
+        pick[rng.choice(len(universe), 90_000, replace=False)] = True
+        b_all = universe[~pick]
+        blk1, ti1 = storage_table(oracle_lib, spec_id, b_all, np.arange(1, 40, dtype=np.uint64), level=0)
+        acc_b = sorted_unique(spec_acc, 30_000, rng)
+        blk3, ti3 = storage_table(oracle_lib, spec_acc, acc_b, np.arange(40, 60, dtype=np.uint64), level=2)
+        acc_keys = workloads.keys_of(acc_b, spec_acc)[0]
+        acc_a = workloads.values_from_keys(spec_acc, [np.sort(acc_keys[rng.choice(30_000, 12_000, replace=False)])],
+                                           rng.random(12_000) < 0.1, rng)
+        blk4, ti4 = storage_table(oracle_lib, spec_acc, acc_a, np.arange(60, 80, dtype=np.uint64), level=1)
+        acc_c = workloads.values_from_keys(spec_acc, [np.sort(acc_keys[rng.choice(30_000, 9_000, replace=False)])],
+                                           rng.random(9_000) < 0.2, rng)
+        blk6, ti6 = storage_table(oracle_lib, spec_acc, acc_c, np.arange(80, 100, dtype=np.uint64), level=1)
+        for blocks, ti, base in ((blk1, ti1, 1), (blk3, ti3, 40), (blk4, ti4, 60), (blk6, ti6, 80)):
+            grid.put_blocks(np.arange(base, base + len(blocks), dtype=np.uint64), np.stack(blocks))
+
+        mem_vals = universe[pick]
+        mem = Memtable(engine, spec_id)
+        shuffled = workloads.shuffle_for_memtable(mem_vals, rng, spec_id)
+        for lo in range(0, len(shuffled), 8190):
+            mem.put(shuffled[lo:lo + 8190])
+        mptr, mcount = mem.values()
+        engine.sort_values_batch([(spec_id, mptr, mcount)])
+
+        # The oracle first: batch 1's flush decides batch 2's input table.
+        a1 = np.arange(100, 100 + 3 * 9, dtype=np.uint64)
+        a2 = np.arange(200, 200 + 2 * 65, dtype=np.uint64)
+        a3 = np.arange(400, 400 + 2 * 9, dtype=np.uint64)
+        a4 = np.arange(500, 500 + 2 * 65, dtype=np.uint64)
+        t = oracle_tree(oracle_lib, spec_id, BS)
+        o1 = oracle_lib.compact(t, [mem_vals], workloads.split_blocks(b_all, t.block_value_count_max),
+                                a_immutable=True, drop_tombstones=False, level_b=0, cluster=CLUSTER,
+                                snapshot_min=48, addresses=a1)
+        out_t0 = TableInfo.decode(o1.table_infos[0], spec_id.key_size)
+        a_vals = table_values(o1.blocks[:10], spec_id)[: out_t0.value_count]
+        lo_key, hi_key = out_t0.key_min, out_t0.key_max
+        more = sorted_unique(spec_id, 40_000, rng)
+        mk = workloads.keys_of(more, spec_id)
+        mint = mk[0].astype(object) | (mk[1].astype(object) << 64)
+        fresh = more[(mint > lo_key) & (mint < hi_key)]
+        in_a = set(map(bytes, a_vals[:, :16]))
+        fresh = fresh[[bytes(v[:16]) not in in_a for v in fresh]]
+        blk5, ti5 = storage_table(oracle_lib, spec_id, fresh, np.arange(300, 320, dtype=np.uint64), level=1)
+
+        def gjob(spec, level, snap, addrs, drop=False, **kw):
+            return Job(spec, kw.pop("segs_a", []), [], kw.pop("imm", False), drop, level, CLUSTER, snap, addrs, None,
+                       flags=abi.COMPACTION_GRID, grid=grid, **kw)
+
+        h1 = engine.submit([gjob(spec_id, 0, 48, a1, segs_a=[(mptr, mcount)], imm=True, tables_b=[ti1.ref()]),
+                            gjob(spec_acc, 2, 48, a2, drop=True, tables_a=[ti4.ref()], tables_b=[ti3.ref()])])
+        grid.put_blocks(np.arange(300, 300 + len(blk5), dtype=np.uint64), np.stack(blk5))
+        h2 = engine.submit([gjob(spec_id, 1, 64, a3, tables_a=[out_t0.ref()], tables_b=[ti5.ref()])])
+        h3 = engine.submit([gjob(spec_acc, 2, 48, a4, drop=True, tables_a=[ti6.ref()], tables_b=[ti3.ref()])])
+        for h in (h3, h2, h1):
+            h.wait()
+        res = [h1.result(0), h1.result(1), h2.result(0), h3.result(0)]
+        for h in (h1, h2, h3):
+            h.release()
+        check_job(oracle_lib, grid, spec_id, *res[0], mem_vals, True, [b_all], False, 0, 48, a1)
+        check_job(oracle_lib, grid, spec_acc, *res[1], acc_a, False, [acc_b], True, 2, 48, a2)
+        check_job(oracle_lib, grid, spec_id, *res[2], a_vals, False, [fresh], False, 1, 64, a3)
+        check_job(oracle_lib, grid, spec_acc, *res[3], acc_c, False, [acc_b], True, 2, 48, a4)
+        # Batch 2 found its input table only through the grid: it was trusted
+        # (batch 1's output) or validated, and nothing failed.
+        assert all(r.status == 0 for r, _ in res)
+    finally:
+        if mem is not None:
+            mem.close()
+        grid.close()
+
+
 def test_grid_rejects_corrupt_and_unexpected_blocks(engine, oracle_lib):
     """read_block_validate on blocks from storage (a flipped body byte), and
     read_block_from_cache's checksum comparison on trusted blocks (a table
