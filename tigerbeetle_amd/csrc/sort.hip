@@ -133,11 +133,23 @@ __device__ __forceinline__ uint32_t *seg_hist(uint32_t *hist, uint32_t s) { retu
 
 // The key and the next item's key (the next lane's; lane 63 loads its
 // neighbour, which may sit in the next tile) of every lane of a row.
-__device__ __forceinline__ void row_keys(const SortSeg &S, uint32_t li, bool in, uint64_t k[3], uint64_t kn[3]) {
-    k[0] = k[1] = k[2] = 0;
-    if (in) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
+// Both loads are issued before either is used (one memory round trip per row):
+// row_load issues them, row_next forms the neighbours once they are in.
+__device__ __forceinline__ void row_load(const SortSeg &S, uint32_t li, uint64_t k[3], uint64_t kx[3]) {
+    k[0] = k[1] = k[2] = kx[0] = kx[1] = kx[2] = 0;
+    if (li < S.n) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
+    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kx);
+}
+__device__ __forceinline__ void row_next(uint32_t li, uint32_t n, const uint64_t k[3], const uint64_t kx[3],
+                                         uint64_t kn[3]) {
     for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
-    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kn);
+    if ((threadIdx.x & 63) == 63 && li + 1 < n)
+        for (uint32_t l = 0; l < 3; l++) kn[l] = kx[l];
+}
+__device__ __forceinline__ void row_keys(const SortSeg &S, uint32_t li, uint64_t k[3], uint64_t kn[3]) {
+    uint64_t kx[3];
+    row_load(S, li, k, kx);
+    row_next(li, S.n, k, kx, kn);
 }
 
 // --------------------------------------------------------------------------
@@ -159,11 +171,21 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
         if (lt * kSortTile + r * kSortThreads >= n) break; // wave-uniform (whole row past the end)
         const bool in = li < n;
+        // The row's first 128 bytes of every value are loaded with its keys
+        // (one round trip), then stored; longer values loop.
+        u32x4 v[8];
+        if (in) {
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                if (16 * q < vs) v[q] = gld<u32x4>(S.values + (size_t)li * vs + 16 * q);
+        }
         uint64_t k[3], kn[3];
-        row_keys(S, li, in, k, kn);
+        row_keys(S, li, k, kn);
         if (!in) continue;
-        for (uint32_t b = 0; b < vs; b += 128) { // up to 8 loads in flight before their stores
-            u32x4 v[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++)
+            if (16 * q < vs) gst<u32x4>(S.copy + (size_t)li * vs + 16 * q, v[q]);
+        for (uint32_t b = 128; b < vs; b += 128) { // up to 8 loads in flight before their stores
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
                 if (b + 16 * q < vs) v[q] = gld<u32x4>(S.values + (size_t)li * vs + b + 16 * q);
@@ -315,17 +337,23 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
     const uint32_t nd = S.ndig, nr = S.nruns, ib = S.ib, n = S.n;
     if (!nd) return; // uniform: a sorted table
     for (uint32_t j = 0; j < nd; j++) s_hist[j][tid] = 0;
-    if (tid < kMaxRuns) s_run[tid] = S.run[tid];
+    if (tid < kMaxRuns) s_run[tid] = segs[sg].run[tid]; // not S.run[tid]: a dynamic index would put S in scratch
     if (tid == 0) s_viol = 0;
     __syncthreads();
     const uint32_t lt = blockIdx.x - S.tile_base;
     uint32_t viol = 0;
-    for (uint32_t r = 0; r < kSortRounds; r++) {
+    const uint32_t left = n - lt * kSortTile; // > 0: the tile is in the table
+    const uint32_t rows = left >= kSortTile ? kSortRounds : (left + kSortThreads - 1) / kSortThreads;
+    // The next row's keys load while a row is packed (round 3, one box, with
+    // S out of scratch: config 3's pack 119 -> 100 us; two rows ahead: 98).
+    uint64_t k[3], kx[3];
+    row_load(S, lt * kSortTile + tid, k, kx);
+    for (uint32_t r = 0; r < rows; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-        if (lt * kSortTile + r * kSortThreads >= n) break; // uniform
         const bool in = li < n;
-        uint64_t k[3], kn[3];
-        row_keys(S, li, in, k, kn);
+        uint64_t k2[3] = {0, 0, 0}, kx2[3] = {0, 0, 0}, kn[3];
+        if (r + 1 < rows) row_load(S, li + kSortThreads, k2, kx2);
+        row_next(li, n, k, kx, kn);
         const uint64_t p = pack_bits(s_run, nr, k);
         if (in) gst<uint64_t>(words + S.item_base + li, p << ib | li);
         for (uint32_t j = 0; j < nd; j++) hist_add(s_hist[j], (uint32_t)(p >> (8 * j)) & 255u, in);
@@ -335,6 +363,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
                 const uint64_t m = low_mask(8 * (j + 1));
                 if ((p & m) > (q & m)) viol |= 1u << j;
             }
+        }
+        for (uint32_t l = 0; l < 3; l++) {
+            k[l] = k2[l];
+            kx[l] = kx2[l];
         }
     }
     if (viol) atomicOr(&s_viol, viol);
