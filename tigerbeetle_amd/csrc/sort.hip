@@ -304,8 +304,10 @@ __global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs) {
 }
 
 // One wave's 64 digits into an LDS histogram row: a digit shared by the
-// whole row (a slowly varying key byte) is one add; otherwise the lanes
-// with equal digits (8 ballots) add once through their first lane.
+// whole row (a slowly varying key byte) is one add; otherwise every lane adds
+// its own (the LDS serialises equal addresses). Round 3, one box: grouping
+// equal digits first by 8 match ballots (one add per distinct digit) cost
+// more VALU than it saved -- config 3's pack 100 -> 67 us without it.
 __device__ __forceinline__ void hist_add(uint32_t *row, uint32_t d, bool in) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t act = __ballot(in);
@@ -316,13 +318,7 @@ __device__ __forceinline__ void hist_add(uint32_t *row, uint32_t d, bool in) {
         if (lane == first) atomicAdd(&row[d0], (uint32_t)__builtin_popcountll(act));
         return;
     }
-    uint64_t peers = act;
-#pragma unroll
-    for (uint32_t b = 0; b < 8; b++) {
-        const uint64_t bal = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bal : ~bal;
-    }
-    if (in && !(peers & ((1ull << lane) - 1))) atomicAdd(&row[d], (uint32_t)__builtin_popcountll(peers));
+    if (in) atomicAdd(&row[d], 1u);
 }
 
 // Pack: one workgroup per tile of an unsorted table.
