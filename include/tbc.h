@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TBC_ABI_VERSION 3u
+#define TBC_ABI_VERSION 4u
 
 typedef enum tbc_status {
     TBC_OK = 0,
@@ -208,8 +208,10 @@ tbc_status tbc_grid_block_pointer(const tbc_grid *grid, uint64_t address, void *
 tbc_status tbc_grid_put_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_blocks,
                                uint32_t count);
 /* grid.write_block towards storage: copy `count` blocks' images
- * [0, block_size) to host buffers. Enqueued on the engine stream; the
- * buffers are valid after tbc_synchronize (or a later batch's completion). */
+ * [0, block_size) to host buffers; returns once the buffers hold them. Waits
+ * (on the device) for every batch tail enqueued so far. Buffers inside a
+ * range registered with tbc_host_register are written by DMA directly; others
+ * go through the pinned staging ring with every slot in flight. */
 tbc_status tbc_grid_get_blocks(tbc_grid *grid, const uint64_t *addresses, void *const *host_blocks,
                                uint32_t count);
 
@@ -226,7 +228,11 @@ tbc_status tbc_grid_get_blocks(tbc_grid *grid, const uint64_t *addresses, void *
  * when that is NULL, the header checksum of the block at `previous_address`
  * in the grid — an earlier close — or 0 when previous_address is 0) and its
  * header checksum. Enqueued on the engine stream; no host wait beyond the
- * pinned staging copies. The blocks are trusted grid blocks afterwards.
+ * pinned staging copies. The blocks are trusted grid blocks afterwards. When
+ * `previous_checksum` is NULL, the block at `previous_address` must be a
+ * verified manifest block of this grid (closed by an earlier call); if it is
+ * not, nothing is linked: the new blocks keep a zero header checksum (every
+ * later read fails validation) and stay unverified.
  * TBC_ERR_INVALID_ARGUMENT if a packed header contradicts its address, the
  * chain or ManifestNode.metadata's asserts (schema.zig:534-554). */
 tbc_status tbc_manifest_close_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_images,
@@ -248,6 +254,14 @@ tbc_status tbc_memtable_put(tbc_memtable *memtable, const void *values, uint32_t
 tbc_status tbc_memtable_values(const tbc_memtable *memtable, void **out_values, uint32_t *out_count);
 /* make_mutable: empty the table (after its immutable compaction flushed it). */
 tbc_status tbc_memtable_reset(tbc_memtable *memtable);
+
+/* ---- registered host memory ------------------------------------------------
+ * hipHostRegister of a caller range (TigerBeetle's I/O buffers are allocated
+ * once at startup): tbc_grid_put_blocks / tbc_grid_get_blocks move blocks
+ * from or into a registered range by DMA, without the staging ring's host
+ * copy. Ranges must not overlap; unregister waits for enqueued work. */
+tbc_status tbc_host_register(tbc_engine *engine, void *ptr, uint64_t bytes);
+tbc_status tbc_host_unregister(tbc_engine *engine, void *ptr);
 
 /* ---- device memory (staging for the host adapter; synchronous copies) ------ */
 tbc_status tbc_device_alloc(tbc_engine *engine, uint64_t bytes, void **out_ptr);
@@ -346,7 +360,11 @@ tbc_status tbc_kway_merge(tbc_engine *engine, const tbc_tree *tree, const tbc_se
  * All input/output device memory must stay valid until the batch completes.
  * Batches may be submitted without waiting for earlier ones: a batch whose
  * output blocks overlap those of an earlier batch still being checksummed
- * waits for it on the device; other batches run beside it. */
+ * waits for it on the device; other batches run beside it. A batch's output
+ * blocks may be read or overwritten by other calls (tbc_copy_to_host,
+ * tbc_copy_device_async, tbc_memset_device, ...) only after tbc_batch_poll or
+ * tbc_batch_wait has returned its result: parts of a batch (its chains,
+ * index blocks and results) run on tail streams those calls do not wait for. */
 tbc_status tbc_compaction_submit(tbc_engine *engine, const tbc_compaction *compactions, uint32_t count,
                                  tbc_batch **out_batch);
 /* Non-blocking: TBC_PENDING while running, then TBC_OK or the first error. */

@@ -212,3 +212,73 @@ def test_copy_device_batch(engine):
         want[off + shift:off + shift + n] = s[off + shift:off + shift + n]
         off += n + 64
     assert np.array_equal(d, want)
+
+
+def test_copy_batch_descriptors_survive_kway_scratch_growth():
+    """growing the k-way scratch must leave the copy
+    batch's descriptor buffer alone. On a fresh engine: a copy batch (its
+    descriptor buffer allocated), a k-way merge large enough to grow the
+    k-way scratch, another copy batch with data checks, then deinit."""
+    from tigerbeetle_amd import Engine
+    eng = Engine(device=0, block_size=1 << 20)
+    try:
+        rng = np.random.default_rng(0xC0DE)
+        spec = trees.BY_NAME["transfers.id"]
+
+        def copy_round(seed):
+            data = np.random.default_rng(seed).integers(0, 256, 3 << 20, dtype=np.uint8)
+            src = eng.upload(data)
+            dst = eng.alloc(len(data))
+            dst.zero()
+            eng.copy_device_batch([(dst.ptr + o, src.ptr + o, 1 << 20) for o in (0, 1 << 20, 2 << 20)])
+            eng.synchronize()
+            assert np.array_equal(dst.download(), data)
+
+        copy_round(1)
+        limbs = workloads.unique_sorted_keys(spec, 400_000, rng)
+        streams, idxs = [], []
+        for _ in range(4):
+            idx = np.sort(rng.choice(400_000, 100_000, replace=False))
+            idxs.append(idx)
+            streams.append(workloads.values_from_keys(spec, [l[idx] for l in limbs], np.zeros(len(idx), bool), rng))
+        bufs = [eng.upload(s) for s in streams]
+        out = eng.alloc(400_000 * 32)
+        n = eng.kway_merge(spec, [(b.ptr, len(s)) for b, s in zip(bufs, streams)], out)
+        assert n == len(np.unique(np.concatenate(idxs)))  # one value per distinct key
+        copy_round(2)
+        copy_round(3)
+    finally:
+        eng.close()
+
+
+def test_grid_block_transfers_staged_and_registered(engine):
+    """tbc_grid_put_blocks / tbc_grid_get_blocks (round 4: the D2H ring keeps
+    every slot in flight; registered host ranges go by direct DMA): 20 blocks
+    (more than the 8 staging slots) round-trip byte for byte through pageable
+    memory, through host-registered arrays, and mixed; the verified bytes of
+    staged blocks are cleared by one launch (a later trusted check fails)."""
+    bs = engine.block_size
+    grid = Grid(engine, 64)
+    try:
+        rng = np.random.default_rng(0x9C1E)
+        n = 20
+        addrs = rng.permutation(np.arange(1, 65, dtype=np.uint64))[:n]
+        imgs = rng.integers(0, 256, size=(n, bs), dtype=np.uint8)
+        grid.put_blocks(addrs, imgs)
+        assert np.array_equal(grid.get_blocks(addrs), imgs)
+        reg_in = rng.integers(0, 256, size=(n, bs), dtype=np.uint8)
+        reg_out = np.zeros_like(reg_in)
+        engine.host_register(reg_in)
+        engine.host_register(reg_out)
+        try:
+            grid.put_blocks(addrs, reg_in)
+            got = grid.get_blocks(addrs, out=reg_out)
+            assert got is reg_out and np.array_equal(reg_out, reg_in)
+            with pytest.raises(abi.TbcError):  # overlapping registration refused
+                engine.host_register(reg_in[1:3])
+        finally:
+            engine.host_unregister(reg_in)
+            engine.host_unregister(reg_out)
+        assert np.array_equal(grid.get_blocks(addrs[::-1]), reg_in[::-1])
+    finally:
+        grid.close()

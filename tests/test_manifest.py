@@ -93,6 +93,30 @@ def test_gpu_manifest_chain_links_a_block_closed_earlier():
         assert np.array_equal(g[:len(w)], w)
 
 
+@pytest.mark.gpu
+def test_gpu_manifest_refuses_to_link_an_untrusted_block():
+    """linking by address needs a verified manifest block there.
+    A previous address holding a block staged from storage (unverified) or a
+    non-manifest block leaves the new blocks unlinked with a zero header
+    checksum, so validating them fails; a trusted one links as the oracle."""
+    from tigerbeetle_amd import Engine, Grid
+    bs = 4096
+    with Engine(device=0, block_size=bs) as eng:
+        grid = Grid(eng, 16)
+        try:
+            first, _ = manifest.manifest_blocks(grid, _infos(40, 1), [5, 6], CLUSTER)
+            grid.put_blocks([3], np.pad(first[1], (0, bs - len(first[1])))[None])  # a valid manifest image
+            for prev in (3, 7):  # 3: staged from storage (unverified); 7: never written (not a manifest block)
+                images = manifest.pack_blocks(_infos(31, 2), [9, 10], CLUSTER, bs, previous_address=prev)
+                manifest.close_on_grid(grid, images, [9, 10], previous_address=prev, previous_checksum=None)
+                got = grid.get_blocks([9, 10])
+                assert not got[:, :16].any(), prev  # header checksums left zero
+                res = eng.validate_blocks([grid.pointer(9), grid.pointer(10)], [0, 0], [9, 10])
+                assert all(r == 1 for r in res), res  # invalid_checksum
+        finally:
+            grid.close()
+
+
 class _DictStore:
     """The oracle's close_block into a host dict (the CPU side of the log tests)."""
 

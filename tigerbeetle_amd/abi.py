@@ -34,7 +34,7 @@ COMPACTION_VALUES_ONLY = 1  # tbc_compaction.flags
 COMPACTION_GRID = 2
 COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped
 SPECULATION_NONE, SPECULATION_HELD, SPECULATION_BROKEN = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class TbcError(RuntimeError):
@@ -139,6 +139,8 @@ _SIGNATURES = {
     "tbc_tree_layout_get": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.POINTER(TreeLayout)]),
     "tbc_engine_arena_usage": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                               ctypes.POINTER(ctypes.c_uint32)]),
+    "tbc_host_register": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
+    "tbc_host_unregister": (ctypes.c_int, [_P, _P]),
     "tbc_device_alloc": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
     "tbc_device_free": (ctypes.c_int, [_P, _P]),
     "tbc_copy_to_device": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64]),

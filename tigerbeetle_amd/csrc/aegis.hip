@@ -545,14 +545,28 @@ __global__ __launch_bounds__(1024) void k_manifest_bodies(const uint64_t *addres
 // links the previous block's header checksum (the first block's comes from
 // the host, or from the header of `previous_address` in the grid, written by
 // an earlier close on this stream), then set_checksum over [16, 256).
+//
+// The grid's previous block is only linked if it is a verified manifest block
+// (BlockType.manifest = 3, schema.zig:63): otherwise nothing is chained, the
+// closed blocks keep a zero header checksum (so any later read fails
+// read_block_validate) and stay unverified. Linked blocks are marked verified
+// here, one store per block.
 __global__ __launch_bounds__(64) void k_manifest_chain(const uint64_t *addresses, uint32_t count, uint8_t *grid_base,
                                                        uint32_t block_size, uint64_t previous_address,
-                                                       const uint64_t *previous_checksum) {
+                                                       const uint64_t *previous_checksum, uint8_t *verified) {
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t hdr[64];
+    const uint32_t lane = threadIdx.x;
+    if (!previous_checksum && previous_address) {
+        const uint8_t *pb = grid_base + (size_t)(previous_address - 1) * block_size;
+        if (!verified[previous_address - 1] || pb[240] != 3) { // not a trusted manifest block: refuse to link
+            for (uint32_t i = 0; i < count; i++)
+                if (lane < 4) gst<uint32_t>(grid_base + (size_t)(addresses[i] - 1) * block_size + 4 * lane, 0u);
+            return;
+        }
+    }
     load_tables(sT);
     __syncthreads();
-    const uint32_t lane = threadIdx.x;
     uint32_t prev = 0; // lane c < 4: column c of the previous block's checksum
     if (lane < 4) {
         if (previous_checksum)
@@ -575,6 +589,7 @@ __global__ __launch_bounds__(64) void k_manifest_chain(const uint64_t *addresses
         // Lanes c < 4 of the lower group hold column c of the tag.
         if (lane < 4) gst<uint32_t>(blk + 4 * lane, tag);
         prev = lane < 4 ? tag : 0u;
+        if (lane == 0) verified[addresses[i] - 1] = 1; // engine-written: trusted like compaction outputs
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -1844,14 +1859,15 @@ int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_
 }
 
 int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *grid_base, uint32_t block_size,
-                          uint64_t previous_address, const uint64_t *d_previous_checksum, void *stream) {
+                          uint64_t previous_address, const uint64_t *d_previous_checksum, uint8_t *d_verified,
+                          void *stream) {
     if (count == 0) return 0;
     const uint32_t wpb = waves_per_block((count + 1) / 2);
     hipLaunchKernelGGL(k_manifest_bodies, dim3(((count + 1) / 2 + wpb - 1) / wpb), dim3(64 * wpb), 0,
                        (hipStream_t)stream, d_addresses, count, grid_base, block_size);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_manifest_chain, dim3(1), dim3(64), 0, (hipStream_t)stream, d_addresses, count, grid_base,
-                       block_size, previous_address, d_previous_checksum);
+                       block_size, previous_address, d_previous_checksum, d_verified);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -148,6 +148,11 @@ struct tbc_engine {
     int next_tail = 0;
     Arena dev, host;
     Staging staging;
+    // Host ranges the caller registered (tbc_host_register: hipHostRegister):
+    // blocks to or from them are copied by DMA directly, without the staging
+    // ring's host memcpy (TigerBeetle's I/O buffers are allocated once at
+    // startup, so a replica registers them once).
+    std::vector<std::pair<uint64_t, uint64_t>> registered;
     std::vector<hipEvent_t> event_pool;
     // Merge mask buffer (2 bits per merged position of a batch: 512 bytes
     // per tile). Batches run in stream order, so one buffer serves them all;
@@ -209,8 +214,18 @@ static hipEvent_t take_event(tbc_engine *e) {
     return ev;
 }
 
-// Host -> device through the pinned ring, enqueued on the engine stream.
+static bool is_registered(const tbc_engine *e, const void *p, uint64_t bytes) {
+    const uint64_t lo = (uint64_t)(uintptr_t)p, hi = lo + bytes;
+    for (const auto &r : e->registered)
+        if (r.first <= lo && hi <= r.second) return true;
+    return false;
+}
+
+// Host -> device through the pinned ring, enqueued on the engine stream
+// (registered memory: one direct DMA).
 static bool stage_h2d(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    if (is_registered(e, src, bytes))
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) == hipSuccess;
     Staging &st = e->staging;
     const uint8_t *s = (const uint8_t *)src;
     uint8_t *d = (uint8_t *)dst;
@@ -232,26 +247,85 @@ static bool stage_h2d(tbc_engine *e, void *dst, const void *src, uint64_t bytes)
     return true;
 }
 
-// Device -> host through the pinned ring (waits for each chunk).
-static bool stage_d2h(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+// Device -> host of many ranges. Registered destinations: direct DMA, one
+// wait at the end. Others through the pinned ring with every slot in flight:
+// a slot's chunk is copied out (host memcpy) only when the ring comes back to
+// it, so the DMA of the next chunks overlaps the memcpy of earlier ones
+// (round 3 waited for each chunk before issuing the next: 7.2 GB/s).
+struct D2H {
+    void *dst;
+    const void *src;
+    uint64_t bytes;
+};
+static bool stage_d2h_many(tbc_engine *e, const D2H *items, uint32_t count) {
     Staging &st = e->staging;
-    const uint8_t *s = (const uint8_t *)src;
-    uint8_t *d = (uint8_t *)dst;
-    while (bytes) {
-        const int slot = st.next;
-        st.next = (st.next + 1) % Staging::kSlots;
-        const uint64_t n = bytes < Staging::kSlotBytes ? bytes : Staging::kSlotBytes;
-        uint8_t *p = st.base + (uint64_t)slot * Staging::kSlotBytes;
-        if (hipMemcpyAsync(p, s, n, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-            hipEventRecord(st.ev[slot], e->stream) != hipSuccess || hipEventSynchronize(st.ev[slot]) != hipSuccess)
-            return false;
-        st.used[slot] = true;
-        memcpy(d, p, n);
-        s += n;
-        d += n;
-        bytes -= n;
+    struct Pending {
+        uint8_t *dst = nullptr;
+        uint64_t n = 0;
+    } pend[Staging::kSlots];
+    bool ok = true;
+    // A slot's earlier user (an H2D stage) must be done before it is refilled.
+    for (int k = 0; k < Staging::kSlots; k++)
+        if (st.used[k] && hipEventSynchronize(st.ev[k]) != hipSuccess) return false;
+    auto drain = [&](int slot) {
+        if (!pend[slot].n) return;
+        ok = ok && hipEventSynchronize(st.ev[slot]) == hipSuccess;
+        if (ok) memcpy(pend[slot].dst, st.base + (uint64_t)slot * Staging::kSlotBytes, pend[slot].n);
+        pend[slot].n = 0;
+    };
+    bool direct = false;
+    for (uint32_t i = 0; ok && i < count; i++) {
+        const uint8_t *s = (const uint8_t *)items[i].src;
+        uint8_t *d = (uint8_t *)items[i].dst;
+        uint64_t bytes = items[i].bytes;
+        if (is_registered(e, d, bytes)) {
+            ok = hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, e->stream) == hipSuccess;
+            direct = true;
+            continue;
+        }
+        while (ok && bytes) {
+            const int slot = st.next;
+            st.next = (st.next + 1) % Staging::kSlots;
+            drain(slot);
+            const uint64_t n = bytes < Staging::kSlotBytes ? bytes : Staging::kSlotBytes;
+            uint8_t *p = st.base + (uint64_t)slot * Staging::kSlotBytes;
+            ok = ok && hipMemcpyAsync(p, s, n, hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+                 hipEventRecord(st.ev[slot], e->stream) == hipSuccess;
+            st.used[slot] = true;
+            pend[slot].dst = d;
+            pend[slot].n = n;
+            s += n;
+            d += n;
+            bytes -= n;
+        }
     }
-    return true;
+    for (int k = 0; k < Staging::kSlots; k++) drain((st.next + k) % Staging::kSlots);
+    if (direct) ok = ok && hipStreamSynchronize(e->stream) == hipSuccess;
+    return ok;
+}
+
+// A list of 64-bit values (block addresses) copied to the device through a
+// pinned staging slot, into a device arena region the caller closes once the
+// work using it is enqueued (later arena users are later on the same stream).
+static const uint64_t *stage_u64s(tbc_engine *e, const uint64_t *values, uint32_t count, uint64_t *region) {
+    Staging &st = e->staging;
+    const uint64_t bytes = 8ull * count;
+    if (bytes > Staging::kSlotBytes) return nullptr;
+    const int slot = st.next;
+    st.next = (st.next + 1) % Staging::kSlots;
+    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return nullptr;
+    uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    memcpy(host, values, bytes);
+    uint8_t *d = e->dev.open(bytes, region);
+    if (!d) return nullptr;
+    const bool ok = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
+                    hipEventRecord(st.ev[slot], e->stream) == hipSuccess;
+    st.used[slot] = true;
+    if (!ok) {
+        e->dev.close(*region);
+        return nullptr;
+    }
+    return (const uint64_t *)d;
 }
 
 constexpr uint64_t kInitialMaskWords = (1ull << 28) / kMergeTile * (2 * kMergeTile / 64);
@@ -462,6 +536,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     for (auto &p : e->pending_sorts) e->event_pool.push_back(p.done);
     for (auto &t : e->tail_out) e->event_pool.push_back(t.done);
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
+    for (const auto &r : e->registered) hipHostUnregister((void *)(uintptr_t)r.first);
     if (e->sort_last) hipEventDestroy(e->sort_last);
     if (e->sort_stream) hipStreamDestroy(e->sort_stream);
     for (int s = 0; s < Staging::kSlots; s++)
@@ -535,12 +610,17 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
     if (!join_tails(e)) return TBC_ERR_DEVICE; // no running batch reads a block being replaced
-    for (uint32_t i = 0; i < count; i++) {
-        if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size) ||
-            hipMemsetAsync(g->verified + addresses[i] - 1, 0, 1, e->stream) != hipSuccess) // validate before trusting
+    if (!count) return TBC_OK;
+    for (uint32_t i = 0; i < count; i++)
+        if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size))
             return TBC_ERR_DEVICE;
-    }
-    return TBC_OK;
+    // Validate before trusting: one launch clears every staged block's verified byte.
+    uint64_t region = 0;
+    const uint64_t *d_addr = stage_u64s(e, addresses, count, &region);
+    if (!d_addr) return TBC_ERR_DEVICE;
+    const bool ok = launch_grid_set_verified(d_addr, count, g->verified, 0, e->stream) == 0;
+    e->dev.close(region);
+    return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *const *blocks, uint32_t count) {
@@ -550,10 +630,10 @@ tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *con
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
     if (!join_tails(e)) return TBC_ERR_DEVICE; // blocks still being sealed by a batch tail
+    std::vector<D2H> items(count);
     for (uint32_t i = 0; i < count; i++)
-        if (!stage_d2h(e, blocks[i], g->base + (addresses[i] - 1) * e->block_size, e->block_size))
-            return TBC_ERR_DEVICE;
-    return TBC_OK;
+        items[i] = D2H{blocks[i], g->base + (addresses[i] - 1) * e->block_size, e->block_size};
+    return stage_d2h_many(e, items.data(), count) ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *host_images,
@@ -609,15 +689,15 @@ tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, con
     uint64_t region = 0;
     uint8_t *d = e->dev.open(meta, &region);
     if (!d) return TBC_ERR_OUT_OF_MEMORY;
+    // The chain kernel marks the closed blocks verified (trusted like
+    // compaction outputs), or refuses to link an untrusted previous block.
     bool ok = hipMemcpyAsync(d, host, meta, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
               launch_manifest_close((const uint64_t *)d, count, g->base, bs, previous_address,
-                                    previous_checksum ? (const uint64_t *)(d + 8ull * count) : nullptr, e->stream) == 0 &&
+                                    previous_checksum ? (const uint64_t *)(d + 8ull * count) : nullptr, g->verified,
+                                    e->stream) == 0 &&
               hipEventRecord(st.ev[slot], e->stream) == hipSuccess;
     st.used[slot] = true;
     e->dev.close(region);
-    // Engine-written manifest blocks are trusted like compaction outputs.
-    for (uint32_t i = 0; ok && i < count; i++)
-        ok = hipMemsetAsync(g->verified + addresses[i] - 1, 1, 1, e->stream) == hipSuccess;
     return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
 
@@ -690,6 +770,31 @@ tbc_status tbc_tree_layout_get(const tbc_engine *e, const tbc_tree *tree, tbc_tr
     out->index_keys_max_offset = L.kmax_off;
     out->index_addresses_offset = L.addr_off;
     return TBC_OK;
+}
+
+tbc_status tbc_host_register(tbc_engine *e, void *ptr, uint64_t bytes) {
+    if (!e || !ptr || !bytes) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    const uint64_t lo = (uint64_t)(uintptr_t)ptr;
+    for (const auto &r : e->registered)
+        if (lo < r.second && r.first < lo + bytes) return TBC_ERR_INVALID_ARGUMENT; // overlaps a registered range
+    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) return TBC_ERR_DEVICE;
+    e->registered.push_back({lo, lo + bytes});
+    return TBC_OK;
+}
+
+tbc_status tbc_host_unregister(tbc_engine *e, void *ptr) {
+    if (!e || !ptr) return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    const uint64_t lo = (uint64_t)(uintptr_t)ptr;
+    for (size_t i = 0; i < e->registered.size(); i++)
+        if (e->registered[i].first == lo) {
+            // Copies from or into it may still be enqueued.
+            if (tbc_synchronize(e) != TBC_OK) return TBC_ERR_DEVICE;
+            e->registered.erase(e->registered.begin() + (long)i);
+            return hipHostUnregister(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+        }
+    return TBC_ERR_INVALID_ARGUMENT;
 }
 
 tbc_status tbc_device_alloc(tbc_engine *e, uint64_t bytes, void **out_ptr) {
@@ -1081,7 +1186,6 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
             return TBC_ERR_DEVICE;
         }
         if (e->kway_scratch) hipFree(e->kway_scratch);
-    if (e->copy_desc) hipFree(e->copy_desc);
         e->kway_scratch = nullptr;
         e->kway_scratch_size = 0;
         const uint64_t want = align_up(need + need / 8, 1ull << 24);

@@ -141,6 +141,24 @@ int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, cons
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// One thread per address: the grid's `verified` byte of each block set to
+// `value` (blocks staged from storage: 0, validated before they are trusted;
+// blocks the engine wrote: 1), one launch for a whole list instead of one
+// 1-byte fill per block.
+__global__ __launch_bounds__(256) void k_grid_set_verified(const uint64_t *addresses, uint32_t count, uint8_t *verified,
+                                                           uint8_t value) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < count) verified[addresses[i] - 1] = value;
+}
+
+int launch_grid_set_verified(const uint64_t *d_addresses, uint32_t count, uint8_t *d_verified, uint8_t value,
+                             void *stream) {
+    if (!count) return 0;
+    hipLaunchKernelGGL(k_grid_set_verified, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_addresses,
+                       count, d_verified, value);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // tbc_copy_device_batch: many device-to-device copies (16-byte aligned,
 // multiples of 16 bytes) in one launch. One workgroup per 64 KiB chunk:
 // every lane's sixteen 16-byte loads are issued before its stores.

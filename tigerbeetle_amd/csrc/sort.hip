@@ -103,6 +103,7 @@ struct SortSeg {
 
 struct SortBatch {
     uint32_t active; // passes some table needs
+    uint32_t broken; // a pass hit a wait bound (a broken invariant): k_sort_rescue re-sorts every moved table
 };
 
 __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t ts_off, uint64_t k[3]) {
@@ -479,7 +480,7 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
                                                 const uint32_t *tile_order, uint32_t p, uint32_t ntiles,
                                                 uint64_t *words0, uint64_t *words1, const uint32_t *bins,
                                                 uint64_t *status, uint32_t epoch, uint32_t *tile_counter,
-                                                uint32_t *done) {
+                                                uint32_t *done, SortBatch *batch) {
     constexpr uint32_t R = kSortRounds;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t ep = (uint64_t)epoch << 32;
@@ -507,7 +508,10 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
             if (tid == 0) {
                 for (uint32_t spins = 0; __hip_atomic_load(&done[p - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                                              ntiles;) {
-                    if (++spins > (1u << 26)) break; // bounded (a broken invariant, not a hang)
+                    if (++spins > (1u << 26)) { // bounded: a broken invariant, reported, not a hang
+                        atomicOr(&batch->broken, 1u);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(2);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -624,7 +628,10 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
                 }
                 if (fin) break;
                 if (stall) {
-                    if (++spins > (1u << 24)) break; // bounded (a broken invariant, not a hang)
+                    if (++spins > (1u << 24)) { // bounded: a broken invariant, reported, not a hang
+                        atomicOr(&batch->broken, 1u);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                 } else {
                     pred -= kLook;
@@ -646,7 +653,7 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
 
 // One launch per pass below kDirectPasses: the kernel boundary orders the
 // passes. A pass no table needs returns at once.
-__global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass(const SortSeg *segs, const SortBatch *batch,
+__global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass(const SortSeg *segs, SortBatch *batch,
                                                             const uint32_t *tile_seg, const uint32_t *tile_order,
                                                             uint32_t p, uint32_t ntiles, uint64_t *words0,
                                                             uint64_t *words1, const uint32_t *bins, uint64_t *status,
@@ -654,7 +661,7 @@ __global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass(const SortSeg *se
     __shared__ PassShared sh;
     if (!((batch->active >> p) & 1u)) return; // uniform: no table has this many passes
     sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, words0, words1, bins, status, epoch, tile_counter,
-                    nullptr);
+                    nullptr, batch);
 }
 
 // Passes [kDirectPasses, kMaxPasses) in ONE launch (most batches need none:
@@ -664,7 +671,7 @@ __global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass(const SortSeg *se
 // grid barrier, no residency assumption), and the completion counters with
 // agent-scope release/acquire order the passes across XCDs. Each pass takes
 // a fresh look-back epoch.
-__global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass_rest(const SortSeg *segs, const SortBatch *batch,
+__global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass_rest(const SortSeg *segs, SortBatch *batch,
                                                                  const uint32_t *tile_seg, const uint32_t *tile_order,
                                                                  uint32_t ntiles, uint64_t *words0, uint64_t *words1,
                                                                  const uint32_t *bins, uint64_t *status,
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(kSortThreads, 3) void k_sort_pass_rest(const SortSe
     for (uint32_t p = kDirectPasses; p < kMaxPasses; p++) {
         if (!((batch->active >> p) & 1u)) return; // passes run as a prefix: none beyond either
         sort_pass_tiles(sh, segs, tile_seg, tile_order, p, ntiles, words0, words1, bins, status,
-                        epoch0 + (p - kDirectPasses), tile_counter, done);
+                        epoch0 + (p - kDirectPasses), tile_counter, done, batch);
         // Its last tile's stores are released and counted before the next pass.
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __syncthreads();
@@ -773,14 +780,18 @@ __device__ __forceinline__ void pack_bytes(const uint8_t *map, uint32_t nb, cons
     }
 }
 
-__global__ __launch_bounds__(256) void k_sort_rescue(SortSeg *segs, uint32_t N, uint64_t *keys0, uint64_t *keys1,
-                                                     uint32_t *idx0, uint32_t *idx1) {
+__global__ __launch_bounds__(256) void k_sort_rescue(SortSeg *segs, const SortBatch *batch, uint32_t N,
+                                                     uint64_t *keys0, uint64_t *keys1, uint32_t *idx0, uint32_t *idx1) {
     __shared__ uint8_t s_map[kMaxBytes];
     __shared__ uint32_t s_off[kRadix];
     __shared__ uint32_t s_wc[4][kRadix];
     __shared__ uint32_t s_wsum[4];
     const SortSeg S = segs[blockIdx.x];
-    if (!S.overflow) return;
+    // A pass that hit a wait bound (SortBatch.broken) may have left any moved
+    // table's words incomplete: every such table is sorted again from its
+    // put-order copy, so a broken invariant costs time, never order.
+    const bool broken = *(volatile const uint32_t *)&batch->broken != 0 && S.nact;
+    if (!S.overflow && !broken) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < kMaxBytes) s_map[tid] = segs[blockIdx.x].byte_src[tid];
     __syncthreads();
@@ -1019,7 +1030,8 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     }
     hipLaunchKernelGGL(k_sort_finish, dim3(ntiles * (kSortTile / kFinishItems)), dim3(256), 0, s, d_segs,
                        (const uint32_t *)d_tile, (const uint64_t *)words0, (const uint64_t *)words1);
-    hipLaunchKernelGGL(k_sort_rescue, dim3(nseg), dim3(256), 0, s, d_segs, N, keys0, keys1, idx0, idx1);
+    hipLaunchKernelGGL(k_sort_rescue, dim3(nseg), dim3(256), 0, s, d_segs, (const SortBatch *)d_batch, N, keys0,
+                       keys1, idx0, idx1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

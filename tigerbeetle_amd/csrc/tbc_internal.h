@@ -330,8 +330,16 @@ int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, cons
 uint32_t fused_max_chain_waves();
 // ManifestLog.close_block of `count` staged manifest blocks (grid addresses in
 // d_addresses): body checksums, then the header chain in order.
+// previous_address (with no d_previous_checksum) must name a verified manifest
+// block of the grid; otherwise the new blocks' header checksums are left
+// zero (every later read fails validation) and they stay unverified. Closed
+// blocks are marked verified by the chain kernel itself.
 int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *grid_base, uint32_t block_size,
-                          uint64_t previous_address, const uint64_t *d_previous_checksum, void *stream);
+                          uint64_t previous_address, const uint64_t *d_previous_checksum, uint8_t *d_verified,
+                          void *stream);
+// The grid's `verified` byte of every listed block set to `value` (one launch).
+int launch_grid_set_verified(const uint64_t *d_addresses, uint32_t count, uint8_t *d_verified, uint8_t value,
+                             void *stream);
 int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32_t count, uint8_t *d_out,
                           void *stream);
 // One copy of tbc_copy_device_batch: chunks [chunk0, chunk0 + ceil(bytes / copy_chunk_bytes())).

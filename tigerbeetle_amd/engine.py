@@ -152,9 +152,14 @@ class Grid:
         check(lib().tbc_grid_put_blocks(self.handle, A.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), P, n),
               "tbc_grid_put_blocks")
 
-    def get_blocks(self, addresses) -> np.ndarray:
+    def get_blocks(self, addresses, out: np.ndarray | None = None) -> np.ndarray:
+        """Copy blocks to host images (n, block_size); `out` may be a
+        preallocated (e.g. host-registered) array of at least n rows."""
         n = len(addresses)
-        out = np.zeros((max(1, n), self.engine.block_size), dtype=np.uint8)
+        if out is None:
+            out = np.zeros((max(1, n), self.engine.block_size), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.shape[0] >= n
+        assert out.shape[1] == self.engine.block_size
         A = np.ascontiguousarray(addresses, dtype=np.uint64)
         P = (ctypes.c_void_p * max(1, n))(*[out.ctypes.data + i * self.engine.block_size for i in range(n)])
         check(lib().tbc_grid_get_blocks(self.handle, A.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), P, n),
@@ -316,6 +321,16 @@ class Engine:
 
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
+
+    def host_register(self, array: np.ndarray) -> None:
+        """tbc_host_register: grid block transfers into or out of this
+        (contiguous) host array go by DMA without the staging ring's copy.
+        The caller keeps the array alive until host_unregister."""
+        assert array.flags.c_contiguous and array.nbytes
+        check(lib().tbc_host_register(self.handle, array.ctypes.data, array.nbytes), "tbc_host_register")
+
+    def host_unregister(self, array: np.ndarray) -> None:
+        check(lib().tbc_host_unregister(self.handle, array.ctypes.data), "tbc_host_unregister")
 
     def upload(self, array: np.ndarray, pad: int = 0) -> DeviceBuffer:
         a = np.ascontiguousarray(array)
