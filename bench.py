@@ -57,8 +57,8 @@ class Workload:
         self.sort_bytes = 0
         self.out_bytes = 0
         self.job_args = []
-        self.jobs_alt: list = []
-        self.flip = 0
+        self.job_sets: list = []  # output sets beyond the first (rotate())
+        self.turn = 0
         base_addr = 1
         for gid in job_ids:
             js = configs.GENERATORS[config](gid)
@@ -121,30 +121,33 @@ class Workload:
             self.bufs.append(out)
             del js
 
-    def double_buffer(self, eng: Engine, limit: int = 64 << 30) -> bool:
-        """A second set of output blocks, so that consecutive steps write
-        different blocks and step k+1's fronts may run beside step k's
-        chains (the engine makes a batch wait for an earlier tail only when
-        their outputs alias). Skipped above `limit` bytes of outputs."""
-        if self.out_bytes > limit or self.jobs_alt:
-            return bool(self.jobs_alt)
-        for spec, segs_a, segs_b, a_imm, drop, level_b, addrs, flags, nbytes in self.job_args:
-            out = eng.alloc(nbytes)
-            self.bufs.append(out)
-            self.jobs_alt.append(Job(spec, segs_a, segs_b, a_imm, drop, level_b, 0xA5A5, 48, addrs, out,
-                                     flags=flags))
-        return True
+    def rotate(self, eng: Engine, sets: int, limit: int = 96 << 30) -> int:
+        """Output sets for `sets` steps in flight: consecutive steps write
+        different blocks, so step k+1's fronts may run beside step k's chains
+        (the engine makes a batch wait for an earlier tail only when their
+        outputs alias, as a replica's half-bars write freshly acquired
+        addresses). As many sets as fit under `limit` bytes of outputs;
+        returns the number of sets."""
+        while 1 + len(self.job_sets) < sets and (2 + len(self.job_sets)) * self.out_bytes <= limit:
+            jobs = []
+            for spec, segs_a, segs_b, a_imm, drop, level_b, addrs, flags, nbytes in self.job_args:
+                out = eng.alloc(nbytes)
+                self.bufs.append(out)
+                jobs.append(Job(spec, segs_a, segs_b, a_imm, drop, level_b, 0xA5A5, 48, addrs, out, flags=flags))
+            self.job_sets.append(jobs)
+        return 1 + len(self.job_sets)
 
     def submit(self, eng: Engine):
         """Land + sort the bar's memtables (config 3), then submit the
-        compaction batch (no wait). With double_buffer(), steps alternate
-        between the two output sets."""
+        compaction batch (no wait). With rotate(), steps take the output
+        sets in turn."""
         if self.landings:
             eng.copy_device_batch(self.landings)
         if self.sorts:
             eng.sort_values_batch(self.sorts)
-        jobs = self.jobs_alt if (self.jobs_alt and self.flip) else self.jobs
-        self.flip ^= 1
+        sets = [self.jobs] + self.job_sets
+        jobs = sets[self.turn % len(sets)]
+        self.turn += 1
         return eng.submit(jobs)
 
     def step(self, eng: Engine):
@@ -487,8 +490,11 @@ def main() -> None:
                     help="config 5: BASELINE's 1B values (216 jobs) divided over the GPUs (strong scaling)")
     ap.add_argument("--no-split", action="store_true", help="config 4 at N > 1: shard whole jobs only")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="wait for each step before submitting the next (default: step k+1 is enqueued before "
-                         "step k is waited for, so the host's submit and wake-up do not idle the GPU)")
+                    help="wait for each step before submitting the next (default: steps are enqueued ahead, see "
+                         "--depth, so the host's submit and wake-up do not idle the GPU)")
+    ap.add_argument("--depth", type=int, default=3,
+                    help="steps in flight: step k+D-1 is enqueued before step k is waited for, and the outputs "
+                         "rotate over D sets (a replica's consecutive half-bars write freshly acquired blocks)")
     args = ap.parse_args()
     njobs = args.jobs or configs.DEFAULT_JOBS.get(args.config, 1)
 
@@ -550,8 +556,40 @@ def main() -> None:
         b.wait()
         return b
 
-    for _ in range(args.warmup):
-        step().release()
+    # Steps run back to back on the engine's streams (the same work each
+    # step, every step's results checked below for the last one). Overlapped:
+    # up to `depth` steps are enqueued before the oldest is waited for (each
+    # batch has its own arena region and results; the outputs rotate over
+    # `depth` sets; stream order keeps the mask buffer consistent), so the
+    # device never idles for the host and consecutive steps' AEGIS chains
+    # share the chip (the engine pipelines a UNIQUE_KEYS batch submitted
+    # while another is running). A split step (config 4, N > 1) exchanges
+    # between its phases: sequential.
+    overlap = not args.no_overlap and part is None
+    depth = max(1, args.depth) if overlap else 1
+    out_sets = wl.rotate(eng, depth) if overlap else 1
+    depth = min(depth, out_sets)
+    ktimes: dict = {}
+    marks = []
+
+    def finish(b, record=True):
+        b.wait()
+        if record:
+            marks.append(time.perf_counter())
+            for k, v in b.kernel_times().items():
+                ktimes[k] = ktimes.get(k, 0.0) + v
+        b.release()
+
+    def run(nsteps, record=True):
+        pending = []
+        for _ in range(nsteps):
+            pending.append(submit())
+            if len(pending) >= depth:
+                finish(pending.pop(0), record)
+        while pending:
+            finish(pending.pop(0), record)
+
+    run(args.warmup, record=False)  # the same loop (and code paths) as the timed steps
 
     def barrier():
         eng.synchronize()
@@ -565,42 +603,22 @@ def main() -> None:
     gc.collect()
     gc.disable()  # no collector pause inside the timed region
     t0 = time.perf_counter()
-    ktimes: dict = {}
-    marks = []
-
-    def finish(b):
-        b.wait()
-        marks.append(time.perf_counter())
-        for k, v in b.kernel_times().items():
-            ktimes[k] = ktimes.get(k, 0.0) + v
-        b.release()
-
-    # Steps run back to back on the engine's streams (the same work each
-    # step, every step's results checked below for the last one). Overlapped:
-    # step k+1 is enqueued before step k is waited for (each batch has its
-    # own arena region and results; stream order keeps the shared outputs
-    # and mask buffer consistent), so the device never idles for the host.
-    # A split step (config 4, N > 1) exchanges between its phases: sequential.
-    overlap = not args.no_overlap and part is None
-    doubled = overlap and wl.double_buffer(eng)
-    pending = None
-    for _ in range(args.steps):
-        b = submit()
-        if not overlap:
-            finish(b)
-            continue
-        if pending is not None:
-            finish(pending)
-        pending = b
-    if pending is not None:
-        finish(pending)
+    run(args.steps)
     barrier()
     gc.enable()
     if os.environ.get("TBC_BENCH_TRACE"):
         print("step ms:", " ".join(f"{(b - a) * 1e3:.2f}" for a, b in zip([t0] + marks, marks)), file=sys.stderr)
     dt = time.perf_counter() - t0
-    # Check the last step's results: every job OK, and output shape for the bytes.
-    b = step()
+    # Check a step's results: every job OK, and output shape for the bytes
+    # (submitted behind another, so it takes the timed steps' path).
+    if overlap:
+        b_prev = submit()
+        b = submit()
+        b_prev.wait()
+        b_prev.release()
+        b.wait()
+    else:
+        b = step()
     out_values = data_blocks = tables = index_bytes = 0
     if part is not None:
         assert part.result is not None and (part.result.result is None or part.result.result.status == 0)
@@ -665,7 +683,7 @@ def main() -> None:
                    "jobs_per_gpu": njobs, "input_bytes_per_gpu": wl.input_bytes, "block_size": bs,
                    "parallelism": f"shard-by-job x{world}" + (f" + key-range split of job {split_id}"
                                                                 if split_id is not None else ""),
-                   "steps_overlapped": overlap, "outputs_double_buffered": doubled},
+                   "steps_overlapped": overlap, "steps_in_flight": depth, "output_sets": out_sets},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

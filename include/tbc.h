@@ -90,6 +90,14 @@ typedef struct tbc_config {
 } tbc_config;
 
 #define TBC_CONFIG_PROFILE 1u /* record hipEvents around every kernel (tbc_batch_kernel_times) */
+/* Block pass of TBC_COMPACTION_UNIQUE_KEYS batches. By default a batch
+ * submitted while an earlier batch's tail is still running is pipelined (its
+ * bodies merged on the engine stream, its AEGIS chains on a tail stream
+ * beside other batches' chains: throughput), and a batch submitted alone
+ * takes the fused pass (every chain at once, bodies built beside them:
+ * latency). PIPELINE / LATENCY force one or the other. */
+#define TBC_CONFIG_PIPELINE 2u
+#define TBC_CONFIG_LATENCY 4u
 
 typedef struct tbc_engine tbc_engine;
 typedef struct tbc_batch tbc_batch;

@@ -34,3 +34,21 @@ def engine_small():
     e = Engine(device=0, block_size=4096)
     yield e
     e.close()
+
+
+@pytest.fixture(scope="session")
+def engine_pipe():
+    """1 MiB blocks, UNIQUE_KEYS batches always pipelined (TBC_CONFIG_PIPELINE):
+    bodies merged on the engine stream, chains on a tail stream."""
+    from tigerbeetle_amd import Engine
+    e = Engine(device=0, block_size=1 << 20, profile=True, pipeline=True)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="session")
+def engine_small_pipe():
+    from tigerbeetle_amd import Engine
+    e = Engine(device=0, block_size=4096, profile=True, pipeline=True)
+    yield e
+    e.close()

@@ -273,7 +273,7 @@ def test_grid_block_transfers_staged_and_registered(engine):
         try:
             grid.put_blocks(addrs, reg_in)
             got = grid.get_blocks(addrs, out=reg_out)
-            assert got is reg_out and np.array_equal(reg_out, reg_in)
+            assert np.shares_memory(got, reg_out) and np.array_equal(reg_out, reg_in)
             with pytest.raises(abi.TbcError):  # overlapping registration refused
                 engine.host_register(reg_in[1:3])
         finally:

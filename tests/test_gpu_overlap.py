@@ -98,8 +98,9 @@ def test_back_to_back_speculated_batches_share_outputs(engine, oracle_lib):
         outs.append(out)
     keep = []
     fl = abi.COMPACTION_UNIQUE_KEYS
-    b1 = engine.submit(_jobs(engine, first, addrs, outs, keep, bs, fl))
-    b2 = engine.submit(_jobs(engine, second, addrs, outs, keep, bs, fl))
+    j1, j2 = _jobs(engine, first, addrs, outs, keep, bs, fl), _jobs(engine, second, addrs, outs, keep, bs, fl)
+    b1 = engine.submit(j1)
+    b2 = engine.submit(j2)
     b1.wait()
     b2.wait()
     for i, (ji, a, out) in enumerate(zip(second, addrs, outs)):
@@ -113,3 +114,55 @@ def test_back_to_back_speculated_batches_share_outputs(engine, oracle_lib):
         assert np.array_equal(infos, o.table_infos)
     b1.release()
     b2.release()
+
+
+@pytest.mark.gpu
+def test_speculated_batches_pipelined_three_in_flight(engine, oracle_lib):
+    """Round 4: a UNIQUE_KEYS batch submitted while an earlier batch's tail is
+    running is pipelined (bodies merged by k_produce_unique on the engine
+    stream, chains on a tail stream beside the earlier batches' chains).
+    Three batches into three output sets, then a fourth into the first set
+    (it must wait for the first batch's tail), submitted without waiting;
+    held and broken speculations mixed. Every batch's TableInfos and the
+    final blocks of every output set equal the oracle's."""
+    from tigerbeetle_amd import abi
+    bs = 1 << 20
+    names = ["transfers.id", "transfers.timestamp", "transfers.debit_account_id", "transfers.amount"]
+    rng_a = np.random.default_rng(413)
+    kw = dict(n_a=60_000, b_table_sizes=[50_000, 40_000], a_immutable=False, overlap=0.0)
+    kw_broken = dict(kw, overlap=0.01)
+    inputs = []
+    for step in range(4):
+        rng = np.random.default_rng(400 + step)
+        inputs.append([workloads.make_job_inputs(trees.BY_NAME[n], rng, **(kw_broken if (step + i) % 3 == 0 else kw))
+                       for i, n in enumerate(names)])
+    addrs = [np.asarray(workloads.addresses_for(workloads.worst_case_blocks(trees.BY_NAME[n], 150_000, bs) + 3,
+                                                rng_a, 1, 0.1), dtype=np.uint64) for n in names]
+    sets = []
+    for _ in range(3):
+        outs = []
+        for a in addrs:
+            out = engine.alloc(len(a) * bs)
+            out.zero()
+            outs.append(out)
+        sets.append(outs)
+    keep = []
+    fl = abi.COMPACTION_UNIQUE_KEYS
+    job_lists = [_jobs(engine, inputs[s], addrs, sets[s % 3], keep, bs, fl) for s in range(4)]  # staged first
+    batches = [engine.submit(jl) for jl in job_lists]  # back to back: earlier tails still running
+    for b in batches:
+        b.wait()
+    for s, b in enumerate(batches):
+        if s:  # submitted while an earlier batch's tail ran: the pipelined pass
+            assert "produce" in b.kernel_times(), s
+        for i, ji in enumerate(inputs[s]):
+            r, infos = b.result(i)
+            o = run_oracle(oracle_lib, ji, bs, addrs[i])
+            assert r.status == 0 and o.status == 0
+            assert r.block_count == len(o.blocks) and np.array_equal(infos, o.table_infos), (s, i)
+            if s >= 1:  # set 0's blocks are batch 3's (batch 0's were overwritten)
+                got = sets[s % 3][i].download(r.block_count * bs).reshape(-1, bs)
+                for k, (g, w) in enumerate(zip(got, o.blocks)):
+                    assert np.array_equal(disk_image(g), disk_image(w)), (s, ji.tree.name, k)
+    for b in batches:
+        b.release()

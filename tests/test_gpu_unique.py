@@ -17,6 +17,19 @@ from tigerbeetle_amd import abi, trees, workloads
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(params=["fused", "pipelined"])
+def eng_small(request, engine_small, engine_small_pipe):
+    """Both block passes of a speculated batch (engine.hip submit_impl): the
+    fused latency pass (a batch alone), and the pipelined one (bodies merged
+    by k_produce_unique on the engine stream, chains on a tail stream)."""
+    return engine_small if request.param == "fused" else engine_small_pipe
+
+
+@pytest.fixture(params=["fused", "pipelined"])
+def eng(request, engine, engine_pipe):
+    return engine if request.param == "fused" else engine_pipe
+
 U = abi.COMPACTION_UNIQUE_KEYS
 HELD, BROKEN, NONE = abi.SPECULATION_HELD, abi.SPECULATION_BROKEN, abi.SPECULATION_NONE
 
@@ -59,7 +72,7 @@ UNIQUE_TREES = ["transfers.id", "transfers.timestamp", "transfers.debit_account_
 
 
 @pytest.mark.parametrize("name", UNIQUE_TREES)
-def test_unique_held_small_blocks(oracle_lib, engine_small, name):
+def test_unique_held_small_blocks(oracle_lib, eng_small, name):
     """Unique keys (disk A, immutable A, A only, B only): speculation holds."""
     cases = [
         (name, dict(n_a=3000, b_table_sizes=[2000, 1500, 900], a_immutable=False, overlap=0.0), U, HELD),
@@ -68,12 +81,12 @@ def test_unique_held_small_blocks(oracle_lib, engine_small, name):
         (name, dict(n_a=0, b_table_sizes=[777, 123], a_immutable=False, overlap=0.0), U, HELD),
         (name, dict(n_a=1, b_table_sizes=[1], a_immutable=False, overlap=0.0), U, HELD),
     ]
-    _run(oracle_lib, engine_small, cases, 4096, seed=11)
+    _run(oracle_lib, eng_small, cases, 4096, seed=11)
 
 
 @pytest.mark.parametrize("name", ["transfers.id", "transfers.timestamp", "transfers.debit_account_id",
                                   "accounts.ledger"])
-def test_unique_broken_small_blocks(oracle_lib, engine_small, name):
+def test_unique_broken_small_blocks(oracle_lib, eng_small, name):
     """Repeated keys (A/B overlap, immutable duplicates, secondary put/remove
     pairs) and dropped tombstones break the speculation; the recomputation
     must give the merge path's blocks, beside jobs whose speculation holds and
@@ -91,7 +104,7 @@ def test_unique_broken_small_blocks(oracle_lib, engine_small, name):
         # tombstones kept (not the last level): speculation holds
         cases.append((name, dict(n_a=2500, b_table_sizes=[900], a_immutable=False, overlap=0.0, tomb_frac=0.05),
                       U, HELD))
-    _run(oracle_lib, engine_small, cases, 4096, seed=12)
+    _run(oracle_lib, eng_small, cases, 4096, seed=12)
 
 
 def _repeat_at_block_start(spec, vcm, block: int, first_in_a: bool, seed: int) -> workloads.JobInputs:
@@ -119,19 +132,19 @@ def _repeat_at_block_start(spec, vcm, block: int, first_in_a: bool, seed: int) -
 
 
 @pytest.mark.parametrize("block,first_in_a", [(1, True), (1, False), (2, True), (4, False)])
-def test_unique_one_repeat_at_a_block_boundary(oracle_lib, engine_small, block, first_in_a):
+def test_unique_one_repeat_at_a_block_boundary(oracle_lib, eng_small, block, first_in_a):
     """A single repeated key exactly where a data block starts: the check that
     crosses producers (a producer's first value against its predecessor in
     the previous block) must break the speculation, and the recomputed blocks
     must be the reference's. Constructed, never skipped."""
     spec = _spec("transfers.id", 4096)
-    vcm = engine_small.layout(spec).block_value_count_max
+    vcm = eng_small.layout(spec).block_value_count_max
     ji = _repeat_at_block_start(spec, vcm, block, first_in_a, seed=3 + block)
     n = len(ji.a_values) + sum(len(t) for t in ji.b_tables)
     rng = np.random.default_rng(5)
     addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, n, 4096) + 3, rng, 5)
     outcome = []
-    (res,), _ = gpu_run(engine_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
+    (res,), _ = gpu_run(eng_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
     r, infos, blocks = res
     o = run_oracle(oracle_lib, ji, 4096, addrs)
     assert o.status == 0 and r.status == 0
@@ -143,11 +156,11 @@ def test_unique_one_repeat_at_a_block_boundary(oracle_lib, engine_small, block, 
     assert np.array_equal(infos, o.table_infos)
 
 
-def test_unique_no_repeat_at_block_starts_holds(oracle_lib, engine_small):
+def test_unique_no_repeat_at_block_starts_holds(oracle_lib, eng_small):
     """The same construction without the repeat (A/B alternate across every
     block start): the speculation holds."""
     spec = _spec("transfers.id", 4096)
-    vcm = engine_small.layout(spec).block_value_count_max
+    vcm = eng_small.layout(spec).block_value_count_max
     rng = np.random.default_rng(9)
     n = 6 * vcm + 17
     limbs = workloads.unique_sorted_keys(spec, n, rng)
@@ -158,7 +171,7 @@ def test_unique_no_repeat_at_block_starts_holds(oracle_lib, engine_small):
     ji = workloads.JobInputs(spec, vals[in_a], False, [b[i:i + tmax] for i in range(0, len(b), tmax)], False)
     addrs = workloads.addresses_for(workloads.worst_case_blocks(spec, n, 4096) + 3, rng, 5)
     outcome = []
-    (res,), _ = gpu_run(engine_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
+    (res,), _ = gpu_run(eng_small, [ji], 4096, [addrs], flags=U, speculation=outcome)
     r, infos, blocks = res
     o = run_oracle(oracle_lib, ji, 4096, addrs)
     assert outcome == [HELD] and r.block_count == len(o.blocks)
@@ -167,11 +180,11 @@ def test_unique_no_repeat_at_block_starts_holds(oracle_lib, engine_small):
     assert np.array_equal(infos, o.table_infos)
 
 
-def test_unique_config2_shape(oracle_lib, engine):
+def test_unique_config2_shape(oracle_lib, eng):
     """1 MiB blocks, BASELINE config 2's job shape scaled down (disk A + 8 B
     tables of the transfers.id tree), held; plus one broken job in the batch."""
     name = "transfers.id"
     cases = [(name, dict(n_a=120_000, b_table_sizes=[40_000] * 8, a_immutable=False, overlap=0.0), U, HELD)
              for _ in range(3)]
     cases.append((name, dict(n_a=90_000, b_table_sizes=[30_000] * 4, a_immutable=False, overlap=0.001), U, BROKEN))
-    _run(oracle_lib, engine, cases, 1 << 20, seed=21)
+    _run(oracle_lib, eng, cases, 1 << 20, seed=21)

@@ -30,6 +30,8 @@ STATUS_NAMES = {
 KEY_TIMESTAMP, KEY_ID_U128, KEY_COMPOSITE_U64, KEY_COMPOSITE_U128 = 0, 1, 2, 3
 USAGE_GENERAL, USAGE_SECONDARY_INDEX = 0, 1
 CONFIG_PROFILE = 1
+CONFIG_PIPELINE = 2
+CONFIG_LATENCY = 4
 COMPACTION_VALUES_ONLY = 1  # tbc_compaction.flags
 COMPACTION_GRID = 2
 COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped

@@ -1573,7 +1573,11 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         // VALU lane moves that win when a chain waits alone on LDS latency.
         // k_assemble ran before this kernel (stream order): every survivor of
         // the block must have landed.
-        if (__hip_atomic_load(ready + j.dblock_base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
+        // (A speculated job whose speculation held was merged by
+        // k_produce_unique, before this kernel in stream order: no counts.)
+        const bool produced = j.unique && res[j.job_index].spec != kSpecBroken;
+        if (!produced &&
+            __hip_atomic_load(ready + j.dblock_base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
             gst<uint32_t>(const_cast<uint32_t *>(&res[j.job_index].invariant), 0xdeafu);
         GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
         body_tag = aegis_mac32<GlobalMsg, ChainStep>(sT, body);
@@ -1599,6 +1603,50 @@ __global__ __launch_bounds__(3 * 64 * kMaxChainWaves) void k_data_blocks_redo(
     const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
     const uint32_t *ready) {
     data_blocks<true>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready, nullptr, 1u);
+}
+
+// Pipelined speculated batches (engine.hip submit_impl, round 4): the bodies
+// of every speculated job's data blocks, one producer wave per block
+// (produce_unique: the block merges its own positions, speculation checks
+// included), on the engine stream with no chain beside it and no throttle;
+// the chains run later on a tail stream (k_data_blocks<false>), so chains of
+// consecutive batches share the chip while the next batch's bodies are
+// merged. A workgroup is kProduceWaves producers with their LDS staging
+// only (no T-tables), so it fits beside the chain workgroups of running tails.
+constexpr uint32_t kProduceWaves = 4;
+
+__global__ __launch_bounds__(64 * kProduceWaves) void k_produce_unique(const JobDesc *jobs, int njobs, uint32_t total,
+                                                                       const JobResultDev *res,
+                                                                       const SplitDesc *bsplits) {
+    __shared__ uint64_t sStage[kProduceWaves][kStageWords];
+    __shared__ uint32_t sProg[kProduceWaves];
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t m = blockIdx.x * kProduceWaves + w;
+    if (m >= total) return; // wave-uniform (producers use wave-level barriers only)
+    const int ji = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
+    const JobDesc &j = jobs[ji];
+    const uint32_t k = m - j.dblock_base;
+    if (!j.unique || k >= res[j.job_index].data_block_count) return;
+    const uint64_t n_out = res[j.job_index].value_count, first = (uint64_t)k * j.vcm;
+    const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
+    uint8_t *body = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize;
+    const SplitDesc sp = bsplits[j.dblock_base + k];
+    uint32_t *err = const_cast<uint32_t *>(&res[j.job_index].invariant);
+    uint32_t *spec = const_cast<uint32_t *>(&res[j.job_index].spec);
+    switch (j.key_kind) {
+    case kKeyTimestamp:
+        produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        break;
+    case kKeyIdU128:
+        produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        break;
+    case kKeyCompositeU64:
+        produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        break;
+    default:
+        produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        break;
+    }
 }
 
 // Throughput regime, pass 1: assemble every data block body from the merge's
@@ -1976,6 +2024,28 @@ int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables,
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_produce_unique(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, const JobResultDev *d_results,
+                          const SplitDesc *d_bsplits, void *stream) {
+    if (!total_dblocks) return 0;
+    hipLaunchKernelGGL(k_produce_unique, dim3((total_dblocks + kProduceWaves - 1) / kProduceWaves),
+                       dim3(64 * kProduceWaves), 0, (hipStream_t)stream, d_jobs, njobs, total_dblocks, d_results,
+                       d_bsplits);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Bodies of the jobs the merge decided (phase 0: every job not speculated;
+// phase 1: the speculated jobs whose speculation broke), parallel over merge
+// tiles; each block's landed count goes to d_ready.
+int launch_assemble(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t *d_ready,
+                    const JobResultDev *d_results, const uint64_t *d_status, const uint64_t *d_masks,
+                    const SplitDesc *d_splits, uint32_t phase, void *stream) {
+    if (!total_tiles) return 0;
+    const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
+    hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, (hipStream_t)stream, d_jobs, njobs, total_tiles,
+                       d_status, d_masks, d_splits, d_ready, d_results, phase);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Pipelined batch, front (engine stream, in order with every later batch's
 // front): every body assembled, and the output index blocks' data addresses.
 int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks,
@@ -2013,12 +2083,25 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
             // concurrent tails share the chip by CUs: pack four chains per
             // CU (one per SIMD), more once a batch alone would take over a
             // third of the CUs.
+            // TBC_TAIL_CHAINS (A/B measurement): chain waves per workgroup.
+            static const uint32_t forced = getenv("TBC_TAIL_CHAINS") ? (uint32_t)atoi(getenv("TBC_TAIL_CHAINS")) : 0u;
             uint32_t c = (waves + 85) / 86;
             c = c < 4 ? 4 : (c > 16 ? 16 : (c + 3) & ~3u);
+            if (forced) c = forced < 1 ? 1 : (forced > 16 ? 16 : forced);
             if (c > waves) c = waves;
-            hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
-                               d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
-                               d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
+            // Two or more chains per SIMD share its VALU issue: the round key by
+            // one ds_bpermute (LDS pipe) instead of six VALU lane moves, as the
+            // throughput regime does. TBC_TAIL_STEP=valu|bperm (A/B only).
+            static const char *step_env = getenv("TBC_TAIL_STEP");
+            const bool bperm = step_env ? step_env[0] == 'b' : c >= 8;
+            if (bperm)
+                hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                                   d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                                   d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
+            else
+                hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                                   d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                                   d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         } else {
             const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
             const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);

@@ -1515,6 +1515,16 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // (round 3, one box: config 2 2.276/2.251 -> 2.235/2.222 ms, configs 3
     // and 4 within noise); TBC_NO_TAIL_FORK=1 keeps them on the engine stream.
     static const bool no_tail_fork = getenv("TBC_NO_TAIL_FORK") != nullptr; // A/B measurement only
+    // Pipelined speculated batch (round 4): the speculated bodies are merged
+    // on the engine stream (k_produce_unique) and the chains run on a tail
+    // stream, packed on a share of the CUs, so chains of batches in flight
+    // together share the chip (throughput), instead of one fused block pass
+    // on the engine stream holding every SIMD (latency: 2,016 chains at once
+    // take one chain's time, ~1.9 ms per 1 MiB block, whatever else waits).
+    // Chosen when an earlier batch's tail is still running (the caller
+    // pipelines), or always / never with TBC_CONFIG_PIPELINE / _LATENCY.
+    const bool spec_pipe = spec_regime && !(e->flags & TBC_CONFIG_LATENCY) &&
+                           ((e->flags & TBC_CONFIG_PIPELINE) || !e->tail_out.empty());
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
@@ -1719,6 +1729,47 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && count)
             ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
                                     e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+        if (ok) {
+            tbc_engine::TailOutputs to;
+            to.done = take_event(e);
+            ok = to.done && hipEventRecord(to.done, T) == hipSuccess;
+            for (uint32_t i = 0; ok && i < count; i++) {
+                const uint64_t lo = (uint64_t)(uintptr_t)jobs_in[i].output_blocks;
+                to.ranges.push_back({lo, lo + (uint64_t)jobs_in[i].address_count * e->block_size});
+            }
+            if (ok) e->tail_out.push_back(std::move(to));
+            else if (to.done) e->event_pool.push_back(to.done);
+        }
+    } else if (any_unique && spec_pipe) {
+        // Front (engine stream): block splits and results of the speculated
+        // jobs, the merge of the others and their bodies, the speculated
+        // bodies, then the recomputation of broken speculations (merge and
+        // bodies; each kernel leaves at once when none broke). Tail: the
+        // chains of every data block, the index blocks, the results.
+        const JobDesc *dj = (const JobDesc *)d_in;
+        ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
+        mark_cb(b, "partition_blocks");
+        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
+                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
+        ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 0, s) == 0;
+        mark_cb(b, "assemble");
+        ok = ok && launch_produce_unique(dj, (int)count, dblocks, d_res, d_bsplits, s) == 0;
+        mark_cb(b, "produce");
+        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
+                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+        ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 1, s) == 0;
+        mark_cb(b, "recompute_assemble");
+        const int ti = e->next_tail;
+        e->next_tail = (e->next_tail + 1) % e->ntails;
+        hipStream_t T = e->tail[ti];
+        b->fork = take_event(e);
+        ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
+        b->mark_stream = T;
+        mark_cb(b, "tail_wait");
+        ok = ok && launch_blocks_tail(dj, (int)count, dblocks, tables, d_res, d_infos, d_status, e->masks,
+                                      d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {

@@ -319,6 +319,14 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
                        void *stream, void (*mark)(void *, const char *), void *mark_ctx);
 int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
                         uint8_t *d_infos, void *stream);
+// Pipelined speculated batches: every speculated job's bodies, one producer
+// wave per data block (aegis.hip k_produce_unique), and the bodies of the
+// jobs the merge decided (k_assemble; phase 0 / 1 as phase_skips).
+int launch_produce_unique(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, const JobResultDev *d_results,
+                          const SplitDesc *d_bsplits, void *stream);
+int launch_assemble(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t *d_ready,
+                    const JobResultDev *d_results, const uint64_t *d_status, const uint64_t *d_masks,
+                    const SplitDesc *d_bsplits, uint32_t phase, void *stream);
 int launch_grid_checks(const InputCheck *d_checks, uint32_t count, const uint8_t *d_verified, const JobDesc *d_jobs,
                        int njobs, JobResultDev *d_results, uint32_t block_size, void *stream);
 int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_verified, const JobDesc *d_jobs,

@@ -286,8 +286,14 @@ class KwayMerge:
 
 class Engine:
     def __init__(self, device: int = 0, block_size: int = BLOCK_SIZE, arena_bytes: int = 0,
-                 profile: bool = False):
-        cfg = abi.Config(device, block_size, arena_bytes, abi.CONFIG_PROFILE if profile else 0, 0)
+                 profile: bool = False, pipeline: bool | None = None):
+        """pipeline: None = the engine decides per UNIQUE_KEYS batch (pipelined
+        when an earlier batch is still running), True / False = always / never
+        (TBC_CONFIG_PIPELINE / TBC_CONFIG_LATENCY)."""
+        flags = abi.CONFIG_PROFILE if profile else 0
+        if pipeline is not None:
+            flags |= abi.CONFIG_PIPELINE if pipeline else abi.CONFIG_LATENCY
+        cfg = abi.Config(device, block_size, arena_bytes, flags, 0)
         h = ctypes.c_void_p()
         check(lib().tbc_engine_init(ctypes.byref(cfg), ctypes.byref(h)), "tbc_engine_init")
         self.handle = h.value
