@@ -1532,6 +1532,24 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                    d.dblock_max > 0;
         any_unique |= d.unique != 0;
     }
+    // Pipelined: the speculated jobs' tiles of kUniqueTile positions and
+    // their merge-path splits (merge.hip k_merge_unique). TBC_PIPE_PRODUCERS=1
+    // (A/B measurement only) merges them by one producer wave per block instead.
+    static const bool pipe_producers = getenv("TBC_PIPE_PRODUCERS") != nullptr;
+    const bool unique_tiles = spec_pipe && any_unique && !pipe_producers;
+    uint32_t utiles = 0, usplits = 0;
+    for (uint32_t k = 0; k < count; k++) {
+        JobDesc &d = sj[k];
+        d.utile_base = utiles;
+        d.usplit_base = usplits;
+        d.utile_count = 0;
+        if (unique_tiles && d.unique) {
+            const uint64_t n = (uint64_t)d.a.n + d.b.n;
+            d.utile_count = (uint32_t)((n + kUniqueTile - 1) / kUniqueTile);
+            utiles += d.utile_count;
+            usplits += d.utile_count + 1;
+        }
+    }
 
     // Device layout of the batch.
     const uint64_t sz_jobs = align_up(sizeof(JobDesc) * (uint64_t)count, 256);
@@ -1542,8 +1560,10 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     const uint64_t sz_checks = align_up(sizeof(InputCheck) * n_checks, 256);
     const uint64_t sz_resolve = align_up(sizeof(ResolveItem) * (uint64_t)resolve.size(), 256);
     const uint64_t sz_in = sz_jobs + sz_segs + sz_addr + sz_order + sz_checks + sz_resolve;
-    // tile splits, then (speculated jobs) one split per data block
-    const uint64_t sz_splits = align_up(sizeof(SplitDesc) * ((uint64_t)splits + (any_unique ? dblocks : 0)), 256);
+    // tile splits, then (speculated jobs) one split per data block, then the
+    // unique-tile splits (pipelined speculated batches)
+    const uint64_t sz_splits =
+        align_up(sizeof(SplitDesc) * ((uint64_t)splits + (any_unique ? dblocks : 0) + usplits), 256);
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     // tile status, block tiles, per-block landed counts, the assembling
     // merge's look-back words (one per tile) and its ticket counters
@@ -1560,6 +1580,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     uint8_t *d_in = dbase;
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
     SplitDesc *d_bsplits = any_unique ? d_splits + splits : nullptr;
+    SplitDesc *d_usplits = usplits ? d_splits + splits + dblocks : nullptr;
     uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
     uint32_t *d_block_tile = (uint32_t *)(d_status + tiles);
     uint32_t *d_ready = d_block_tile + dblocks;
@@ -1749,14 +1770,20 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // bodies; each kernel leaves at once when none broke). Tail: the
         // chains of every data block, the index blocks, the results.
         const JobDesc *dj = (const JobDesc *)d_in;
-        ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
-        mark_cb(b, "partition_blocks");
+        if (unique_tiles) {
+            ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, s, mark_cb, b) == 0;
+        } else {
+            ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
+            mark_cb(b, "partition_blocks");
+        }
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 0, s) == 0;
         mark_cb(b, "assemble");
-        ok = ok && launch_produce_unique(dj, (int)count, dblocks, d_res, d_bsplits, s) == 0;
-        mark_cb(b, "produce");
+        if (!unique_tiles) {
+            ok = ok && launch_produce_unique(dj, (int)count, dblocks, d_res, d_bsplits, s) == 0;
+            mark_cb(b, "produce");
+        }
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 1, s) == 0;

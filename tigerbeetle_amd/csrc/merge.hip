@@ -189,6 +189,200 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 }
 
 // --------------------------------------------------------------------------
+// Pipelined speculated batches (engine.hip submit_impl, round 4): a
+// TBC_COMPACTION_UNIQUE_KEYS job's bodies merged tile by tile on the engine
+// stream, HBM-bound, while earlier batches' AEGIS chains run on tail streams.
+// If no key repeats and no tombstone is dropped, every value survives
+// (compaction.zig:483-559 dedup and :757-798 merge keep it), so merged
+// position g lands at data block g / vcm, slot g % vcm: A[i] at
+// (i - ia0) + |{B in the tile < A[i]}|, B[j] at (j - jb0) + |{A in the tile
+// <= B[j]}| (A first on equal keys). The speculation holds iff no output key
+// equals its merged predecessor's: an A key equal to its lower bound in B
+// (the tile's B range, or the first B after it), an A key equal to the A
+// before it, a B key equal to the B before it; and no A tombstone when
+// tombstones are dropped. A broken job is marked (JobResultDev.spec) and
+// recomputed through the merge path by the batch's phase 1.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, int njobs, uint32_t nsplits,
+                                                          SplitDesc *usplits, JobResultDev *res) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= nsplits) return;
+    const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.usplit_base; });
+    const JobDesc &j = jobs[ji];
+    if (!j.unique || g - j.usplit_base > j.utile_count) return;
+    const uint32_t t = g - j.usplit_base;
+    const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
+    const uint32_t d = (uint64_t)t * kUniqueTile < n ? t * kUniqueTile : n;
+    uint32_t lo;
+    switch (j.key_kind) {
+    case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
+    case kKeyIdU128: lo = merge_path_split<kKeyIdU128>(j, d); break;
+    case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
+    default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
+    }
+    SplitDesc s;
+    s.i = lo;
+    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
+    const uint32_t jb = d - lo;
+    s.seg_b = nb ? seg_search(j.b, jb > 0 ? jb - 1 : 0) : 0;
+    s.pad = 0;
+    usplits[g] = s;
+    if (t == 0) { // speculative results (write_blocks' shape for n values, compaction.zig:806-850)
+        JobResultDev &r = res[j.job_index];
+        r.value_count = n;
+        r.data_block_count = j.dblock_max;
+        r.table_count = j.table_max;
+        r.block_count = j.dblock_max + j.table_max;
+        r.spec = kSpecHeld;
+    }
+}
+
+struct UniqueShared {
+    // Entries: [0, na + 1) = A[ia0 - 1 .. ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1];
+    // limb l of entry e at key[l * (kUniqueTile + 3) + e].
+    uint64_t key[3 * (kUniqueTile + 3)];
+    uint8_t tomb[kUniqueTile + 1];
+    uint32_t bad;
+};
+
+template <int KIND>
+__device__ __forceinline__ void merge_unique_tile(UniqueShared &sh, const JobDesc &j, uint32_t t,
+                                                  const SplitDesc *usplits, JobResultDev *res) {
+    constexpr int KL = KeyLimbs<KIND>::value;
+    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, R = T + 3;
+    uint64_t *s_key = sh.key;
+    uint8_t *s_tomb = sh.tomb;
+    uint32_t &s_bad = sh.bad;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
+    const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
+    const SplitDesc s0 = usplits[j.usplit_base + t];
+    const uint32_t ia0 = s0.i, ia1 = usplits[j.usplit_base + t + 1].i;
+    const uint32_t jb0 = d0 - ia0, jb1 = d1 - ia1;
+    const uint32_t na = ia1 - ia0, nb = jb1 - jb0;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
+    const bool drop = j.drop_tombstones != 0;
+    const uint32_t eb = na + 1; // first B entry (B[jb0 - 1])
+    if (tid == 0) s_bad = 0;
+    // Keys (and A tombstones) into LDS; pointers through cursors that start at
+    // the split's segments and only move forward.
+    SegCursor ca, cb;
+    ca.init(j.a, s0.seg_a);
+    cb.init(j.b, s0.seg_b);
+    for (uint32_t e = tid; e < na + nb + 3; e += NT) {
+        const bool is_a = e < eb;
+        const int64_t idx = is_a ? (int64_t)ia0 - 1 + e : (int64_t)jb0 - 1 + (e - eb);
+        const Stream &st = is_a ? j.a : j.b;
+        Key<KL> k;
+#pragma unroll
+        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
+        uint8_t tb = 0;
+        if (idx >= 0 && idx < (int64_t)st.n) {
+            const uint32_t i = (uint32_t)idx;
+            const uint8_t *p = elem_ptr(st, seg_search(st, i), i, vs);
+            k = load_key<KIND>(p, ts);
+            if (is_a) tb = (uint8_t)load_tomb(p, ts);
+        }
+#pragma unroll
+        for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
+        if (is_a) s_tomb[e] = tb;
+    }
+    __syncthreads();
+    auto entry = [&](uint32_t e) {
+        Key<KL> k;
+#pragma unroll
+        for (int l = 0; l < KL; l++) k.l[l] = s_key[l * R + e];
+        return k;
+    };
+    bool bad = false;
+    const uint32_t vcm = j.vcm, chunks = vs >> 4;
+    for (uint32_t e = tid; e < na + nb; e += NT) {
+        const bool is_a = e < na;
+        uint32_t pos;
+        const uint8_t *src;
+        if (is_a) {
+            const Key<KL> ka = entry(1 + e);
+            // |{B in the tile < ka}|: lower bound over entries [eb + 1, eb + 1 + nb).
+            uint32_t lo = 0, hi = nb;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (key_lt(entry(eb + 1 + mid), ka)) lo = mid + 1;
+                else hi = mid;
+            }
+            pos = e + lo;
+            // The B at the lower bound (inside the tile, or the first after it).
+            const bool b_there = lo < nb || jb1 < nb_all;
+            bad |= b_there && key_eq(entry(eb + 1 + lo), ka);
+            bad |= (ia0 + e > 0) && key_eq(entry(e), ka);
+            bad |= drop && s_tomb[1 + e];
+            const uint32_t i = ia0 + e;
+            ca.advance(i);
+            src = ca.elem(i, vs);
+        } else {
+            const uint32_t b = e - na;
+            const Key<KL> kb = entry(eb + 1 + b);
+            // |{A in the tile <= kb}|: upper bound over entries [1, 1 + na).
+            uint32_t lo = 0, hi = na;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (key_le(entry(1 + mid), kb)) lo = mid + 1;
+                else hi = mid;
+            }
+            pos = b + lo;
+            bad |= (jb0 + b > 0) && key_eq(entry(eb + b), kb);
+            const uint32_t i = jb0 + b;
+            cb.advance(i);
+            src = cb.elem(i, vs);
+        }
+        const uint32_t g = d0 + pos;
+        const uint32_t k = g / vcm;
+        uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(g - k * vcm) * vs;
+        for (uint32_t c = 0; c < chunks; c++) gst<u32x4>(dst + 16 * c, gld<u32x4>(src + 16 * c));
+    }
+    if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    if (tid == 0 && s_bad) {
+        __hip_atomic_store(&res[j.job_index].spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
+                                                                 const SplitDesc *usplits, JobResultDev *res) {
+    __shared__ UniqueShared sh;
+    const uint32_t g = blockIdx.x;
+    const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
+    const JobDesc &j = jobs[ji];
+    if (!j.unique || g - j.utile_base >= j.utile_count) return; // uniform
+    const uint32_t t = g - j.utile_base;
+    switch (j.key_kind) {
+    case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(sh, j, t, usplits, res); break;
+    case kKeyIdU128: merge_unique_tile<kKeyIdU128>(sh, j, t, usplits, res); break;
+    case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(sh, j, t, usplits, res); break;
+    default: merge_unique_tile<kKeyCompositeU128>(sh, j, t, usplits, res); break;
+    }
+}
+
+int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
+                        JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
+    hipStream_t s = (hipStream_t)stream;
+    if (!njobs) return 0;
+    const JobDesc &l = h_jobs[njobs - 1];
+    const uint32_t nsplits = l.usplit_base + (l.unique ? l.utile_count + 1 : 0);
+    const uint32_t ntiles = l.utile_base + l.utile_count;
+    if (!nsplits || !ntiles) return 0;
+    hipLaunchKernelGGL(k_partition_unique, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
+                       d_usplits, d_results);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (mark) mark(mark_ctx, "partition_unique");
+    hipLaunchKernelGGL(k_merge_unique, dim3(ntiles), dim3(kUniqueThreads), 0, s, d_jobs, njobs, ntiles,
+                       (const SplitDesc *)d_usplits, d_results);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (mark) mark(mark_ctx, "merge_unique");
+    return 0;
+}
+
+// --------------------------------------------------------------------------
 // One pass per tile (merged positions [d0, d1)): load keys, decide each
 // position's side (A or B) and whether it survives, and publish them as two
 // bit masks per 64 positions plus the tile's survivor count. Tiles are

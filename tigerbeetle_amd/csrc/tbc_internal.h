@@ -79,7 +79,17 @@ struct JobDesc {
     // Speculating batches: the number of broken speculations (one word of the
     // batch's zeroed scratch); phase-1 kernels leave at once while it is 0.
     uint32_t *spec_any;
+    // Pipelined speculated batches (merge.hip k_merge_unique): the job's
+    // tiles of kUniqueTile merged positions, batch-wide numbering, and their
+    // utile_count + 1 merge-path splits (0 tiles for a job not speculated).
+    uint32_t utile_base, utile_count, usplit_base, pad1;
 };
+
+// Merged positions per tile of k_merge_unique: the tile's keys (plus three
+// neighbours) fit in 12.1 KiB of LDS for 24-byte keys, so its workgroups fit
+// beside chain workgroups that hold 140 KiB of a CU's 160.
+constexpr uint32_t kUniqueTile = 512;
+constexpr uint32_t kUniqueThreads = 256;
 
 struct SplitDesc {
     uint32_t i;     // A elements before the tile boundary (merge path)
@@ -292,6 +302,13 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
 // survives).
 int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, SplitDesc *d_bsplits,
                             JobResultDev *d_results, void *stream);
+// Pipelined speculated batches: merge-path splits every kUniqueTile merged
+// positions of every speculated job plus its speculative results, then ONE
+// merge of each tile writing every value straight to its output slot (every
+// value survives) with the speculation checks (a broken job is marked for
+// the recomputation phase).
+int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
+                        JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
