@@ -161,9 +161,11 @@ class SplitPart:
     """This rank's key range of ONE job split across all ranks (split.py,
     SURVEY §8(e)2): splitters from the job's data-block first keys (identical
     on every rank, no communication), only this rank's range of A and B
-    staged, and per step compact_split — phase 1 values-only, all-gathers of
-    the survivor counts and table heads (RCCL over xGMI with the nccl
-    backend), phase 2 re-blocking the tables this rank owns."""
+    staged, and per step compact_split — a count-only merge, an all-gather of
+    the survivor counts (RCCL over xGMI with the nccl backend), the range's
+    bodies written in place at their global positions, the partial block's
+    values to its owner, the owned data blocks finished in place, one table's
+    index entries to its owner, the owned index blocks sealed."""
 
     def __init__(self, eng: Engine, js, gid: int, rank: int, world: int, exchange, bs: int):
         from tigerbeetle_amd import split, workloads

@@ -133,6 +133,11 @@ typedef struct tbc_segment {
  * the latency regime of a plain batch (no GRID / VALUES_ONLY, few enough
  * output blocks that every chain runs at once); ignored elsewhere. */
 #define TBC_COMPACTION_UNIQUE_KEYS 4u
+/* COUNT_ONLY: the merge alone (survivor rules included); the result's
+ * value_count is the number of survivors and nothing is written
+ * (output_blocks may be NULL). Phase A of a job split by key range
+ * (tbc_compaction.output_offset, tbc_compaction_seal). */
+#define TBC_COMPACTION_COUNT_ONLY 8u
 
 /* ---- GPU-resident grid (src/vsr/grid.zig, src/lsm/set_associative_cache.zig) ----
  * The blocks of the data file's grid zone for addresses [1, block_count],
@@ -180,7 +185,43 @@ typedef struct tbc_compaction {
     const tbc_table_ref *tables_b; /* host array: range_b.tables in ascending key order */
     uint32_t table_count_a;
     uint32_t table_count_b;
+    /* VALUES_ONLY only (0 otherwise): this compaction is one key range of a
+     * job split across GPUs, preceded in the job's merged output by
+     * output_offset survivors of the other ranges. Survivor i is written at
+     * the job's output position output_offset + i: data block
+     * k = position / block_value_count_max, slot k + k / data_block_count_max
+     * of output_blocks (the whole job's acquire order), so every rank builds
+     * its part of the job's blocks in place (tbc_compaction_seal). */
+    uint64_t output_offset;
 } tbc_compaction;
+
+/* ---- sealing a job split by key range -----------------------
+ * The blocks of ONE job whose survivors were written in place across ranks
+ * (VALUES_ONLY + output_offset; a straddling data block's values gathered by
+ * its owner): data blocks [block_first, block_first + block_count) get their
+ * headers and checksums (data_block_finish, table.zig:306-384) and their
+ * index entries (checksum, key_min, key_max, address) written into their
+ * table's index block slot; then the index blocks of tables
+ * [table_first, table_first + table_count) are sealed from the entries found
+ * in their slots (index_block_finish, table.zig:403-457: every entry of such
+ * a table must be in place, written by this engine or copied in from the
+ * rank that finished that block) with one TableInfo each (level_b).
+ * value_count is the whole job's survivor count: it fixes every block and
+ * table boundary. One batch on the engine stream; tbc_batch_result(0)
+ * reports the data blocks and tables of this call and its TableInfos. */
+typedef struct tbc_seal {
+    tbc_tree tree;
+    uint64_t cluster[2];
+    uint64_t snapshot_min;
+    uint8_t level_b;
+    uint8_t reserved[3];
+    uint32_t address_count;    /* the job's acquire order (all of it) */
+    const uint64_t *addresses; /* host array */
+    void *output_blocks;       /* device: the job's output blocks, address_count * block_size bytes */
+    uint64_t value_count;      /* survivors of the whole job */
+    uint32_t block_first, block_count;
+    uint32_t table_first, table_count;
+} tbc_seal;
 
 /* Per-compaction result (after tbc_batch_poll returned TBC_OK). */
 typedef struct tbc_compaction_result {
@@ -377,6 +418,8 @@ tbc_status tbc_compaction_submit(tbc_engine *engine, const tbc_compaction *compa
                                  tbc_batch **out_batch);
 /* Non-blocking: TBC_PENDING while running, then TBC_OK or the first error. */
 tbc_status tbc_batch_poll(tbc_batch *batch);
+/* Enqueue the sealing of one split job's blocks (see tbc_seal above). */
+tbc_status tbc_compaction_seal(tbc_engine *engine, const tbc_seal *seal, tbc_batch **out_batch);
 /* Blocking wait (tests / benchmarks only; the adapter polls). */
 tbc_status tbc_batch_wait(tbc_batch *batch);
 /* Results of compaction `index`; table_infos receives table_count entries of

@@ -30,6 +30,7 @@ def test_abi_version_and_struct_layout_match_c():
         "tbc_compaction_result": (abi.CompactionResult, [f for f, _ in abi.CompactionResult._fields_]),
         "tbc_tree_layout": (abi.TreeLayout, [f for f, _ in abi.TreeLayout._fields_]),
         "tbc_table_ref": (abi.TableRef, ["address", "checksum", "value_count"]),
+        "tbc_seal": (abi.Seal, [f for f, _ in abi.Seal._fields_ if not f.startswith("reserved")]),
     }
     lines = ['#include "tbc.h"', "#include <stdio.h>", "#include <stddef.h>", "int main(void) {"]
     expect = []

@@ -1,7 +1,9 @@
 """Key-range split of one compaction on the GPU (tigerbeetle_amd/split.py,
-SURVEY.md §8e.2): every rank runs compact_split through libtbc.so; the tables
-each rank writes must equal, byte for byte, the same tables of the oracle's
-unsplit job. Ranks share the box's one GPU (one process and engine each) and
+SURVEY.md §8e.2): every rank runs compact_split through libtbc.so (COUNT_ONLY
+merge, VALUES_ONLY at its global output offset, tbc_compaction_seal); the
+data blocks, index blocks and TableInfos each rank finishes must equal, byte
+for byte, the same blocks of the oracle's unsplit job, and each rank sends at
+most one partial block's values and one table's index entries. Ranks share the box's one GPU (one process and engine each) and
 exchange counts and heads over gloo; on an 8-GPU node the same code runs with
 the nccl backend (RCCL over xGMI) and device buffers."""
 import os
@@ -70,22 +72,25 @@ def _run_rank(name, rank, world, exchange):
         res = split.compact_split(eng, job, cuts, exchange, rank, staged=True)
         whole = run_oracle(oracle, ji, bs, addrs)
         assert whole.status == 0
+        plan = res.plan
+        if plan.total != whole.value_count:
+            return False, f"rank {rank}: total {plan.total} != {whole.value_count}"
+        if res.exchanged["heads"] > (vcm - 1) * spec.value_size or \
+                res.exchanged["entries"] > (dbcm - 1) * split.entry_bytes(spec.key_size):
+            return False, f"rank {rank}: exchanged {res.exchanged}"
+        got = res.arena.download().reshape(-1, bs)
+        slots = [split.data_block_slot(k, dbcm) for k in range(*res.blocks)]
+        slots += [split.index_block_slot(t, plan.k_last(t)) for t in range(*res.tables)]
+        for slot in slots:
+            if not np.array_equal(disk_image(got[slot]), disk_image(whole.blocks[slot])):
+                return False, f"rank {rank}: block slot {slot} differs"
         t0, t1 = res.tables
-        if t0 == t1:
-            return True, f"rank {rank}: no tables"
-        lo, hi = split.table_address_range(t0, t1, res.plan.total, vcm, dbcm)
-        if res.plan.total != whole.value_count:
-            return False, f"rank {rank}: total {res.plan.total} != {whole.value_count}"
-        got = res.blocks.download((hi - lo) * bs).reshape(-1, bs)
-        for k in range(hi - lo):
-            if not np.array_equal(disk_image(got[k]), disk_image(whole.blocks[lo + k])):
-                return False, f"rank {rank}: block {lo + k} differs"
         if not np.array_equal(res.table_infos, whole.table_infos[t0:t1]):
             return False, f"rank {rank}: TableInfo differs"
-        return True, f"rank {rank}: tables {t0}..{t1} OK"
+        return True, f"rank {rank}: blocks {res.blocks} tables {res.tables} OK ({len(slots)} slots)"
 
 
-def test_split_single_rank_reblocks_bit_exact():
+def test_split_single_rank_bit_exact():
     from tigerbeetle_amd import split
     ok, msg = _run_rank("debit_4k", 0, 1, split.SingleRank())
     assert ok, msg
@@ -173,3 +178,52 @@ def test_values_only_bodies_equal_full_compaction(bs, name):
                    np.asarray(addrs, dtype=np.uint64), out)
         with pytest.raises(Exception):
             eng.submit([job, job2])
+
+
+@pytest.mark.parametrize("bs,name", [(4096, "debit_4k"), (1 << 20, "id_1mib")])
+def test_count_only_and_values_at_offset(bs, name):
+    """TBC_COMPACTION_COUNT_ONLY gives the full compaction's survivor count and
+    writes nothing; VALUES_ONLY with output_offset places survivor i at the
+    job's output position offset + i (block and slot of the job's layout)."""
+    from helpers import gpu_run
+    from tigerbeetle_amd import Engine, abi, split
+    from tigerbeetle_amd.engine import Job, stage_blocks
+    from tigerbeetle_amd import workloads
+    spec, bs, ji, addrs = _inputs(name)
+    with Engine(device=0, block_size=bs) as eng:
+        (full, _, blocks), = gpu_run(eng, [ji], bs, [addrs])[0]
+        lay = eng.layout(spec)
+        vcm, dbcm, vs = lay.block_value_count_max, lay.data_block_count_max, spec.value_size
+        abuf = eng.upload(ji.a_values)
+        bbuf, segs_b = stage_blocks(eng, [workloads.split_blocks(t, vcm) for t in ji.b_tables], vs, bs)
+        a_seg = [(abuf.ptr, len(ji.a_values))]
+        cnt = Job(spec, a_seg, segs_b, True, ji.drop_tombstones, 1, 0x1234, 48, np.zeros(0, np.uint64), None,
+                  flags=abi.COMPACTION_COUNT_ONLY)
+        b = eng.submit([cnt])
+        b.wait()
+        r, _ = b.result(0)
+        b.release()
+        assert r.status == 0 and r.value_count == full.value_count
+        off = vcm // 3 + 7  # not a block boundary
+        n_slots = split.data_block_slot((off + full.value_count - 1) // vcm, dbcm) + 1
+        out = eng.alloc(n_slots * bs)
+        out.zero()
+        job = Job(spec, a_seg, segs_b, True, ji.drop_tombstones, 1, 0x1234, 48,
+                  np.arange(1, n_slots + 1, dtype=np.uint64), out, flags=abi.COMPACTION_VALUES_ONLY,
+                  output_offset=off)
+        b = eng.submit([job])
+        b.wait()
+        r, _ = b.result(0)
+        b.release()
+        assert r.status == 0 and r.value_count == full.value_count
+        got = out.download().reshape(-1, bs)
+        placed = []
+        for g in range(off, off + full.value_count, 1):
+            k = g // vcm
+            if g == off or g % vcm == 0:
+                end = min((k + 1) * vcm, off + full.value_count)
+                row = got[split.data_block_slot(k, dbcm)]
+                placed.append(row[256 + (g - k * vcm) * vs: 256 + (end - k * vcm) * vs].reshape(-1, vs))
+        want = np.concatenate([blocks[split.data_block_slot(k, dbcm), 256:256 + min(vcm, full.value_count - k * vcm)
+                                      * vs].reshape(-1, vs) for k in range(full.data_block_count)])
+        assert np.array_equal(np.concatenate(placed), want)

@@ -1,10 +1,18 @@
 """Key-range split of one compaction across ranks (tigerbeetle_amd/split.py,
-SURVEY.md §8e.2) on CPU: the splitters, the count exchange, table ownership
-and the head exchange, with the oracle standing in for each rank's GPU
-compaction. The re-blocked tables must equal the unsplit job's output byte for
-byte (blocks, index blocks, checksums, TableInfos)."""
+SURVEY.md §8e.2) on CPU: the splitters, then split.compact_split itself —
+count exchange, bodies in place at global positions, the partial block's
+values to its owner, data blocks finished in place, index entries to the
+table's owner, index blocks sealed — run against an oracle-backed stand-in
+for each rank's engine (the oracle merges each rank's key range; data and
+index blocks are finished by a Python restatement of data_block_finish /
+index_block_finish checked by the comparison itself). The union of the
+ranks' data blocks, index blocks and TableInfos must equal the unsplit job's
+output byte for byte, and each exchange must stay within one block's values
+and one table's index entries per rank."""
 import os
 import socket
+import threading
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
@@ -13,6 +21,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from helpers import data_values_from_blocks, disk_image, oracle_tree
+from oracle import oracle as _oracle
 from tigerbeetle_amd import split, trees, workloads
 
 BS = 4096
@@ -59,29 +68,6 @@ def _compact(oracle, spec, a, a_immutable, b, drop, addrs):
                        level_b=LEVEL_B, cluster=CLUSTER, snapshot_min=SNAPSHOT_MIN, addresses=addrs)
     assert r.status == 0
     return r
-
-
-def _rank_phase1(oracle, spec, ji, cuts, rank):
-    (a_lo, b_lo), (a_hi, b_hi) = cuts[rank], cuts[rank + 1]
-    a, b = ji.a_values[a_lo:a_hi], _b_all(ji)[b_lo:b_hi]
-    n = len(a) + len(b)
-    scratch = np.arange(1, workloads.worst_case_blocks(spec, max(n, 1), BS) + 1, dtype=np.uint64)
-    r = _compact(oracle, spec, a, ji.a_immutable, b, ji.drop_tombstones, scratch)
-    return data_values_from_blocks(r.blocks[: len(r.blocks)], spec.value_size)
-
-
-def _rank_phase2(oracle, spec, plan, rank, survivors_of, addrs):
-    """Re-block rank's owned tables from its survivors and the exchanged heads."""
-    lay = spec.layout(BS)
-    t0, t1 = plan.tables[rank]
-    if t0 == t1:
-        return [], np.zeros((0, 128), np.uint8)
-    stream = np.concatenate([survivors_of(q)[st:st + c] for q, st, c in plan.stream(rank)])
-    lo, hi = split.table_address_range(t0, t1, plan.total, lay["block_value_count_max"],
-                                       lay["data_block_count_max"])
-    r = _compact(oracle, spec, stream, False, stream[:0], False, addrs[lo:hi])
-    assert len(r.table_infos) == t1 - t0
-    return [disk_image(b) for b in r.blocks], r.table_infos
 
 
 def _cuts(spec, ji, world):
@@ -132,21 +118,6 @@ def test_split_points_never_split_a_key(case):
             assert max(sizes) - min(sizes) <= 2 + (na + nb) // world // 4
 
 
-def test_plan_tables_edges():
-    vcm, dbcm = 10, 3
-    T = vcm * dbcm
-    plan = split.plan_tables([0, 45, 0, 5, 31, 0], vcm, dbcm)
-    assert plan.total == 81 and plan.offsets == [0, 0, 45, 45, 50, 81]
-    assert plan.tables == [(0, 0), (0, 2), (2, 2), (2, 2), (2, 3), (3, 3)]
-    assert plan.need == [0, 0, 0, 5, 10, 0]
-    assert plan.stream(1) == [(1, 0, 45), (3, 0, 5), (4, 0, 10)]
-    assert plan.stream(4) == [(4, 10, 21)]
-    assert all(plan.stream(r) == [] for r in (0, 2, 3, 5))
-    assert split.table_address_range(0, 2, 81, vcm, dbcm) == (0, 8)
-    assert split.table_address_range(2, 3, 81, vcm, dbcm) == (8, 12)
-    assert split.table_address_range(2, 3, 2 * T + 1, vcm, dbcm) == (8, 10)
-
-
 @pytest.mark.parametrize("case", range(len(CASES)))
 @pytest.mark.parametrize("world", [2, 3, 5, 8])
 def test_block_cuts_read_only_boundary_blocks(case, world):
@@ -175,30 +146,269 @@ def test_block_cuts_read_only_boundary_blocks(case, world):
         assert split.staged_bytes(cuts, p, vs) <= (n // world + 2 * vcm * (world > 1) + 2 * vcm) * vs
 
 
+
+def test_plan_split_edges():
+    vcm, dbcm = 10, 3
+    plan = split.plan_split([0, 45, 0, 5, 31, 0], vcm, dbcm)
+    assert plan.total == 81 and plan.offsets == [0, 0, 45, 45, 50, 81]
+    assert plan.data_blocks == 9 and plan.table_count == 3
+    assert [plan.blocks(p) for p in range(6)] == [(0, 0), (0, 5), (5, 5), (5, 5), (5, 9), (9, 9)]
+    assert [plan.tables(p) for p in range(6)] == [(0, 0), (0, 2), (2, 2), (2, 2), (2, 3), (3, 3)]
+    # rank 1's last block (40..49) takes 5 values from rank 3 and 0 from rank 4 (it starts block 5)
+    assert [plan.head(p) for p in range(6)] == [(0, 0), (0, 0), (45, 0), (45, 5), (50, 0), (81, 0)]
+    assert plan.block_owner(4) == 1 and plan.block_owner(5) == 4 and plan.table_owner(1) == 1
+    # rank 4 finishes blocks 5..8: block 5 belongs to table 1 (rank 1's)
+    assert plan.entries(4) == (1, 2, 1) and plan.entries(1) == (0, 0, 0)
+    assert plan.k_last(2) == 8 and plan.head_max == 5 and plan.entries_max == 1
+    solo = split.plan_split([7], 10, 3)
+    assert solo.blocks(0) == (0, 1) and solo.tables(0) == (0, 1) and solo.head(0) == (0, 0)
+
+
+# --- an oracle-backed stand-in for one rank's engine ---------------------------
+
+def _header(size, address, block_type, tree_id, m0, m1, m2, cluster=CLUSTER, snapshot=SNAPSHOT_MIN):
+    """Header.Block (message_header.zig:1153-1178) with the 14 metadata bytes."""
+    h = np.zeros(256, np.uint8)
+    h[80:96] = np.frombuffer(cluster.to_bytes(16, "little"), np.uint8)
+    h[96:100] = np.frombuffer(int(size).to_bytes(4, "little"), np.uint8)
+    h[110] = 20
+    for off, v in ((128, m0), (132, m1), (136, m2)):
+        h[off:off + 4] = np.frombuffer(int(v).to_bytes(4, "little"), np.uint8)
+    h[140:142] = np.frombuffer(int(tree_id).to_bytes(2, "little"), np.uint8)
+    h[224:232] = np.frombuffer(int(address).to_bytes(8, "little"), np.uint8)
+    h[232:240] = np.frombuffer(int(snapshot).to_bytes(8, "little"), np.uint8)
+    h[240] = block_type
+    return h
+
+
+def _set_checksums(block, size):
+    block[32:48] = np.frombuffer(_oracle.checksum(block[256:size].tobytes()).to_bytes(16, "little"), np.uint8)
+    block[0:16] = np.frombuffer(_oracle.checksum(block[16:256].tobytes()).to_bytes(16, "little"), np.uint8)
+
+
+class _Buf:
+    def __init__(self, eng, ptr, n):
+        self.eng, self.ptr, self.nbytes = eng, ptr, n
+
+    def download(self, n=None):
+        return self.eng.mem[self.ptr:self.ptr + (self.nbytes if n is None else n)].copy()
+
+    def free(self):
+        pass
+
+
+class _OracleEngine:
+    """What compact_split asks of an engine, on host memory: COUNT_ONLY and
+    VALUES_ONLY-at-offset merges by the oracle, copies, and tbc_compaction_seal
+    restated (data_block_finish / index_block_finish from the entries)."""
+
+    def __init__(self, spec, heap=24 << 20):
+        self.mem = np.zeros(heap, np.uint8)
+        self.top, self.block_size, self.spec = 4096, BS, spec
+        lay = spec.layout(BS)
+        self.vcm, self.dbcm = lay["block_value_count_max"], lay["data_block_count_max"]
+
+    def layout(self, tree):
+        return SimpleNamespace(block_value_count_max=self.vcm, data_block_count_max=self.dbcm)
+
+    def alloc(self, n):
+        p = self.top
+        self.top += (n + 255) // 256 * 256
+        assert self.top <= len(self.mem)
+        return _Buf(self, p, n)
+
+    def upload(self, a):
+        b = self.alloc(a.nbytes)
+        self.mem[b.ptr:b.ptr + a.nbytes] = np.frombuffer(a.tobytes(), np.uint8)
+        return b
+
+    def values(self, segs):
+        vs = self.spec.value_size
+        parts = [self.mem[p:p + n * vs].reshape(-1, vs) for p, n in segs]
+        return np.concatenate(parts) if parts else np.zeros((0, vs), np.uint8)
+
+    def copy_device_async(self, dst, src, n):
+        self.mem[dst:dst + n] = self.mem[src:src + n].copy()
+
+    def copy_device_batch(self, copies):
+        for dst, src, n in copies:
+            self.copy_device_async(dst, src, n)
+
+    def synchronize(self):
+        pass
+
+    def submit(self, jobs):
+        from tigerbeetle_amd import abi
+        (j,) = jobs
+        a, b = self.values(j.segments_a), self.values(j.segments_b)
+        r = _compact(_oracle, self.spec, a, j.a_immutable, b, j.drop_tombstones,
+                     np.arange(1, workloads.worst_case_blocks(self.spec, max(1, len(a) + len(b)), BS) + 2,
+                               dtype=np.uint64))
+        surv = data_values_from_blocks(r.blocks, self.spec.value_size)
+        if j.flags & abi.COMPACTION_VALUES_ONLY:
+            vs = self.spec.value_size
+            for i, v in enumerate(surv):
+                g = j.output_offset + i
+                k = g // self.vcm
+                at = j.output.ptr + split.data_block_slot(k, self.dbcm) * BS + 256 + (g - k * self.vcm) * vs
+                self.mem[at:at + vs] = v
+        res = SimpleNamespace(value_count=len(surv), status=0, table_count=0)
+        return SimpleNamespace(wait=lambda: None, release=lambda: None,
+                               result=lambda i: (res, np.zeros((0, 128), np.uint8)))
+
+    def seal(self, tree, cluster, snapshot_min, level_b, addresses, arena, value_count, blocks, tables):
+        spec, vs, ks, vcm, dbcm = self.spec, self.spec.value_size, self.spec.key_size, self.vcm, self.dbcm
+        plan = split.plan_split([value_count], vcm, dbcm)
+        db = plan.data_blocks
+
+        def slot_ptr(slot):
+            return arena.ptr + slot * BS
+
+        def key_bytes(v):
+            limbs = workloads.keys_of(v[None, :], spec)
+            return b"".join(int(l[0]).to_bytes(8, "little") for l in limbs).ljust(ks, b"\0")
+
+        for k in range(*blocks):
+            cnt = min(vcm, value_count - k * vcm)
+            at = slot_ptr(split.data_block_slot(k, dbcm))
+            blk = self.mem[at:at + BS]
+            size = 256 + cnt * vs
+            addr = int(addresses[split.data_block_slot(k, dbcm)])
+            blk[:256] = _header(size, addr, 5, spec.tree_id, vcm, cnt, vs, cluster, snapshot_min)
+            _set_checksums(blk, size)
+            blk[size:-(-size // 4096) * 4096] = 0
+            t, s = k // dbcm, k % dbcm
+            img = slot_ptr(split.index_block_slot(t, plan.k_last(t)))
+            body = blk[256:size].reshape(-1, vs)
+            entry = [blk[:16].tobytes() + bytes(16), key_bytes(body[0]), key_bytes(body[-1]),
+                     addr.to_bytes(8, "little")]
+            for (dst, n), e in zip(split.entry_ranges(img, s, 1, dbcm, ks), entry):
+                self.mem[dst:dst + n] = np.frombuffer(e, np.uint8)
+        infos = []
+        T = vcm * dbcm
+        for t in range(*tables):
+            k0, k_last = t * dbcm, plan.k_last(t)
+            nblk = k_last - k0 + 1
+            at = slot_ptr(split.index_block_slot(t, k_last))
+            blk = self.mem[at:at + BS]
+            index_size = spec.layout(BS)["index_size"]
+            addr = int(addresses[split.index_block_slot(t, k_last)])
+            blk[:256] = _header(index_size, addr, 4, spec.tree_id, nblk, dbcm, ks, cluster, snapshot_min)
+            for dst, n in split.entry_ranges(at, nblk, dbcm - nblk, dbcm, ks):
+                self.mem[dst:dst + n] = 0
+            _set_checksums(blk, index_size)
+            blk[index_size:-(-index_size // 4096) * 4096] = 0
+            kmin = self.mem[at + 256 + 32 * dbcm: at + 256 + 32 * dbcm + ks]
+            kmax_at = at + 256 + 32 * dbcm + ks * dbcm + ks * (nblk - 1)
+            info = np.zeros(128, np.uint8)
+            info[0:ks] = kmin
+            info[32:32 + ks] = self.mem[kmax_at:kmax_at + ks]
+            info[64:80] = blk[0:16]
+            info[96:104] = np.frombuffer(addr.to_bytes(8, "little"), np.uint8)
+            info[104:112] = np.frombuffer(int(snapshot_min).to_bytes(8, "little"), np.uint8)
+            info[112:120] = 0xFF
+            info[120:124] = np.frombuffer(min(T, value_count - t * T).to_bytes(4, "little"), np.uint8)
+            info[124:126] = np.frombuffer(int(spec.tree_id).to_bytes(2, "little"), np.uint8)
+            info[126] = (level_b & 0x3F) | (1 << 6)
+            infos.append(info)
+        res = SimpleNamespace(status=0, table_count=tables[1] - tables[0])
+        return res, (np.stack(infos) if infos else np.zeros((0, 128), np.uint8))
+
+
+class _ThreadExchange:
+    """All-gathers between rank threads of one process (CPU tests)."""
+
+    def __init__(self, world):
+        self.world, self.barrier, self.slots = world, threading.Barrier(world), [None] * world
+
+    def rank(self, r, eng):
+        ex = self
+
+        class Rank:
+            def all_gather_counts(self, count):
+                return ex._gather(r, int(count))
+
+            def all_gather_heads(self, engine, segments, nbytes):
+                mine = b"".join(engine.mem[p:p + n].tobytes() for p, n in segments).ljust(nbytes, b"\0")
+                got = ex._gather(r, mine)
+                bufs = [engine.upload(np.frombuffer(g, np.uint8)) if nbytes else None for g in got]
+                return bufs, [b.ptr if b else 0 for b in bufs]
+        return Rank()
+
+    def _gather(self, r, x):
+        self.barrier.wait()
+        self.slots[r] = x
+        self.barrier.wait()
+        out = list(self.slots)
+        self.barrier.wait()
+        return out
+
+
+def _run_split(spec, ji, addrs, world, cuts, exchanges, engines):
+    from tigerbeetle_amd.engine import Job
+    results, errors = [None] * world, []
+    b_all = _b_all(ji)
+
+    def rank(p):
+        try:
+            eng = engines[p]
+            (a0, b0), (a1, b1) = cuts[p], cuts[p + 1]
+            segs = []
+            for vals in (ji.a_values[a0:a1], b_all[b0:b1]):
+                buf = eng.upload(np.ascontiguousarray(vals)) if len(vals) else None
+                segs.append([(buf.ptr, len(vals))] if buf else [])
+            job = Job(spec, segs[0], segs[1], ji.a_immutable, ji.drop_tombstones, LEVEL_B, CLUSTER, SNAPSHOT_MIN,
+                      np.asarray(addrs, np.uint64), None)
+            results[p] = split.compact_split(eng, job, cuts, exchanges[p], p, staged=True)
+        except Exception as e:  # noqa: BLE001 - reported below, other threads must not hang
+            errors.append((p, repr(e)))
+            exchanges[p]  # noqa: B018
+            raise
+    threads = [threading.Thread(target=rank, args=(p,)) for p in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not errors, errors
+    return results
+
+
+def _check_union(spec, ji, addrs, world, results, engines):
+    whole = _compact(_oracle, spec, ji.a_values, ji.a_immutable, _b_all(ji), ji.drop_tombstones, addrs)
+    plan = results[0].plan
+    assert plan.total == whole.value_count
+    lay = spec.layout(BS)
+    vcm, dbcm = lay["block_value_count_max"], lay["data_block_count_max"]
+    got = {}
+    for p, res in enumerate(results):
+        arena = engines[p].mem[res.arena.ptr:res.arena.ptr + res.arena.nbytes].reshape(-1, BS)
+        for k in range(*res.blocks):
+            got[split.data_block_slot(k, dbcm)] = arena[split.data_block_slot(k, dbcm)]
+        for t in range(*res.tables):
+            got[split.index_block_slot(t, plan.k_last(t))] = arena[split.index_block_slot(t, plan.k_last(t))]
+    assert sorted(got) == list(range(len(whole.blocks)))
+    for i, w in enumerate(whole.blocks):
+        assert np.array_equal(disk_image(got[i]), disk_image(w)), i
+    assert np.array_equal(np.concatenate([r.table_infos for r in results]), whole.table_infos)
+    # Exchanged bytes: at most one partial block's values and one table's entries per rank.
+    for r in results:
+        assert r.exchanged["heads"] <= (vcm - 1) * spec.value_size
+        assert r.exchanged["entries"] <= (dbcm - 1) * split.entry_bytes(spec.key_size)
+
+
 @pytest.mark.parametrize("case", range(len(CASES)))
 @pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
 @pytest.mark.parametrize("method", ["merge_path", "blocks"])
 def test_split_job_equals_unsplit_job(oracle_lib, case, world, method):
     spec, ji, addrs = _inputs(case)
-    whole = _compact(oracle_lib, spec, ji.a_values, ji.a_immutable, _b_all(ji), ji.drop_tombstones, addrs)
     cuts = _cuts(spec, ji, world) if method == "merge_path" else _block_cuts(spec, ji, world)
-    surv = [_rank_phase1(oracle_lib, spec, ji, cuts, p) for p in range(world)]
-    lay = spec.layout(BS)
-    plan = split.plan_tables([len(s) for s in surv], lay["block_value_count_max"], lay["data_block_count_max"])
-    assert plan.total == whole.value_count
-    images, infos = [], []
-    for p in range(world):
-        im, inf = _rank_phase2(oracle_lib, spec, plan, p, lambda q: surv[q], addrs)
-        images += im
-        infos.append(inf)
-    expect = [disk_image(b) for b in whole.blocks]
-    assert len(images) == len(expect)
-    for g, w in zip(images, expect):
-        assert np.array_equal(g, w)
-    assert np.array_equal(np.concatenate(infos), whole.table_infos)
+    engines = [_OracleEngine(spec) for _ in range(world)]
+    tex = _ThreadExchange(world)
+    results = _run_split(spec, ji, addrs, world, cuts, [tex.rank(p, engines[p]) for p in range(world)], engines)
+    _check_union(spec, ji, addrs, world, results, engines)
 
 
-# --- the same flow with the exchange over gloo, world_size 2 and 3 -----------
+# --- the same flow with the exchange over gloo (TorchExchange), world 2 and 3 --
 
 def _free_port():
     s = socket.socket()
@@ -212,24 +422,27 @@ def _worker(rank, world, port, case, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from oracle import oracle
+    from tigerbeetle_amd.engine import Job
     spec, ji, addrs = _inputs(case)
     reads = []
     cuts = _block_cuts(spec, ji, world, reads)      # identical on every rank, no communication
     assert len(reads) <= 2 * (world - 1)            # index keys + boundary blocks only
-    mine = _rank_phase1(oracle, spec, ji, cuts, rank)  # stages only [cuts[rank], cuts[rank+1])
-    ex = split.TorchExchange(dist)
-    lay = spec.layout(BS)
-    plan = split.plan_tables(ex.all_gather_counts(len(mine)), lay["block_value_count_max"],
-                             lay["data_block_count_max"])
-    vs = spec.value_size
-    head = np.zeros((max(1, plan.head_max), vs), np.uint8)
-    head[: plan.need[rank]] = mine[: plan.need[rank]]
-    heads = [torch.empty(head.size, dtype=torch.uint8) for _ in range(world)]
-    dist.all_gather(heads, torch.from_numpy(head.reshape(-1)))
-    heads = [h.numpy().reshape(-1, vs) for h in heads]
-    images, infos = _rank_phase2(oracle, spec, plan, rank, lambda r: mine if r == rank else heads[r], addrs)
-    q.put((rank, [bytes(x) for x in images], infos.tobytes()))
+    eng = _OracleEngine(spec)
+    (a0, b0), (a1, b1) = cuts[rank], cuts[rank + 1]
+    segs = []
+    for vals in (ji.a_values[a0:a1], _b_all(ji)[b0:b1]):  # stages only this rank's range
+        buf = eng.upload(np.ascontiguousarray(vals)) if len(vals) else None
+        segs.append([(buf.ptr, len(vals))] if buf else [])
+    job = Job(spec, segs[0], segs[1], ji.a_immutable, ji.drop_tombstones, LEVEL_B, CLUSTER, SNAPSHOT_MIN,
+              np.asarray(addrs, np.uint64), None)
+    res = split.compact_split(eng, job, cuts, split.TorchExchange(dist), rank, staged=True)
+    arena = eng.mem[res.arena.ptr:res.arena.ptr + res.arena.nbytes].reshape(-1, BS)
+    dbcm = spec.layout(BS)["data_block_count_max"]
+    mine = {split.data_block_slot(k, dbcm): bytes(disk_image(arena[split.data_block_slot(k, dbcm)]))
+            for k in range(*res.blocks)}
+    mine.update({split.index_block_slot(t, res.plan.k_last(t)):
+                 bytes(disk_image(arena[split.index_block_slot(t, res.plan.k_last(t))])) for t in range(*res.tables)})
+    q.put((rank, mine, res.table_infos.tobytes(), res.exchanged))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -248,9 +461,12 @@ def test_split_exchange_over_gloo(oracle_lib, world, case):
         assert p.exitcode == 0
     spec, ji, addrs = _inputs(case)
     whole = _compact(oracle_lib, spec, ji.a_values, ji.a_immutable, _b_all(ji), ji.drop_tombstones, addrs)
-    images = [im for _, ims, _ in out for im in ims]
-    assert images == [bytes(disk_image(b)) for b in whole.blocks]
-    assert b"".join(inf for _, _, inf in out) == whole.table_infos.tobytes()
+    got = {}
+    for _, mine, _, _ in out:
+        got.update(mine)
+    assert sorted(got) == list(range(len(whole.blocks)))
+    assert [got[i] for i in range(len(whole.blocks))] == [bytes(disk_image(b)) for b in whole.blocks]
+    assert b"".join(inf for _, _, inf, _ in out) == whole.table_infos.tobytes()
 
 
 # --- TorchExchange.all_gather_heads (host-staged gloo path) on CPU -----------

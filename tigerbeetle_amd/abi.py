@@ -35,6 +35,7 @@ CONFIG_LATENCY = 4
 COMPACTION_VALUES_ONLY = 1  # tbc_compaction.flags
 COMPACTION_GRID = 2
 COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped
+COMPACTION_COUNT_ONLY = 8  # the merge alone: survivor counts (phase A of a split job)
 SPECULATION_NONE, SPECULATION_HELD, SPECULATION_BROKEN = 0, 1, 2
 ABI_VERSION = 4
 
@@ -119,6 +120,26 @@ class Compaction(ctypes.Structure):
         ("tables_b", ctypes.POINTER(TableRef)),
         ("table_count_a", ctypes.c_uint32),
         ("table_count_b", ctypes.c_uint32),
+        ("output_offset", ctypes.c_uint64),
+    ]
+
+
+class Seal(ctypes.Structure):
+    """tbc_seal: sealing of one job split by key range (tbc_compaction_seal)."""
+    _fields_ = [
+        ("tree", Tree),
+        ("cluster", ctypes.c_uint64 * 2),
+        ("snapshot_min", ctypes.c_uint64),
+        ("level_b", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+        ("address_count", ctypes.c_uint32),
+        ("addresses", ctypes.POINTER(ctypes.c_uint64)),
+        ("output_blocks", ctypes.c_void_p),
+        ("value_count", ctypes.c_uint64),
+        ("block_first", ctypes.c_uint32),
+        ("block_count", ctypes.c_uint32),
+        ("table_first", ctypes.c_uint32),
+        ("table_count", ctypes.c_uint32),
     ]
 
 
@@ -165,6 +186,7 @@ _SIGNATURES = {
     "tbc_kway_wait": (ctypes.c_int, [_P]),
     "tbc_kway_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "tbc_kway_release": (None, [_P]),
+    "tbc_compaction_seal": (ctypes.c_int, [_P, ctypes.POINTER(Seal), ctypes.POINTER(_P)]),
     "tbc_compaction_submit": (ctypes.c_int, [_P, ctypes.POINTER(Compaction), ctypes.c_uint32,
                                              ctypes.POINTER(_P)]),
     "tbc_batch_poll": (ctypes.c_int, [_P]),

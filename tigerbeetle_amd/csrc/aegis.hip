@@ -1476,7 +1476,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     const uint32_t C = chain_waves;
     auto locate = [&](uint32_t m, int &ji_, uint32_t &k_) {
         ji_ = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
-        k_ = m - jobs[ji_].dblock_base;
+        k_ = m - jobs[ji_].dblock_base + jobs[ji_].block_lo;
         return m < total && k_ < res[jobs[ji_].job_index].data_block_count &&
                (phase != 1 || !phase_skips(jobs[ji_], res, phase));
     };
@@ -1575,7 +1575,8 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         // the block must have landed.
         // (A speculated job whose speculation held was merged by
         // k_produce_unique, before this kernel in stream order: no counts.)
-        const bool produced = j.unique && res[j.job_index].spec != kSpecBroken;
+        // (Seal jobs: the caller placed the bodies, tbc_compaction_seal.)
+        const bool produced = (j.unique && res[j.job_index].spec != kSpecBroken) || j.seal;
         if (!produced &&
             __hip_atomic_load(ready + j.dblock_base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
             gst<uint32_t>(const_cast<uint32_t *>(&res[j.job_index].invariant), 0xdeafu);
@@ -1715,12 +1716,12 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
             cb.advance(bb);
             if ((sm >> lane) & 1) {
                 const uint32_t r = __builtin_popcountll(sm & lt);
-                const uint32_t o = out0 + s_pre[0][w] + r;
+                const uint64_t o = j.out_offset + out0 + s_pre[0][w] + r; // the job's merged output position
                 const uint8_t *src = ((am >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(am & lt), vs)
                                                         : cb.elem(bb + __builtin_popcountll(valid & ~am & lt), vs);
-                const uint32_t k = o / vcm;
+                const uint32_t k = (uint32_t)(o / vcm);
                 uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize +
-                               (size_t)(o - k * vcm) * vs;
+                               (size_t)(o - (uint64_t)k * vcm) * vs;
                 s_src[wv][r] = (uint64_t)(uintptr_t)src;
                 s_dst[wv][r] = (uint64_t)(uintptr_t)dst;
             }
@@ -1736,7 +1737,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
         // an agent-scope release writes back the XCD's L2 — per tile, that
         // quadrupled this kernel's time.)
         __syncthreads();
-        if (tid == 0) {
+        if (tid == 0 && j.out_offset == 0) { // (an offset job is VALUES_ONLY: no chains count them)
             const uint32_t cnt = s_pre[0][W];
             uint32_t o = out0;
             while (o < out0 + cnt) {
@@ -1774,11 +1775,11 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
     const uint32_t wave = blockIdx.x;
     const int ji = find_job(jobs, njobs, wave, [](const JobDesc &d) { return d.table_base; });
     const JobDesc &j = jobs[ji];
-    const uint32_t t = wave - j.table_base;
+    const uint32_t t = wave - j.table_base + j.table_lo; // the job's table index
     const uint32_t lane = threadIdx.x & 63, g = lane & 31;
     const uint32_t db = res[j.job_index].data_block_count;
     const uint32_t tables = res[j.job_index].table_count;
-    if (t >= j.table_max || t >= tables) return;
+    if (t - j.table_lo >= j.table_max || t >= tables) return;
     const uint64_t n_out = res[j.job_index].value_count;
     const uint32_t k0 = t * j.dbcm;
     const uint32_t nblk = (db - k0) < j.dbcm ? (db - k0) : j.dbcm;
@@ -1787,18 +1788,28 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
     uint8_t *idx = (uint8_t *)sIdx;
     for (uint32_t i = lane; i < j.index_size / 4; i += 64) sIdx[i] = 0;
     wave_sync();
+    const uint8_t *image = block_ptr(j, index_block_slot(t, k_last)); // seal jobs: the entries in place
     for (uint32_t s = lane; s < nblk; s += 64) {
         const uint32_t k = k0 + s;
         const uint64_t first = (uint64_t)k * j.vcm;
         const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
         const uint32_t slot = data_block_slot(k, j.dbcm);
         const uint8_t *blk = block_ptr(j, slot);
-        uint64_t kmin[4], kmax[4];
-        value_key(j, blk + kHeaderSize, kmin);
-        value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
+        uint64_t kmin[4] = {0, 0, 0, 0}, kmax[4] = {0, 0, 0, 0};
         uint64_t *cks = (uint64_t *)(idx + j.idx_checksums_off + 32 * s);
-        cks[0] = ld64(blk);
-        cks[1] = ld64(blk + 8);
+        if (j.seal) {
+            for (uint32_t l = 0; l < ks / 8; l++) {
+                kmin[l] = ld64(image + j.idx_keys_min_off + ks * s + 8 * l);
+                kmax[l] = ld64(image + j.idx_keys_max_off + ks * s + 8 * l);
+            }
+            cks[0] = ld64(image + j.idx_checksums_off + 32 * s);
+            cks[1] = ld64(image + j.idx_checksums_off + 32 * s + 8);
+        } else {
+            value_key(j, blk + kHeaderSize, kmin);
+            value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
+            cks[0] = ld64(blk);
+            cks[1] = ld64(blk + 8);
+        }
         for (uint32_t l = 0; l < ks / 8; l++) {
             ((uint64_t *)(idx + j.idx_keys_min_off + ks * s))[l] = kmin[l];
             ((uint64_t *)(idx + j.idx_keys_max_off + ks * s))[l] = kmax[l];
@@ -1839,7 +1850,7 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
         const uint64_t vcount = (n_out - (uint64_t)k0 * j.vcm) < (uint64_t)nblk * j.vcm
                                     ? (n_out - (uint64_t)k0 * j.vcm)
                                     : (uint64_t)nblk * j.vcm;
-        uint32_t *info = (uint32_t *)(infos + (size_t)(j.info_base + t) * kTableInfoSize);
+        uint32_t *info = (uint32_t *)(infos + (size_t)(j.info_base + t - j.table_lo) * kTableInfoSize);
         uint32_t v = 0;
         const uint32_t i = g; // dwords 0..31
         if (i < 8) {
@@ -2044,6 +2055,62 @@ int launch_assemble(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint
     hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, (hipStream_t)stream, d_jobs, njobs, total_tiles,
                        d_status, d_masks, d_splits, d_ready, d_results, phase);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Seal jobs (tbc_compaction_seal): one thread per finished data block writes
+// its index entry — checksum (16 bytes, then 16 zero), key_min, key_max,
+// address (TableIndex, schema.zig:80-260) — into its table's index block
+// slot, where the table's owner (this rank, or another one the entries are
+// sent to) seals the index block.
+__global__ __launch_bounds__(256) void k_index_entries(const JobDesc *job, uint32_t blocks, const JobResultDev *res) {
+    const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+    const JobDesc &j = *job;
+    if (m >= blocks) return;
+    const uint32_t k = j.block_lo + m;
+    const uint32_t db = res->data_block_count;
+    if (k >= db) return;
+    const uint32_t t = k / j.dbcm, s = k - t * j.dbcm;
+    const uint32_t k_last = ((t + 1) * j.dbcm < db ? (t + 1) * j.dbcm : db) - 1;
+    const uint64_t first = (uint64_t)k * j.vcm;
+    const uint32_t cnt = (uint32_t)((res->value_count - first) < j.vcm ? (res->value_count - first) : j.vcm);
+    const uint32_t slot = data_block_slot(k, j.dbcm);
+    const uint8_t *blk = block_ptr(j, slot);
+    uint8_t *image = block_ptr(j, index_block_slot(t, k_last));
+    uint64_t kmin[4], kmax[4];
+    value_key(j, blk + kHeaderSize, kmin);
+    value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
+    uint64_t *cks = (uint64_t *)(image + j.idx_checksums_off + 32 * s);
+    cks[0] = ld64(blk);
+    cks[1] = ld64(blk + 8);
+    cks[2] = cks[3] = 0;
+    for (uint32_t l = 0; l < j.key_size / 8; l++) {
+        ((uint64_t *)(image + j.idx_keys_min_off + j.key_size * s))[l] = kmin[l];
+        ((uint64_t *)(image + j.idx_keys_max_off + j.key_size * s))[l] = kmax[l];
+    }
+    ((uint64_t *)(image + j.idx_addresses_off))[s] = gld<uint64_t>(j.addresses + slot);
+}
+
+int launch_seal(const JobDesc *d_job, uint32_t blocks, uint32_t tables, JobResultDev *d_results, uint8_t *d_infos,
+                void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (blocks) {
+        const uint32_t waves = (blocks + 1) / 2;
+        const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
+        const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
+        hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_job,
+                           1, blocks, (const JobResultDev *)d_results, (const uint64_t *)nullptr,
+                           (const uint64_t *)nullptr, (const uint32_t *)nullptr, (const SplitDesc *)nullptr, c,
+                           (const uint32_t *)nullptr, (const SplitDesc *)nullptr, 0u);
+        if (hipGetLastError() != hipSuccess) return -1;
+        hipLaunchKernelGGL(k_index_entries, dim3((blocks + 255) / 256), dim3(256), 0, s, d_job, blocks,
+                           (const JobResultDev *)d_results);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (tables) {
+        hipLaunchKernelGGL(k_index_blocks, dim3(tables), dim3(1024), 0, s, d_job, 1, d_results, d_infos);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    return 0;
 }
 
 // Pipelined batch, front (engine stream, in order with every later batch's

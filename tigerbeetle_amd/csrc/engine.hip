@@ -364,6 +364,10 @@ struct tbc_batch {
     int nmarks = 0;
     bool complete = false;
     tbc_status result = TBC_PENDING;
+    // tbc_compaction_seal: what the call finished (the device results hold
+    // the whole job's shape, which its kernels need).
+    bool seal = false;
+    tbc_compaction_result seal_result{};
 };
 
 struct tbc_kway {
@@ -1362,12 +1366,15 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         memset(&d, 0, sizeof d);
         Layout L;
         const bool grid = (c.flags & TBC_COMPACTION_GRID) != 0;
+        const bool count_only = (c.flags & TBC_COMPACTION_COUNT_ONLY) != 0;
         if (!compute_layout(&c.tree, e->block_size, &L) || L.index_size > kIndexLdsMax ||
-            (c.a_immutable && c.segment_count_a > 1) || (!grid && !c.output_blocks) ||
+            (c.a_immutable && c.segment_count_a > 1) || (!grid && !c.output_blocks && !count_only) ||
             (c.segment_count_a && !c.segments_a) || (!grid && c.segment_count_b && !c.segments_b) ||
             (c.address_count && !c.addresses) ||
-            (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID | TBC_COMPACTION_UNIQUE_KEYS)) ||
-            ((c.flags ^ flags0) & ~TBC_COMPACTION_UNIQUE_KEYS) ||
+            (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID | TBC_COMPACTION_UNIQUE_KEYS |
+                         TBC_COMPACTION_COUNT_ONLY)) ||
+            ((c.flags ^ flags0) & ~TBC_COMPACTION_UNIQUE_KEYS) || (grid && count_only) ||
+            (c.output_offset && !(c.flags & TBC_COMPACTION_VALUES_ONLY)) ||
             (grid && ((c.flags & TBC_COMPACTION_VALUES_ONLY) || c.grid != grid0 || !c.grid || c.grid->engine != e ||
                       (c.table_count_a && (c.a_immutable || !c.tables_a)) || (c.table_count_b && !c.tables_b) ||
                       (!c.a_immutable && c.segment_count_a)))) {
@@ -1415,7 +1422,11 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         const uint64_t n = na + nb;
         const uint64_t db_max = (n + L.vcm - 1) / L.vcm;
         const uint64_t tables_max = (db_max + L.dbcm - 1) / L.dbcm;
-        if (db_max + tables_max > c.address_count) { delete b; return TBC_ERR_CAPACITY; }
+        if (!count_only && db_max + tables_max > c.address_count) { delete b; return TBC_ERR_CAPACITY; }
+        if (c.output_offset && n) { // the job's slot of the last global data block this range writes
+            const uint64_t k_last = (c.output_offset + n - 1) / L.vcm;
+            if (k_last + k_last / L.dbcm + 1 > c.address_count) { delete b; return TBC_ERR_CAPACITY; }
+        }
         d.key_kind = c.tree.key_kind;
         d.usage = c.tree.usage;
         d.value_size = c.tree.value_size;
@@ -1448,6 +1459,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                                   ? segs[0].second : 0;
         }
         d.address_count = c.address_count;
+        d.out_offset = c.output_offset;
         d.out_blocks = grid ? nullptr : (uint8_t *)c.output_blocks;
         d.grid_base = grid ? c.grid->base : nullptr;
         d.merge_tile = kMergeTile; // the staged merge's tile is set below, with the regime
@@ -1508,7 +1520,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // TBC_COMPACTION_UNIQUE_KEYS is honoured in the latency regime of a plain
     // batch: every chain runs at once, so starting them before any merge is
     // what it buys (aegis.hip produce_unique).
-    const bool spec_regime = !grid_mode && !pipeline && !(flags0 & TBC_COMPACTION_VALUES_ONLY) &&
+    const bool spec_regime = !grid_mode && !pipeline &&
+                             !(flags0 & (TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_COUNT_ONLY)) &&
                              (uint64_t)(dblocks + 1) / 2 <= fused_max_chain_waves();
     static const bool no_spec = getenv("TBC_NO_SPECULATION") != nullptr; // A/B measurement only
     // The speculated batch's index blocks and results on a tail stream
@@ -1763,6 +1776,13 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             if (ok) e->tail_out.push_back(std::move(to));
             else if (to.done) e->event_pool.push_back(to.done);
         }
+    } else if (flags0 & TBC_COMPACTION_COUNT_ONLY) {
+        // The merge alone: survivor counts (k_tile_scan's results), nothing written.
+        if (ok && count)
+            ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
+                              d_block_tile, d_order, d_res, s, mark_cb, b, nullptr, d_ticket, d_ready) == 0;
+        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res, hipMemcpyDeviceToHost, s) == hipSuccess;
+        ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     } else if (any_unique && spec_pipe) {
         // Front (engine stream): block splits and results of the speculated
         // jobs, the merge of the others and their bodies, the speculated
@@ -1902,7 +1922,7 @@ static tbc_status check_plain_job(const tbc_engine *e, const tbc_compaction &c, 
         (c.a_immutable && c.segment_count_a > 1) || !c.output_blocks || (c.segment_count_a && !c.segments_a) ||
         (c.segment_count_b && !c.segments_b) || (c.address_count && !c.addresses) ||
         (c.flags & ~(TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_GRID | TBC_COMPACTION_UNIQUE_KEYS)) ||
-        ((c.flags ^ flags0) & ~TBC_COMPACTION_UNIQUE_KEYS) || (c.flags & TBC_COMPACTION_GRID))
+        ((c.flags ^ flags0) & ~TBC_COMPACTION_UNIQUE_KEYS) || (c.flags & TBC_COMPACTION_GRID) || c.output_offset)
         return TBC_ERR_INVALID_ARGUMENT;
     uint64_t n = 0;
     for (int side = 0; side < 2; side++) {
@@ -1952,7 +1972,8 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     static const bool no_groups = getenv("TBC_NO_GROUPS") != nullptr; // A/B measurement only
     uint32_t groups = 1;
     std::vector<uint64_t> n(count, 0);
-    if (!no_groups && count >= 2 && !(jobs_in[0].flags & (TBC_COMPACTION_GRID | TBC_COMPACTION_VALUES_ONLY))) {
+    if (!no_groups && count >= 2 &&
+        !(jobs_in[0].flags & (TBC_COMPACTION_GRID | TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_COUNT_ONLY))) {
         uint64_t waves = 0;
         for (uint32_t i = 0; i < count; i++) {
             const tbc_compaction &c = jobs_in[i];
@@ -2002,6 +2023,104 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         first = last;
     }
     *out = parent;
+    return TBC_OK;
+}
+
+tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **out) {
+    if (!e || !sl || !out) return TBC_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    Layout L;
+    if (!compute_layout(&sl->tree, e->block_size, &L) || L.index_size > kIndexLdsMax || !sl->output_blocks ||
+        !sl->addresses || !sl->value_count)
+        return TBC_ERR_INVALID_ARGUMENT;
+    const uint64_t db = (sl->value_count + L.vcm - 1) / L.vcm, tables = (db + L.dbcm - 1) / L.dbcm;
+    if (db + tables > sl->address_count) return TBC_ERR_CAPACITY;
+    if ((uint64_t)sl->block_first + sl->block_count > db || (uint64_t)sl->table_first + sl->table_count > tables)
+        return TBC_ERR_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    tbc_batch *b = new (std::nothrow) tbc_batch();
+    if (!b) return TBC_ERR_OUT_OF_MEMORY;
+    b->engine = e;
+    b->count = 1;
+    b->info_base.assign(1, 0);
+    b->status.assign(1, TBC_OK);
+    b->seal = true;
+    // What this call finishes: its data blocks and tables, their values.
+    {
+        tbc_compaction_result &r = b->seal_result;
+        const uint64_t T = (uint64_t)L.vcm * L.dbcm;
+        const uint64_t v0 = (uint64_t)sl->table_first * T;
+        const uint64_t v1 = std::min<uint64_t>((uint64_t)(sl->table_first + sl->table_count) * T, sl->value_count);
+        r.value_count = sl->table_count ? v1 - v0 : 0;
+        r.data_block_count = sl->block_count;
+        r.table_count = sl->table_count;
+        r.block_count = sl->block_count + sl->table_count;
+    }
+    JobDesc d;
+    memset(&d, 0, sizeof d);
+    d.key_kind = sl->tree.key_kind;
+    d.usage = sl->tree.usage;
+    d.value_size = sl->tree.value_size;
+    d.timestamp_offset = sl->tree.timestamp_offset;
+    d.key_size = L.key_size;
+    d.vcm = L.vcm;
+    d.dbcm = L.dbcm;
+    d.index_size = L.index_size;
+    d.idx_checksums_off = L.cks_off;
+    d.idx_keys_min_off = L.kmin_off;
+    d.idx_keys_max_off = L.kmax_off;
+    d.idx_addresses_off = L.addr_off;
+    d.block_size = e->block_size;
+    d.tree_id = sl->tree.tree_id;
+    d.level_b = sl->level_b;
+    d.cluster_lo = sl->cluster[0];
+    d.cluster_hi = sl->cluster[1];
+    d.snapshot_min = sl->snapshot_min;
+    d.address_count = sl->address_count;
+    d.out_blocks = (uint8_t *)sl->output_blocks;
+    d.merge_tile = kMergeTile;
+    d.dblock_max = sl->block_count;
+    d.table_max = sl->table_count;
+    d.block_lo = sl->block_first;
+    d.table_lo = sl->table_first;
+    d.seal = 1;
+    JobResultDev r0;
+    memset(&r0, 0, sizeof r0);
+    r0.value_count = sl->value_count;
+    r0.data_block_count = (uint32_t)db;
+    r0.table_count = (uint32_t)tables;
+    r0.block_count = (uint32_t)(db + tables);
+    const uint64_t sz_job = align_up(sizeof(JobDesc), 256), sz_addr = align_up(8ull * sl->address_count, 256);
+    const uint64_t sz_res = align_up(sizeof(JobResultDev), 256);
+    const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)std::max<uint32_t>(1, sl->table_count), 256);
+    uint8_t *dbase = e->dev.open(sz_job + sz_addr + sz_res + sz_infos, &b->dev_region);
+    uint8_t *hbase = dbase ? e->host.open(sz_job + sz_addr + sz_res + sz_infos, &b->host_region) : nullptr;
+    if (!dbase || !hbase) {
+        if (dbase) e->dev.close(b->dev_region);
+        delete b;
+        return TBC_ERR_OUT_OF_MEMORY;
+    }
+    d.addresses = (const uint64_t *)(dbase + sz_job);
+    memcpy(hbase, &d, sizeof d);
+    memcpy(hbase + sz_job, sl->addresses, 8ull * sl->address_count);
+    memcpy(hbase + sz_job + sz_addr, &r0, sizeof r0);
+    JobResultDev *d_res = (JobResultDev *)(dbase + sz_job + sz_addr);
+    b->h_results = (JobResultDev *)(hbase + sz_job + sz_addr);
+    b->h_infos = hbase + sz_job + sz_addr + sz_res;
+    b->done = take_event(e);
+    hipStream_t s = e->stream;
+    bool ok = b->done != nullptr && join_tails(e) &&
+              hipMemcpyAsync(dbase, hbase, sz_job + sz_addr + sz_res, hipMemcpyHostToDevice, s) == hipSuccess &&
+              launch_seal((const JobDesc *)dbase, sl->block_count, sl->table_count, d_res,
+                          dbase + sz_job + sz_addr + sz_res, s) == 0 &&
+              hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess &&
+              hipEventRecord(b->done, s) == hipSuccess;
+    if (!ok) {
+        tbc_synchronize(e);
+        tbc_batch_release(b);
+        return TBC_ERR_DEVICE;
+    }
+    *out = b;
     return TBC_OK;
 }
 
@@ -2086,6 +2205,10 @@ tbc_status tbc_batch_result(tbc_batch *b, uint32_t index, tbc_compaction_result 
     out->table_count = r.table_count;
     out->block_count = r.block_count;
     out->status = r.status;
+    if (b->seal) {
+        *out = b->seal_result;
+        out->status = r.status;
+    }
     if (table_infos) {
         if (table_info_capacity < r.table_count) return TBC_ERR_CAPACITY;
         memcpy(table_infos, b->h_infos + (size_t)b->info_base[index] * kTableInfoSize,

@@ -83,6 +83,17 @@ struct JobDesc {
     // tiles of kUniqueTile merged positions, batch-wide numbering, and their
     // utile_count + 1 merge-path splits (0 tiles for a job not speculated).
     uint32_t utile_base, utile_count, usplit_base, pad1;
+    // Key-range split of one job (split.py). VALUES_ONLY with
+    // out_offset: survivor o lands at the job's merged output position
+    // out_offset + o (its global data block and slot). Seal jobs
+    // (tbc_compaction_seal, seal = 1): bodies are already in place; data
+    // blocks [block_lo, block_lo + dblock_max) are finished and their index
+    // entries written into their tables' index block slots, and the index
+    // blocks of tables [table_lo, table_lo + table_max) are sealed from the
+    // entries found there.
+    uint64_t out_offset;
+    uint32_t block_lo, table_lo;
+    uint32_t seal, pad2;
 };
 
 // Merged positions per tile of k_merge_unique: the tile's keys (plus three
@@ -336,6 +347,10 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
                        void *stream, void (*mark)(void *, const char *), void *mark_ctx);
 int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
                         uint8_t *d_infos, void *stream);
+// tbc_compaction_seal (one seal job): chains + headers of its data blocks and
+// their index entries, then its index blocks from the entries in place.
+int launch_seal(const JobDesc *d_job, uint32_t blocks, uint32_t tables, JobResultDev *d_results, uint8_t *d_infos,
+                void *stream);
 // Pipelined speculated batches: every speculated job's bodies, one producer
 // wave per data block (aegis.hip k_produce_unique), and the bodies of the
 // jobs the merge decided (k_assemble; phase 0 / 1 as phase_skips).

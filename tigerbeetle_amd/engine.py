@@ -73,6 +73,7 @@ class Job:
     grid: "Grid | None" = None   # COMPACTION_GRID: disk tables by reference, outputs into the grid
     tables_a: list = field(default_factory=list)  # [(index address, index checksum u128, value_count)]
     tables_b: list = field(default_factory=list)
+    output_offset: int = 0  # VALUES_ONLY: survivors land at the job's output positions output_offset + i (split.py)
     _keep: list = field(default_factory=list)
     _ctype: object = field(default=None, repr=False)
 
@@ -108,6 +109,7 @@ class Job:
         c.addresses = addrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         c.address_count = len(addrs)
         c.output_blocks = self.output.ptr if self.output is not None else None
+        c.output_offset = self.output_offset
         self._ctype = c
         return c
 
@@ -455,6 +457,35 @@ class Engine:
         h = ctypes.c_void_p()
         check(lib().tbc_compaction_submit(self.handle, arr, len(jobs), ctypes.byref(h)), "tbc_compaction_submit")
         return Batch(self, h.value, jobs)
+
+    def seal(self, tree: TreeSpec, cluster: int, snapshot_min: int, level_b: int, addresses, arena: DeviceBuffer,
+             value_count: int, blocks: tuple, tables: tuple):
+        """tbc_compaction_seal of one split job (blocking): finish data blocks
+        [blocks[0], blocks[1]) in place (headers, checksums, index entries),
+        then seal tables [tables[0], tables[1]) from the entries in their index
+        block slots. Returns (result, TableInfos of the sealed tables)."""
+        addrs = np.ascontiguousarray(addresses, dtype=np.uint64)
+        sl = abi.Seal()
+        sl.tree = tree.ctype()
+        sl.cluster[0], sl.cluster[1] = cluster & ((1 << 64) - 1), cluster >> 64
+        sl.snapshot_min = snapshot_min
+        sl.level_b = level_b
+        sl.address_count = len(addrs)
+        sl.addresses = addrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        sl.output_blocks = arena.ptr
+        sl.value_count = value_count
+        sl.block_first, sl.block_count = blocks[0], blocks[1] - blocks[0]
+        sl.table_first, sl.table_count = tables[0], tables[1] - tables[0]
+        h = ctypes.c_void_p()
+        check(lib().tbc_compaction_seal(self.handle, ctypes.byref(sl), ctypes.byref(h)), "tbc_compaction_seal")
+        b = Batch(self, h.value, [None])
+        try:
+            b.wait()
+            r, infos = b.result(0)
+            check(r.status, "tbc_compaction_seal")
+            return r, infos
+        finally:
+            b.release()
 
 
 def stage_blocks(engine: Engine, tables: list, value_size: int, block_size: int = BLOCK_SIZE):

@@ -19,23 +19,32 @@ blocks (compaction.zig:806-886), counted from the job's first survivor. So:
    most two data blocks per input table, and stages only the blocks of its
    own range (`rank_blocks`); or `split_points`, exact merge-path
    co-ranking over A ∪ B, for a caller that holds every key anyway.
-2. Phase 1: each rank compacts its key range values-only (bodies in scratch
-   data-block slots, no headers or checksums) and takes its survivor count c_p.
-3. Exchange (the only collective): all-gather of the counts c_p, then of each
-   rank's head survivors — the ones the previous table owner still needs to
-   complete a table that starts before this rank's range (≤ one table).
-4. Phase 2: rank p owns the output tables whose first survivor is its own and
-   re-blocks them: a compaction whose disk A is exactly those survivors (own
-   tail + received heads) and whose B is empty writes every value unchanged
-   (copy(.a), compaction.zig:786-804), with the job's addresses for those
-   tables. The blocks, index blocks, checksums and TableInfos are therefore
-   byte-identical to the unsplit job's (tested against the oracle).
+2. Counts: each rank merges its key range without writing anything
+   (TBC_COMPACTION_COUNT_ONLY) for its survivor count c_p; an all-gather of
+   the counts and an exclusive scan give every rank its global output
+   offset o_p (`plan_split`).
+3. Bodies in place: each rank merges its range again (VALUES_ONLY with
+   tbc_compaction.output_offset = o_p), writing every survivor at its global
+   output position: its data block and slot in the job's own block layout.
+4. Data block k belongs to the rank holding its first value (k·vcm); the
+   values of a block that starts on an earlier rank (at most one block per
+   rank: positions [o_p, first block boundary)) go to that block's owner
+   (all-gather of ≤ vcm - 1 values per rank, one copy on the owner).
+5. Each rank finishes the data blocks it owns in place (tbc_compaction_seal:
+   AEGIS-128L body and header checksums, data_block_finish) and writes their
+   index entries (checksum, key_min, key_max, address) into their tables'
+   index block slots.
+6. Table t belongs to the owner of its first data block. A rank whose first
+   block is inside an earlier rank's table sends that table's owner its
+   entries (all-gather of ≤ dbcm - 1 entries per rank, 40 + 2·key_size
+   bytes each); the owner copies them into its index block image and seals
+   its tables (index_block_finish, TableInfo).
 
-Phase 1 runs with TBC_COMPACTION_VALUES_ONLY (merge + body assembly, no AEGIS
-chains or index blocks), so the split costs one extra HBM pass over the
-survivors, not a second set of checksums. Splitting one job pays off only when
-a job is larger than a GPU's share of the half-bar, which no BASELINE config
-needs.
+No value moves twice: the rank merges write the bodies where the blocks
+are, and only one partial block's values plus one table's index entries per
+rank cross ranks. The blocks, checksums and TableInfos are the unsplit job's
+byte for byte (the union over ranks of each rank's data blocks
+`plan.blocks(p)` and tables `plan.tables(p)`; tested against the oracle).
 """
 from __future__ import annotations
 
@@ -43,7 +52,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .abi import COMPACTION_VALUES_ONLY
+from .abi import COMPACTION_VALUES_ONLY as VALUES_ONLY
 
 HEADER_SIZE = 256
 
@@ -196,76 +205,102 @@ def range_segments(counts: list, lo: int, hi: int) -> list:
 
 
 # ---------------------------------------------------------------------------
-# Output ownership after the count exchange.
+# Output ownership after the count exchange (pure arithmetic, same on every rank).
+
+def data_block_slot(k: int, dbcm: int) -> int:
+    """Acquire-order slot of data block k (tbc_internal.h data_block_slot)."""
+    return k + k // dbcm
+
+
+def index_block_slot(t: int, k_last: int) -> int:
+    """Slot of the index block of table t whose last data block is k_last."""
+    return k_last + t + 1
+
 
 @dataclass
-class TablePlan:
-    offsets: list          # global index of each rank's first survivor
-    total: int             # survivors of the whole job
-    table_values: int      # values per full table (vcm · dbcm)
-    tables: list           # [(t0, t1)] tables owned by each rank
-    need: list             # head survivors each rank must send (to earlier owners)
+class SplitPlan:
+    counts: list   # survivors of each rank's key range
+    offsets: list  # global output position of each rank's first survivor
+    total: int     # survivors of the whole job
+    vcm: int
+    dbcm: int
+
+    @property
+    def data_blocks(self) -> int:
+        return -(-self.total // self.vcm)
+
+    @property
+    def table_count(self) -> int:
+        return -(-self.data_blocks // self.dbcm)
+
+    def blocks(self, p: int) -> tuple:
+        """[k0, k1): the data blocks whose first value is rank p's (it finishes them)."""
+        o, c = self.offsets[p], self.counts[p]
+        k0, k1 = -(-o // self.vcm), -(-(o + c) // self.vcm)
+        return (k0, max(k0, k1))
+
+    def tables(self, p: int) -> tuple:
+        """[t0, t1): the tables whose first data block is rank p's (it seals them)."""
+        k0, k1 = self.blocks(p)
+        return (-(-k0 // self.dbcm), -(-k1 // self.dbcm))
+
+    def head(self, p: int) -> tuple:
+        """(position, count): rank p's survivors inside a block an earlier rank owns."""
+        o, c = self.offsets[p], self.counts[p]
+        k0 = -(-o // self.vcm)
+        return (o, min(k0 * self.vcm, o + c) - o)
+
+    def block_owner(self, k: int) -> int:
+        pos = k * self.vcm
+        for p in range(len(self.counts)):
+            if self.counts[p] and self.offsets[p] <= pos < self.offsets[p] + self.counts[p]:
+                return p
+        raise ValueError(f"block {k} is outside the job's output")
+
+    def table_owner(self, t: int) -> int:
+        return self.block_owner(t * self.dbcm)
+
+    def entries(self, p: int) -> tuple:
+        """(table, first slot, count): index entries of rank p's blocks that
+        belong to a table an earlier rank owns (at most one table)."""
+        k0, k1 = self.blocks(p)
+        if k0 == k1 or k0 % self.dbcm == 0:
+            return (k0 // self.dbcm, k0 % self.dbcm, 0)
+        return (k0 // self.dbcm, k0 % self.dbcm, min(k1, (k0 // self.dbcm + 1) * self.dbcm) - k0)
+
+    def k_last(self, t: int) -> int:
+        return min((t + 1) * self.dbcm, self.data_blocks) - 1
 
     @property
     def head_max(self) -> int:
-        return max(self.need) if self.need else 0
+        return max((self.head(p)[1] for p in range(len(self.counts))), default=0)
 
-    def stream(self, rank: int) -> list:
-        """Rank `rank`'s phase-2 input as [(source rank, local start, count)]:
-        its own survivors from its first owned table on, then heads of the
-        following ranks up to the end of its last owned table."""
-        t0, t1 = self.tables[rank]
-        if t0 == t1:
-            return []
-        T = self.table_values
-        start, end = t0 * T, min(t1 * T, self.total)
-        out = []
-        for q in range(rank, len(self.offsets)):
-            o = self.offsets[q]
-            c = (self.offsets[q + 1] if q + 1 < len(self.offsets) else self.total) - o
-            a, b = max(start, o), min(end, o + c)
-            if a < b:
-                assert q == rank or (a == o and b - a <= self.need[q]), "stream exceeds the exchanged head"
-                out.append((q, a - o, b - a))
-            if o + c >= end:
-                break
-        return out
+    @property
+    def entries_max(self) -> int:
+        return max((self.entries(p)[2] for p in range(len(self.counts))), default=0)
 
 
-def plan_tables(counts: list, vcm: int, dbcm: int) -> TablePlan:
-    T = vcm * dbcm
+def plan_split(counts: list, vcm: int, dbcm: int) -> SplitPlan:
     offsets, o = [], 0
     for c in counts:
         offsets.append(o)
         o += int(c)
-    total = o
-    tables, need = [], []
-    for o_p, c in zip(offsets, counts):
-        tables.append((-(-o_p // T), -(-(o_p + c) // T)))
-        need.append(min(int(c), T - o_p % T) if c and o_p % T else 0)
-    return TablePlan(offsets, total, T, tables, need)
+    return SplitPlan([int(c) for c in counts], offsets, o, vcm, dbcm)
 
 
-def table_address_range(t0: int, t1: int, total: int, vcm: int, dbcm: int) -> tuple:
-    """Indices [lo, hi) of tables t0..t1-1 in the job's acquire-order address
-    list: each full table is dbcm data blocks then its index block."""
-    T = vcm * dbcm
-    lo = t0 * (dbcm + 1)
-    if t0 == t1:
-        return lo, lo
-    n = min(t1 * T, total) - t0 * T
-    db = -(-n // vcm)
-    return lo, lo + db + (t1 - t0)
+def entry_ranges(image: int, s0: int, e: int, dbcm: int, key_size: int) -> list:
+    """[(address, bytes)]: index entries [s0, s0 + e) of an index block image
+    (TableIndex layout, schema.zig:80-260): checksums (32 bytes each),
+    keys_min, keys_max, addresses — four contiguous pieces."""
+    ks = key_size
+    cks, kmin = HEADER_SIZE, HEADER_SIZE + 32 * dbcm
+    kmax, addr = kmin + ks * dbcm, kmin + 2 * ks * dbcm
+    return [(image + cks + 32 * s0, 32 * e), (image + kmin + ks * s0, ks * e), (image + kmax + ks * s0, ks * e),
+            (image + addr + 8 * s0, 8 * e)]
 
 
-def survivor_segments(out_ptr: int, count: int, vcm: int, dbcm: int, value_size: int, block_size: int) -> list:
-    """Device segments [(ptr, count)] of a compaction's survivors inside its
-    output arena (data block k in slot k + k // dbcm, values at +256)."""
-    segs = []
-    for k in range(-(-count // vcm)):
-        slot = k + k // dbcm
-        segs.append((out_ptr + slot * block_size + HEADER_SIZE, min(vcm, count - k * vcm)))
-    return segs
+def entry_bytes(key_size: int) -> int:
+    return 32 + 2 * key_size + 8
 
 
 # ---------------------------------------------------------------------------
@@ -334,11 +369,13 @@ class SingleRank:
 
 @dataclass
 class SplitResult:
-    tables: tuple          # (t0, t1): the job's output tables this rank wrote
-    result: object         # tbc_compaction_result of phase 2 (None if no tables)
+    blocks: tuple          # (k0, k1): the job's data blocks this rank finished
+    tables: tuple          # (t0, t1): the job's tables this rank sealed
+    result: object         # tbc_compaction_result of the sealing of those tables (None if none)
     table_infos: np.ndarray
-    blocks: object         # DeviceBuffer of the phase-2 output arena (None if no tables)
-    plan: TablePlan
+    arena: object          # DeviceBuffer: the job's output blocks (slot layout); this rank's are final
+    plan: SplitPlan
+    exchanged: dict        # bytes this rank sent per exchange: counts, heads, entries
 
 
 def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = False, scratch: dict | None = None,
@@ -347,21 +384,23 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     split_points). With staged=True the job's segments hold only this rank's
     range [cuts[rank], cuts[rank+1]) of A and of B (what rank_blocks named,
     staged on this GPU); otherwise the whole job's inputs, sliced here.
-    `scratch` (a dict kept by a caller that repeats the split) keeps the two
-    output arenas between calls; `before_phase2` runs after the exchange, just
-    before phase 2 is submitted (a caller enqueues its other work there)."""
+    `scratch` (a dict kept by a caller that repeats the split) keeps the
+    output arena between calls; `before_phase2` runs once the counts are
+    exchanged, just before the bodies are placed (a caller enqueues its other
+    work there)."""
+    from .abi import COMPACTION_COUNT_ONLY
     from .engine import Job
     tree, bs = job.tree, engine.block_size
-
-    def arena(name: str, nbytes: int):
-        if scratch is None:
-            return engine.alloc(nbytes)
-        buf = scratch.get(name)
-        if buf is None or buf.nbytes < nbytes:
-            buf = scratch[name] = engine.alloc(nbytes)
-        return buf
     lay = engine.layout(tree)
-    vcm, dbcm, vs = lay.block_value_count_max, lay.data_block_count_max, tree.value_size
+    vcm, dbcm, vs, ks = lay.block_value_count_max, lay.data_block_count_max, tree.value_size, tree.key_size
+    addrs = np.asarray(job.addresses, dtype=np.uint64)
+    nbytes = len(addrs) * bs
+    if scratch is None:
+        arena = engine.alloc(nbytes)
+    else:
+        arena = scratch.get("arena")
+        if arena is None or arena.nbytes < nbytes:
+            arena = scratch["arena"] = engine.alloc(nbytes)
 
     def sub(segs, lo, hi):
         return [(segs[s][0] + st * vs, n) for s, st, n in range_segments([n for _, n in segs], lo, hi)]
@@ -373,48 +412,76 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
             "staged segments are not this rank's range"
     else:
         seg_a, seg_b = sub(job.segments_a, a_lo, a_hi), sub(job.segments_b, b_lo, b_hi)
-    n = (a_hi - a_lo) + (b_hi - b_lo)
-    db = -(-n // vcm)
-    nblocks = db + -(-db // dbcm)
-    out1 = arena("phase1", max(1, nblocks) * bs)
-    p1 = Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
-             job.snapshot_min, np.arange(1, nblocks + 1, dtype=np.uint64), out1, flags=COMPACTION_VALUES_ONLY)
-    b1 = engine.submit([p1])
-    b1.wait()
-    r1, _ = b1.result(0)
-    b1.release()
-    if r1.status != 0:
-        raise RuntimeError(f"split phase 1 failed on rank {rank}: status {r1.status}")
-    mine = survivor_segments(out1.ptr, r1.value_count, vcm, dbcm, vs, bs)
 
-    plan = plan_tables(exchange.all_gather_counts(int(r1.value_count)), vcm, dbcm)
-    head = [(p, c * vs) for p, c in sub(mine, 0, plan.need[rank])]
-    keep, head_ptrs = exchange.all_gather_heads(engine, head, plan.head_max * vs)
+    def run(jobs):
+        b = engine.submit(jobs)
+        b.wait()
+        r, infos = b.result(0)
+        b.release()
+        if r.status != 0:
+            raise RuntimeError(f"split on rank {rank}: status {r.status}")
+        return r, infos
 
+    # Counts (the merge alone), then every rank's global output offset.
+    r0, _ = run([Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
+                     job.snapshot_min, addrs[:0], None, flags=COMPACTION_COUNT_ONLY)])
+    plan = plan_split(exchange.all_gather_counts(int(r0.value_count)), vcm, dbcm)
+    sent = {"counts": 8, "heads": 0, "entries": 0}
     if before_phase2 is not None:
         before_phase2()
-    t0, t1 = plan.tables[rank]
-    if t0 == t1:
-        return SplitResult((t0, t1), None, np.zeros((0, 128), dtype=np.uint8), None, plan)
-    seg2 = []
-    for q, st, cnt in plan.stream(rank):
-        if q == rank:
-            seg2 += sub(mine, st, st + cnt)
-        else:  # received head, in segments of at most one block's values
-            seg2 += [(head_ptrs[q] + (st + k) * vs, min(vcm, cnt - k)) for k in range(0, cnt, vcm)]
-    lo, hi = table_address_range(t0, t1, plan.total, vcm, dbcm)
-    addrs = np.asarray(job.addresses, dtype=np.uint64)[lo:hi]
-    if len(addrs) != hi - lo:
-        raise ValueError("address list shorter than the job's output")
-    out2 = arena("phase2", (hi - lo) * bs)
-    p2 = Job(tree, seg2, [], False, False, job.level_b, job.cluster, job.snapshot_min, addrs, out2)
-    b2 = engine.submit([p2])
-    b2.wait()
-    r2, infos = b2.result(0)
-    b2.release()
+    # Bodies at their global positions in the job's own block layout.
+    if plan.counts[rank]:
+        r1, _ = run([Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
+                         job.snapshot_min, addrs, arena, flags=VALUES_ONLY, output_offset=plan.offsets[rank])])
+        assert r1.value_count == plan.counts[rank]
+
+    def position_ptr(pos: int) -> int:
+        k = pos // vcm
+        return arena.ptr + data_block_slot(k, dbcm) * bs + HEADER_SIZE + (pos - k * vcm) * vs
+
+    # The partial block's values to its owner.
+    pos, h = plan.head(rank)
+    sent["heads"] = h * vs
+    keep, ptrs = exchange.all_gather_heads(engine, [(position_ptr(pos), h * vs)] if h else [], plan.head_max * vs)
+    copies = []
+    for q in range(len(plan.counts)):
+        qpos, qh = plan.head(q)
+        if q != rank and qh and plan.block_owner(qpos // vcm) == rank:
+            copies.append((position_ptr(qpos), ptrs[q], qh * vs))
+    if copies:
+        engine.copy_device_batch(copies)
+        engine.synchronize()  # the gathered buffers are released below
     del keep
-    if r2.status != 0 or r2.table_count != t1 - t0:
-        raise RuntimeError(f"split phase 2 failed on rank {rank}: status {r2.status}")
-    if scratch is None:
-        out1.free()
-    return SplitResult((t0, t1), r2, infos, out2, plan)
+    k0, k1 = plan.blocks(rank)
+    t0, t1 = plan.tables(rank)
+
+    def seal(blocks, tables):
+        return engine.seal(tree, job.cluster, job.snapshot_min, job.level_b, addrs, arena, plan.total, blocks, tables)
+
+    if k1 > k0:
+        seal((k0, k1), (t0, t0))
+    # The index entries of a table an earlier rank owns, to that owner.
+    t, s0, e = plan.entries(rank)
+    sent["entries"] = e * entry_bytes(ks)
+    mine = []
+    if e:
+        image = arena.ptr + index_block_slot(t, plan.k_last(t)) * bs
+        mine = entry_ranges(image, s0, e, dbcm, ks)
+    keep, ptrs = exchange.all_gather_heads(engine, mine, plan.entries_max * entry_bytes(ks))
+    copies = []
+    for q in range(len(plan.counts)):
+        qt, qs0, qe = plan.entries(q)
+        if q != rank and qe and plan.table_owner(qt) == rank:
+            image = arena.ptr + index_block_slot(qt, plan.k_last(qt)) * bs
+            off = 0
+            for dst, n in entry_ranges(image, qs0, qe, dbcm, ks):
+                copies.append((dst, ptrs[q] + off, n))
+                off += n
+    if copies:
+        engine.copy_device_batch(copies)
+        engine.synchronize()
+    del keep
+    result, infos = None, np.zeros((0, 128), dtype=np.uint8)
+    if t1 > t0:
+        result, infos = seal((k0, k0), (t0, t1))
+    return SplitResult((k0, k1), (t0, t1), result, infos, arena, plan, sent)

@@ -8,7 +8,7 @@ O=gpurun_out/r04${TAG:-}
 mkdir -p $O
 fatal() { [ "$1" -ge 124 ]; }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_overlap.py tests/test_gpu_unique.py tests/test_gpu_engine.py tests/test_manifest.py -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests_new.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_overlap.py tests/test_gpu_unique.py tests/test_gpu_engine.py tests/test_manifest.py -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests_new.log 2>&1
   rc=$?; tail -2 $O/tests_new.log
   if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)|Error|assert" $O/tests_new.log | head -20; exit $rc; fi
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests_all.log 2>&1
