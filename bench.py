@@ -260,6 +260,10 @@ class ReplayWorkload:
                 jobs, landings = rest
                 eng.copy_device_batch(landings)
                 eng.sort_values_batch(jobs)
+            elif kind == "checkpoint":  # the replica checkpoints with no grid IO in flight
+                eng.synchronize()
+            elif kind == "restart":
+                raise RuntimeError("a benchmark replay never restarts")
             elif kind == "manifest":  # ManifestLog.close_block on the device (manifest.py)
                 images, addresses, prev = rest
                 manifest.close_on_grid(self.grid, images, addresses, prev, None if prev else 0)

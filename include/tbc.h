@@ -247,6 +247,10 @@ tbc_status tbc_engine_arena_usage(const tbc_engine *engine, uint64_t *out_device
 /* ---- grid ------------------------------------------------------------------- */
 tbc_status tbc_grid_init(tbc_engine *engine, uint64_t block_count, tbc_grid **out_grid);
 void tbc_grid_deinit(tbc_grid *grid);
+/* A replica restart (superblock open from a checkpoint): the grid's cache is
+ * cold, so every block is untrusted until a batch that reads it validates it
+ * in full (read_block_validate). Enqueued after every running batch tail. */
+tbc_status tbc_grid_invalidate(tbc_grid *grid);
 /* Device pointer of the block at `address` (1 <= address <= block_count). */
 tbc_status tbc_grid_block_pointer(const tbc_grid *grid, uint64_t address, void **out_ptr);
 /* grid.read_block from storage: stage `count` host block images (block_size

@@ -44,6 +44,9 @@ class OracleManifestStore:
     def read(self, address):
         return self.grid[int(address)]
 
+    def checksum(self, address):
+        return self.checksums[int(address)]
+
 
 class LockstepManifestStore:
     """Every manifest block closed on the GPU grid and by the oracle; reads
@@ -56,6 +59,14 @@ class LockstepManifestStore:
     def close(self, infos, address, previous_address):
         self.gpu.close(infos, address, previous_address)
         self.ref.close(infos, address, previous_address)
+
+    def checksum(self, address):
+        got, want = self.gpu.checksum(address), self.ref.checksum(address)
+        assert got == want, f"manifest block {address} checksum"
+        return got
+
+    def restore_link(self, address, checksum):
+        self.gpu.restore_link(address, checksum)
 
     def read(self, address):
         got = self.gpu.read(address)
@@ -117,6 +128,9 @@ class OracleExecutor:
 
     def flushed(self, name):
         pass
+
+    def restart(self):
+        self.mutable, self.immutable = {}, {}
 
     def table_segments(self, info: TableInfo, spec) -> list:
         """A table's data blocks' values, found through its index block
@@ -187,6 +201,13 @@ class LockstepExecutor:
 
     def flushed(self, name):
         self.gpu.flushed(name)
+
+    def checkpoint(self):
+        self.gpu.checkpoint()
+
+    def restart(self):
+        self.gpu.restart()
+        self.ref.restart()
 
     def submit(self, jobs, cluster):
         return (self.gpu.submit(jobs, cluster), self.ref.submit(jobs, cluster), [name for name, _ in jobs])

@@ -202,6 +202,7 @@ _SIGNATURES = {
     "tbc_grid_deinit": (None, [_P]),
     "tbc_grid_block_pointer": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
     "tbc_grid_put_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
+    "tbc_grid_invalidate": (ctypes.c_int, [_P]),
     "tbc_grid_get_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
     "tbc_manifest_close_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P),
                                                  ctypes.c_uint32, ctypes.c_uint64, _P]),

@@ -368,6 +368,7 @@ struct tbc_batch {
     // the whole job's shape, which its kernels need).
     bool seal = false;
     tbc_compaction_result seal_result{};
+    bool count_only = false; // TBC_COMPACTION_COUNT_ONLY: value_count only
 };
 
 struct tbc_kway {
@@ -599,6 +600,14 @@ void tbc_grid_deinit(tbc_grid *g) {
     hipFree(g->verified);
     hipFree(g->base);
     delete g;
+}
+
+tbc_status tbc_grid_invalidate(tbc_grid *g) {
+    if (!g) return TBC_ERR_INVALID_ARGUMENT;
+    tbc_engine *e = g->engine;
+    hipSetDevice(e->device);
+    if (!join_tails(e)) return TBC_ERR_DEVICE; // no running batch marks a block after this
+    return hipMemsetAsync(g->verified, 0, g->block_count, e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_grid_block_pointer(const tbc_grid *g, uint64_t address, void **out) {
@@ -1778,6 +1787,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         }
     } else if (flags0 & TBC_COMPACTION_COUNT_ONLY) {
         // The merge alone: survivor counts (k_tile_scan's results), nothing written.
+        b->count_only = true;
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
                               d_block_tile, d_order, d_res, s, mark_cb, b, nullptr, d_ticket, d_ready) == 0;
@@ -2209,10 +2219,11 @@ tbc_status tbc_batch_result(tbc_batch *b, uint32_t index, tbc_compaction_result 
         *out = b->seal_result;
         out->status = r.status;
     }
+    if (b->count_only) out->data_block_count = out->table_count = out->block_count = 0; // nothing written
     if (table_infos) {
-        if (table_info_capacity < r.table_count) return TBC_ERR_CAPACITY;
+        if (table_info_capacity < out->table_count) return TBC_ERR_CAPACITY;
         memcpy(table_infos, b->h_infos + (size_t)b->info_base[index] * kTableInfoSize,
-               (size_t)r.table_count * kTableInfoSize);
+               (size_t)out->table_count * kTableInfoSize);
     }
     return TBC_OK;
 }

@@ -168,6 +168,10 @@ class Grid:
               "tbc_grid_get_blocks")
         return out[:n]
 
+    def invalidate(self) -> None:
+        """tbc_grid_invalidate: a restart's cold cache (every block validated before use)."""
+        check(lib().tbc_grid_invalidate(self.handle), "tbc_grid_invalidate")
+
     def close(self) -> None:
         if self.handle:
             lib().tbc_grid_deinit(self.handle)

@@ -11,13 +11,22 @@ config 1: `tigerbeetle benchmark`'s load, benchmark_load.py) this module
 restates that host logic; the compactions themselves run on an `executor`
 (the GPU grid executor below, or the oracle in tests).
 
-Simplifications, stated in DESIGN.md §10: blocks released by compactions
-go to the FreeSet's staging and are only reusable after a checkpoint
-(free_set.zig:383-390); a replay never checkpoints, so they are never
-reused. The manifest log's own block reservations are not simulated
-(manifest_log.zig:647-684), so addresses differ from a replica's by those
-blocks; every address a compaction uses is still a FreeSet acquire from its
-own reservation.
+Blocks released by compactions (their input tables' data and index
+blocks, compaction.zig:571-583) and by the manifest log's compaction
+(manifest_log.zig:792) go to the FreeSet's staging and become free at the
+next checkpoint (free_set.zig:383-390, 434-447), which the replica takes
+after the bar of its trigger op (replica.zig:3470-3501, vsr.zig
+Checkpoint: every vsr_checkpoint_interval ops). A restart from a checkpoint
+(`Forest.restart`) restores the checkpointed manifest, free set and log,
+forgets the grid's trusted blocks (a cold cache: every block is validated
+before use), and replays the ops after the checkpoint with their memtable
+puts while skipping the compactions the checkpoint already holds
+(Tree.compact, tree.zig:627-646; superblock op_compacted).
+
+Simplifications, stated in DESIGN.md §10: the blocks of the checkpoint's
+own encoded free set and client replies are not simulated, so addresses
+differ from a replica's by those blocks; every address a compaction uses is
+still a FreeSet acquire from its own reservation.
 """
 from __future__ import annotations
 
@@ -32,6 +41,20 @@ LSM_LEVELS = trees.LSM_LEVELS            # config.zig:140
 GROWTH = trees.LSM_GROWTH_FACTOR         # config.zig:141
 BAR = trees.LSM_BATCH_MULTIPLE           # config.zig:142
 HALF = BAR // 2
+# constants.zig:47-49 with the production config (config.zig:133-142): 1024
+# journal slots - 32 - 32 * ceil(8 / 32) = 960 ops between checkpoints.
+VSR_CHECKPOINT_INTERVAL = 1024 - BAR - BAR * -(-8 // BAR)
+
+
+def checkpoint_after(checkpoint: int, interval: int = VSR_CHECKPOINT_INTERVAL) -> int:
+    """vsr.Checkpoint.checkpoint_after (vsr.zig:1343-1361)."""
+    return interval - 1 if checkpoint == 0 else checkpoint + interval
+
+
+def trigger_for_checkpoint(checkpoint: int) -> int:
+    """vsr.Checkpoint.trigger_for_checkpoint (vsr.zig:1364-1371): the op whose
+    compaction completes the checkpoint's bar."""
+    return checkpoint + BAR
 
 
 def table_count_max_for_level(level: int) -> int:
@@ -59,9 +82,11 @@ class FreeSet:
 
     def __init__(self, block_count: int):
         self.acquired = np.zeros(block_count, dtype=bool)
+        self.staging = np.zeros(block_count, dtype=bool)  # released, free at the next checkpoint
         self.reservation_blocks = 0
         self.reservation_count = 0
         self.released = 0
+        self.reused = 0  # acquires of addresses freed by a checkpoint
 
     def reserve(self, count: int) -> tuple:
         base = self.reservation_blocks
@@ -82,6 +107,10 @@ class FreeSet:
         a = np.asarray(addresses, dtype=np.int64)
         assert not self.acquired[a - 1].any()
         self.acquired[a - 1] = True
+        if self.freed is not None:
+            self.reused += int(self.freed[a - 1].sum())
+
+    freed = None  # blocks a checkpoint freed (statistics: reuse)
 
     def acquire_from(self, reservation: tuple) -> int:
         """FreeSet.acquire(reservation) (free_set.zig:280-311): the first free
@@ -95,9 +124,28 @@ class FreeSet:
 
     def release(self, address: int) -> None:
         """FreeSet.release (free_set.zig:383-390): staged until the next
-        checkpoint, which a replay never reaches, so never reused."""
-        assert self.acquired[address - 1]
+        checkpoint; still acquired until then (no reservation may reuse it)."""
+        assert self.acquired[address - 1] and not self.staging[address - 1]
+        self.staging[address - 1] = True
         self.released += 1
+
+    def checkpoint(self) -> int:
+        """FreeSet.checkpoint (free_set.zig:434-447): every staged block is
+        freed; no reservation may be outstanding. Returns the count."""
+        assert self.reservation_count == 0 and self.reservation_blocks == 0
+        n = int(self.staging.sum())
+        self.freed = self.staging.copy() if self.freed is None else (self.freed | self.staging)
+        self.acquired &= ~self.staging
+        self.staging[:] = False
+        return n
+
+    def snapshot(self) -> dict:
+        assert self.reservation_count == 0
+        return {"acquired": self.acquired.copy(), "staging": self.staging.copy()}
+
+    def restore(self, snap: dict) -> None:
+        self.acquired, self.staging = snap["acquired"].copy(), snap["staging"].copy()
+        self.reservation_blocks = self.reservation_count = 0
 
     def forfeit(self) -> None:
         self.reservation_count -= 1
@@ -331,10 +379,18 @@ class Forest:
              "transfers.user_data_32", "transfers.timeout", "transfers.ledger", "transfers.code"]
 
     def __init__(self, executor, block_count: int, cluster: int = 0, manifest_log: bool = True,
-                 block_size: int = 1 << 20):
+                 block_size: int = 1 << 20, checkpoint_interval: int | None = VSR_CHECKPOINT_INTERVAL):
         from .manifest import ManifestLog
         self.executor = executor
+        self.block_size = block_size
         self.free_set = FreeSet(block_count)
+        # Checkpoints (replica.zig:3470-3501): after the bar of each trigger op.
+        self.checkpoint_interval = checkpoint_interval
+        self.op_checkpoint = 0
+        self.checkpoints: list = []       # (checkpoint op, trigger op, blocks freed)
+        self._snapshot = None             # host state at the last checkpoint (restart)
+        self.op_compacted_max = 0         # after a restart: ops <= this skip compaction (op_compacted)
+        self.table_blocks: dict = {}      # index block address -> the table's block addresses
         self.trees = {name: Tree(trees.BY_NAME[name]) for name in self.ORDER}
         self.cluster = cluster
         self.pending = None       # (batch handle, [Compaction]) of the running half-bar
@@ -354,13 +410,17 @@ class Forest:
     def compact(self, op: int) -> None:
         """Forest.compact(op) (forest.zig:319-342) then compact_end."""
         beat = op % BAR
+        skipped = op <= self.op_compacted_max  # recovered: the checkpoint holds this op's compaction
         if op >= BAR and beat in (0, HALF):
             started = []
             for name in self.ORDER:
+                if skipped:
+                    self.trees[name].compactions = []
+                    continue
                 for c in self.trees[name].start_half_bar(op, self.free_set):
                     started.append((name, c))
             if self.manifest_log is not None:  # after the grooves (forest.zig:323-331)
-                self.manifest_log.compact(op)
+                self.manifest_log.compact(op, skipped=skipped)
             jobs = [(name, c) for name, c in started if not c.move]
             handle = self.executor.submit(jobs, self.cluster) if jobs else None
             self.pending = (handle, started)
@@ -372,6 +432,7 @@ class Forest:
             for name, c in started:  # the blocks each compaction wrote
                 if not c.move:
                     self.free_set.acquire(c.addresses[:c.result.block_count])
+                    self.record_blocks(c)
             # Grooves' compact_end in forest order, each tree's immutable
             # compaction first, then its level compactions (tree.zig:876-953).
             log = self.manifest_log
@@ -400,6 +461,79 @@ class Forest:
             # TableMemory.sort skips a table whose puts arrived in key order
             # (table_memory.zig:110-150): only the others are sorted.
             self.executor.swap([name for name in swapped if not self.trees[name].immutable_sorted])
+            if self.checkpoint_interval and op == trigger_for_checkpoint(
+                    checkpoint_after(self.op_checkpoint, self.checkpoint_interval)):
+                self.checkpoint(checkpoint_after(self.op_checkpoint, self.checkpoint_interval), op)
+
+    def record_blocks(self, c: Compaction) -> None:
+        """The output tables' blocks (data blocks then the index block per
+        table, in acquire order: compaction.zig:806-886), and the input
+        tables' blocks released (release_table_blocks, compaction.zig:571-583:
+        staged until the next checkpoint)."""
+        dbcm = c.tree.layout(self.block_size)["data_block_count_max"]
+        db = c.result.data_block_count
+        for t, info in enumerate(c.outputs):
+            k0, k_last = t * dbcm, min((t + 1) * dbcm, db) - 1
+            slots = [k + k // dbcm for k in range(k0, k_last + 1)] + [k_last + t + 1]
+            blocks = [int(c.addresses[s]) for s in slots]
+            assert blocks[-1] == info.address
+            self.table_blocks[info.address] = blocks
+        for t in ([c.table_a] if c.table_a is not None else []) + list(c.range_b[2]):
+            for address in self.table_blocks.pop(t.address):
+                self.free_set.release(address)
+
+    def checkpoint(self, op_checkpoint: int, trigger: int) -> None:
+        """The replica's checkpoint after its trigger op's bar (replica.zig
+        commit_op_compact_callback -> checkpoint_data; forest.zig:422-445):
+        the manifest log closes its partial block (manifest_log.zig:767-781),
+        the free set frees every staged block (free_set.zig:434-447), and the
+        host state is what a restart recovers."""
+        if self.manifest_log is not None:
+            self.manifest_log.checkpoint()
+        freed = self.free_set.checkpoint()
+        if hasattr(self.executor, "checkpoint"):
+            self.executor.checkpoint()
+        self.op_checkpoint = op_checkpoint
+        self.checkpoints.append((op_checkpoint, trigger, freed))
+        self._snapshot = self.snapshot()
+
+    def snapshot(self) -> dict:
+        """What the checkpoint persists: the manifest (every tree's levels),
+        the free set, the manifest log, the tables' block lists."""
+        import copy
+        log = self.manifest_log
+        return {
+            "levels": {name: copy.deepcopy(t.levels) for name, t in self.trees.items()},
+            "free_set": self.free_set.snapshot(),
+            "log": None if log is None else log.snapshot(),
+            "table_blocks": {a: list(b) for a, b in self.table_blocks.items()},
+            "op_checkpoint": self.op_checkpoint,
+        }
+
+    def restart(self) -> int:
+        """Crash and recover from the last checkpoint (replica open ->
+        superblock, manifest log open, free set decode): the host state is the
+        checkpoint's, memtables are empty, the grid's cache is cold (the
+        executor forgets every trusted block), and the ops after the
+        checkpoint are replayed with their compactions skipped up to the
+        trigger op (tree.zig:627-646). Returns the first op to replay."""
+        import copy
+        snap = self._snapshot
+        assert snap is not None, "no checkpoint to restart from"
+        for name, t in self.trees.items():
+            fresh = Tree(t.spec)
+            fresh.levels = copy.deepcopy(snap["levels"][name])
+            self.trees[name] = fresh
+        self.free_set.restore(snap["free_set"])
+        if self.manifest_log is not None:
+            self.manifest_log.restore(snap["log"])
+        self.table_blocks = {a: list(b) for a, b in snap["table_blocks"].items()}
+        self.op_checkpoint = snap["op_checkpoint"]
+        self.op_compacted_max = trigger_for_checkpoint(self.op_checkpoint)
+        self.pending = None
+        if hasattr(self.executor, "restart"):
+            self.executor.restart()
+        return self.op_checkpoint + 1
 
     def checkpoint_manifest(self) -> None:
         """ManifestLog.checkpoint (manifest_log.zig:767-781) at the end of a
@@ -407,9 +541,15 @@ class Forest:
         if self.manifest_log is not None:
             self.manifest_log.checkpoint()
 
-    def run(self, load_ops, progress=None) -> None:
-        """Commit every op of a workload: its puts, then Forest.compact(op)."""
+    def run(self, load_ops, progress=None, start: int = 1, stop: int | None = None) -> None:
+        """Commit every op of a workload: its puts, then Forest.compact(op);
+        ops before `start` (already committed: a restart replays from the
+        checkpoint) and after `stop` (a crash) are not committed."""
         for op in load_ops:
+            if op.op < start:
+                continue
+            if stop is not None and op.op > stop:
+                break
             for name, values in op.puts.items():
                 self.put(name, values)
             self.compact(op.op)
@@ -496,6 +636,21 @@ class GridExecutor:
 
     def flushed(self, name: str) -> None:
         pass  # the immutable memtable is reset when it becomes mutable again (swap)
+
+    def checkpoint(self) -> None:
+        """The replica checkpoints with no grid IO in flight
+        (grid.assert_only_repairing): a replay of the record waits here."""
+        if self.recording:
+            self.record.append(("checkpoint",))
+
+    def restart(self) -> None:
+        """A restart: memtables empty, the grid's cache cold."""
+        for name in list(self.mutable):
+            self.mutable[name].reset()
+            self.immutable[name].reset()
+        self.grid.invalidate()
+        if self.recording:
+            self.record.append(("restart",))
 
     def submit(self, jobs: list, cluster: int):
         from . import abi

@@ -235,12 +235,14 @@ class ManifestLog:
         into the grid, so a flush only retires them from the buffer."""
         self.blocks_closed = 0
 
-    def compact(self, op: int) -> None:
+    def compact(self, op: int, skipped: bool = False) -> None:
         """:571-614 then compact_next_block / compact_read_block_callback
-        (:628-718): at a half-bar start, after the trees' reservations."""
+        (:628-718): at a half-bar start, after the trees' reservations.
+        `skipped`: an op the recovered checkpoint already compacted
+        (op_compacted, :659-665)."""
         assert self.reservation is None and self.compact_blocks is None
         assert op % (LSM_BATCH_MULTIPLE // 2) == 0
-        if op < LSM_BATCH_MULTIPLE:
+        if op < LSM_BATCH_MULTIPLE or skipped:
             return
         compact_blocks = min(self.pace.half_bar_compact_blocks(len(self.log_addresses), len(self.table_extents)),
                              len(self.log_addresses) - self.blocks_closed)
@@ -279,6 +281,25 @@ class ManifestLog:
         if self.open_entries:
             self.close_block()
         self.flush()
+
+    def snapshot(self) -> dict:
+        """The log's state a checkpoint persists (checkpoint_references plus
+        the table extents open() rebuilds, :783-809)."""
+        assert not self.open_entries and self.reservation is None
+        newest = self.log_addresses[-1] if self.log_addresses else 0
+        return {"log_addresses": list(self.log_addresses), "table_extents": dict(self.table_extents),
+                "newest": (newest, self.store.checksum(newest) if newest and hasattr(self.store, "checksum") else 0)}
+
+    def restore(self, snap: dict) -> None:
+        """ManifestLog.open from the checkpoint's references: the log's
+        blocks and the table extents (the blocks themselves stay in the grid)."""
+        self.log_addresses = deque(snap["log_addresses"])
+        self.table_extents = dict(snap["table_extents"])
+        newest, checksum = snap["newest"]
+        if newest and hasattr(self.store, "restore_link"):
+            self.store.restore_link(newest, checksum)
+        self.open_entries, self.open_address, self.blocks_closed = [], 0, 0
+        self.reservation, self.compact_blocks = None, None
 
     def references(self) -> tuple:
         """(oldest address, newest address, block count) of the log
@@ -346,11 +367,25 @@ class GridManifestStore:
         self.block_size = grid.engine.block_size
         self.record = record
         self.closed: list = []
+        self.links: dict = {}  # address -> header checksum the host knows (a recovered log's newest block)
+
+    def checksum(self, address: int) -> int:
+        """A closed block's header checksum (what the checkpoint's
+        references record for the log's newest block, manifest_log.zig:783-809)."""
+        blk = self.grid.get_blocks([address])[0]
+        return int.from_bytes(blk[:16].tobytes(), "little")
+
+    def restore_link(self, address: int, checksum: int) -> None:
+        """After a restart the grid's cache is cold: the next block links the
+        newest block by the checksum recovered with the log, not by reading a
+        trusted grid block."""
+        self.links[int(address)] = int(checksum)
 
     def close(self, infos: np.ndarray, address: int, previous_address: int) -> None:
         images = pack_blocks(infos, [address], self.cluster, self.block_size, previous_address)
         assert len(images) == 1
-        close_on_grid(self.grid, images, [address], previous_address, None if previous_address else 0)
+        prev = self.links.pop(int(previous_address), None) if previous_address else 0
+        close_on_grid(self.grid, images, [address], previous_address, prev)
         if self.record is not None:
             self.record.append(("manifest", images, [address], previous_address))
         self.closed.append(address)
