@@ -281,3 +281,60 @@ def test_memtable_put_capacity_and_reset(engine):
         assert m.values()[1] == 0
     finally:
         m.close()
+
+
+def test_grid_unique_keys_held_and_broken(engine, oracle_lib):
+    """Grid batches with TBC_COMPACTION_UNIQUE_KEYS jobs (round 4): their bodies
+    are merged tile by tile straight into the grid (k_merge_unique) beside a
+    mask-merged job; a job whose keys repeat (an A key also in B) breaks its
+    speculation and is recomputed by the merge path in the same front. Every
+    block and TableInfo equals the oracle's; tbc_batch_speculation says which."""
+    rng = np.random.default_rng(0x0A1B)
+    grid = Grid(engine, 700)
+    spec_id = trees.BY_NAME["transfers.id"]
+    spec_ts = trees.BY_NAME["transfers.timestamp"]
+    spec_acc = trees.BY_NAME["accounts.timestamp"]
+    try:
+        uni = sorted_unique(spec_id, 200_000, rng)
+        part = rng.integers(0, 3, size=len(uni))
+        b_vals, a_vals, c_vals = uni[part == 0], uni[part == 1], uni[part == 2]
+        blk_b, ti_b = storage_table(oracle_lib, spec_id, b_vals, np.arange(1, 20, dtype=np.uint64), level=1)
+        blk_a, ti_a = storage_table(oracle_lib, spec_id, a_vals, np.arange(20, 40, dtype=np.uint64), level=0)
+        # broken: C's table repeats 50 keys of B's
+        c_rep = np.concatenate([c_vals, b_vals[rng.choice(len(b_vals), 50, replace=False)]])
+        c_rep = c_rep[np.lexsort(workloads.keys_of(c_rep, spec_id))]  # most significant limb last
+        blk_c, ti_c = storage_table(oracle_lib, spec_id, c_rep, np.arange(40, 60, dtype=np.uint64), level=0)
+        ts_b = sorted_unique(spec_ts, 60_000, rng)
+        blk_t, ti_t = storage_table(oracle_lib, spec_ts, ts_b, np.arange(60, 80, dtype=np.uint64), level=1)
+        ts_a = sorted_unique(spec_ts, 30_000, rng)
+        mem_ts = engine.upload(ts_a)
+        acc_b = sorted_unique(spec_acc, 20_000, rng)
+        blk_acc, ti_acc = storage_table(oracle_lib, spec_acc, acc_b, np.arange(80, 100, dtype=np.uint64), level=2)
+        acc_keys = [np.sort(workloads.keys_of(acc_b, spec_acc)[0][rng.choice(20_000, 5_000, replace=False)])]
+        acc_a = workloads.values_from_keys(spec_acc, acc_keys, np.zeros(5_000, bool), rng)
+        mem_acc = engine.upload(acc_a)
+        for blocks, base in ((blk_b, 1), (blk_a, 20), (blk_c, 40), (blk_t, 60), (blk_acc, 80)):
+            grid.put_blocks(np.arange(base, base + len(blocks), dtype=np.uint64), np.stack(blocks))
+        U, G = abi.COMPACTION_UNIQUE_KEYS, abi.COMPACTION_GRID
+        adr = [np.arange(b, b + n, dtype=np.uint64) for b, n in ((200, 27), (300, 27), (400, 18), (500, 130))]
+        jobs = [Job(spec_id, [], [], False, False, 1, CLUSTER, 48, adr[0], None, flags=G | U, grid=grid,
+                    tables_a=[ti_a.ref()], tables_b=[ti_b.ref()]),                      # held
+                Job(spec_id, [], [], False, False, 1, CLUSTER, 48, adr[1], None, flags=G | U, grid=grid,
+                    tables_a=[ti_c.ref()], tables_b=[ti_b.ref()]),                      # broken
+                Job(spec_ts, [(mem_ts.ptr, len(ts_a))], [], True, False, 1, CLUSTER, 48, adr[2], None,
+                    flags=G | U, grid=grid, tables_b=[ti_t.ref()]),                     # held, immutable A
+                Job(spec_acc, [(mem_acc.ptr, len(acc_a))], [], True, True, 2, CLUSTER, 48, adr[3], None,
+                    flags=G, grid=grid, tables_b=[ti_acc.ref()])]                       # mask merge
+        b = engine.submit(jobs)
+        b.wait()
+        res = [b.result(i) for i in range(4)]
+        spec_out = [b.speculation(i) for i in range(4)]
+        b.release()
+        assert spec_out == [abi.SPECULATION_HELD, abi.SPECULATION_BROKEN, abi.SPECULATION_HELD,
+                            abi.SPECULATION_NONE]
+        check_job(oracle_lib, grid, spec_id, *res[0], a_vals, False, [b_vals], False, 1, 48, adr[0])
+        check_job(oracle_lib, grid, spec_id, *res[1], c_rep, False, [b_vals], False, 1, 48, adr[1])
+        check_job(oracle_lib, grid, spec_ts, *res[2], ts_a, True, [ts_b], False, 1, 48, adr[2])
+        check_job(oracle_lib, grid, spec_acc, *res[3], acc_a, True, [acc_b], True, 2, 48, adr[3])
+    finally:
+        grid.close()

@@ -1550,15 +1550,18 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
-        d.unique = spec_regime && !no_spec && (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) &&
-                   d.dblock_max > 0;
+        // Grid batches (pipelined fronts) merge speculated jobs tile by tile
+        // (k_merge_unique): bodies written once, R + W instead of the mask
+        // merge + assembly's R + 2 W.
+        d.unique = (spec_regime || (grid_mode && !staged)) && !no_spec &&
+                   (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) && d.dblock_max > 0;
         any_unique |= d.unique != 0;
     }
     // Pipelined: the speculated jobs' tiles of kUniqueTile positions and
     // their merge-path splits (merge.hip k_merge_unique). TBC_PIPE_PRODUCERS=1
     // (A/B measurement only) merges them by one producer wave per block instead.
     static const bool pipe_producers = getenv("TBC_PIPE_PRODUCERS") != nullptr;
-    const bool unique_tiles = spec_pipe && any_unique && !pipe_producers;
+    const bool unique_tiles = any_unique && ((spec_pipe && !pipe_producers) || grid_mode);
     uint32_t utiles = 0, usplits = 0;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
@@ -1722,12 +1725,26 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && !resolve.empty())
             ok = launch_grid_resolve(d_resolve, (uint32_t)resolve.size(), (uint64_t *)(uintptr_t)dev_seg, d_checks,
                                      grid0->base, grid0->block_count, e->block_size, d_res, s) == 0;
+        // Speculated jobs (UNIQUE_KEYS) merged tile by tile straight into
+        // their blocks; the others by the mask merge and k_assemble; broken
+        // speculations recomputed by the merge path (phase 1) before the
+        // index block layout reads the final shapes.
+        if (ok && unique_tiles)
+            ok = launch_merge_unique((const JobDesc *)d_in, sj.data(), (int)count, d_usplits, d_res, s, mark_cb, b) == 0;
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
                               d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
+        if (ok && any_unique)
+            ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
+                              d_block_tile, d_order, d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
+        if (ok && any_unique) {
+            ok = launch_assemble((const JobDesc *)d_in, (int)count, tiles, d_ready, d_res, d_status, e->masks,
+                                 d_splits, 1, s) == 0;
+            mark_cb(b, "recompute_assemble");
+        }
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];

@@ -557,6 +557,17 @@ class Forest:
                 progress(op.op)
 
 
+def unique_keys(name: str) -> bool:
+    """Trees whose keys are never put twice in the benchmark's state machine
+    (TBC_COMPACTION_UNIQUE_KEYS): transfers are immutable (every transfer
+    tree's key holds the transfer's unique timestamp or id), and an account's
+    id and indexed fields never change after creation (state_machine.zig
+    create_account; balance updates re-put only the accounts object tree,
+    groove.zig:911-1006). The engine verifies it on the device and recomputes
+    a compaction whose speculation breaks."""
+    return name != "accounts.timestamp"
+
+
 def key_summary(values: np.ndarray, spec: trees.TreeSpec) -> tuple:
     """(first key, min key, max key, keys non-decreasing) of a put batch,
     keys as integers (key_from_value: composite_key.zig:48-50, groove.zig)."""
@@ -662,8 +673,9 @@ class GridExecutor:
                 segs_a, tables_a = [(ptr, n)], []
             else:
                 segs_a, tables_a = [], [c.table_a.ref()]
+            flags = abi.COMPACTION_GRID | (abi.COMPACTION_UNIQUE_KEYS if unique_keys(name) else 0)
             js.append(Job(c.tree, segs_a, [], c.table_a is None, c.drop_tombstones, c.level_b, cluster,
-                          c.snapshot_min, c.addresses, None, flags=abi.COMPACTION_GRID, grid=self.grid,
+                          c.snapshot_min, c.addresses, None, flags=flags, grid=self.grid,
                           tables_a=tables_a, tables_b=[t.ref() for t in c.range_b[2]]))
         if self.recording:
             self.record.append(("batch", js))
