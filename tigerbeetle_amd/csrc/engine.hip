@@ -1431,7 +1431,11 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         const uint64_t n = na + nb;
         const uint64_t db_max = (n + L.vcm - 1) / L.vcm;
         const uint64_t tables_max = (db_max + L.dbcm - 1) / L.dbcm;
-        if (!count_only && db_max + tables_max > c.address_count) { delete b; return TBC_ERR_CAPACITY; }
+        // (An offset range writes only its data blocks' slots: checked below.)
+        if (!count_only && !c.output_offset && db_max + tables_max > c.address_count) {
+            delete b;
+            return TBC_ERR_CAPACITY;
+        }
         if (c.output_offset && n) { // the job's slot of the last global data block this range writes
             const uint64_t k_last = (c.output_offset + n - 1) / L.vcm;
             if (k_last + k_last / L.dbcm + 1 > c.address_count) { delete b; return TBC_ERR_CAPACITY; }
