@@ -52,9 +52,10 @@ def main() -> None:
     shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
     # Instantiations of one kernel share a short name: keep the heaviest.
-    avg_ns, tot_ns = {}, {}
+    avg_ns, tot_ns, calls = {}, {}, {}
     for r in csv.DictReader(open(stats)):
         k = short(r["Name"])
+        calls[k] = calls.get(k, 0) + int(r["Calls"])  # every instantiation's launches
         if float(r["TotalDurationNs"]) > tot_ns.get(k, -1.0):
             avg_ns[k], tot_ns[k] = float(r["AverageNs"]), float(r["TotalDurationNs"])
     fetch = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
@@ -75,7 +76,7 @@ def main() -> None:
     for k in sorted(avg_ns):
         f = fetch.get(k, 0.0) * 1024 * 2
         w = write.get(k, 0.0) * 1024
-        out["kernels"][k] = {"avg_ns": avg_ns[k], "fetch_bytes": round(f), "write_bytes": round(w),
+        out["kernels"][k] = {"avg_ns": avg_ns[k], "calls": calls[k], "fetch_bytes": round(f), "write_bytes": round(w),
                              "traffic_bytes": round(f + w),
                              "traffic_gbs": round((f + w) / avg_ns[k], 1) if avg_ns[k] else None}
         if k in sq:
