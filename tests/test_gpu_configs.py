@@ -31,22 +31,30 @@ def _oracle_job(oracle_lib, js, bs, addrs):
 # their device sorts, a whole forest unit of config 4, and config 5's 27 jobs
 # (13,824 output blocks: the throughput regime — 4 pipelined job groups,
 # k_assemble, chain-only k_data_blocks over 1 MiB bodies).
+# Configs 2-4 also through the pipelined block pass (TBC_CONFIG_PIPELINE: what
+# bench.py's steps in flight take): speculated jobs merged by k_merge_unique,
+# chains packed on a tail stream.
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("config", [2, 3, 4, 5])
-def test_full_size_jobs_bit_exact(oracle_lib, config):
+@pytest.mark.parametrize("config,mode", [(2, "fused"), (2, "pipelined"), (3, "fused"), (3, "pipelined"),
+                                         (4, "fused"), (4, "pipelined"), (5, "auto")])
+def test_full_size_jobs_bit_exact(oracle_lib, config, mode):
     import bench
     from tigerbeetle_amd import Engine, abi
     bs = 1 << 20
     job_ids = list(range(configs.DEFAULT_JOBS[config]))
-    with Engine(device=0, block_size=bs, arena_bytes=2 << 30, profile=True) as eng:
+    pipeline = {"fused": False, "pipelined": True, "auto": None}[mode]
+    with Engine(device=0, block_size=bs, arena_bytes=2 << 30, profile=True, pipeline=pipeline) as eng:
         wl = bench.Workload(eng, config, job_ids, bs)
         wl.step(eng).release()          # twice: the memtables are re-landed and re-sorted
         b = wl.step(eng)
         total_blocks = 0
         kernels = b.kernel_times()
-        if config == 2:  # the latency regime with every job speculated (and held)
+        if config == 2 and mode == "fused":  # the latency regime with every job speculated (and held)
             assert "partition_blocks" in kernels and "assemble" not in kernels, kernels
+        if config == 2:
             assert all(b.speculation(i) == abi.SPECULATION_HELD for i in range(len(wl.jobs)))
+        if mode == "pipelined":  # speculated jobs merged tile by tile, chains on a tail
+            assert "merge_unique" in kernels and "tail_wait" in kernels, kernels
         if config == 5:  # the throughput regime: pipelined groups, assembled bodies, chain-only kernel
             assert "assemble" in kernels and "tail_wait" in kernels, kernels
         for i, (job, js) in enumerate(zip(wl.jobs, wl.specs)):
