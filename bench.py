@@ -524,6 +524,8 @@ def main() -> None:
     ap.add_argument("--depth", type=int, default=3,
                     help="steps in flight: step k+D-1 is enqueued before step k is waited for, and the outputs "
                          "rotate over D sets (a replica's consecutive half-bars write freshly acquired blocks)")
+    ap.add_argument("--pipeline", choices=["auto", "on", "off"], default="auto",
+                    help="UNIQUE_KEYS batches: the engine's choice (auto), always pipelined, or always fused")
     args = ap.parse_args()
     njobs = args.jobs or configs.DEFAULT_JOBS.get(args.config, 1)
 
@@ -544,7 +546,8 @@ def main() -> None:
         dist = td
 
     bs = 1 << 20
-    eng = Engine(device=local, block_size=bs, profile=True, arena_bytes=2 << 30)
+    eng = Engine(device=local, block_size=bs, profile=True, arena_bytes=2 << 30,
+                 pipeline={"auto": None, "on": True, "off": False}[args.pipeline])
     if args.config == 1:
         return main_config1(args, eng, rank, world, local, dist, backend, bs)
     # Weak scaling: njobs jobs per GPU; the global job set is sharded by

@@ -237,55 +237,77 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
     }
 }
 
-struct UniqueShared {
-    // Entries: [0, na + 1) = A[ia0 - 1 .. ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1];
-    // limb l of entry e at key[l * (kUniqueTile + 3) + e].
-    uint64_t key[3 * (kUniqueTile + 3)];
-    uint8_t tomb[kUniqueTile + 1];
-    uint32_t bad;
-};
+// LDS of a k_merge_unique workgroup, sized per launch by the batch's widest
+// key (dynamic): the tile's broken flag, then KL key limbs per entry (limb l
+// of entry e at key[l * kUniqueRow + e]; entries [0, na + 1) = A[ia0 - 1 ..
+// ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1]), then the A tombstones.
+// A u128 id tree's tile takes 8.6 KiB, so two workgroups fit beside an AEGIS
+// chain workgroup's T-tables on one CU (a 3-limb static layout fit one).
+constexpr uint32_t kUniqueRow = kUniqueTile + 3;
+static inline uint32_t unique_lds_bytes(int kl) { return 16 + (uint32_t)kl * kUniqueRow * 8 + kUniqueTile + 1; }
 
+// One tile, one merged element per thread (tile order: its A elements, then
+// its B elements). The element's value is loaded with its key, before the
+// workgroup's barrier, so its HBM latency overlaps the ranking; every
+// pointer comes from a cursor started at the split's segments (a tile spans
+// one or two input blocks), not a search of the segment table.
 template <int KIND>
-__device__ __forceinline__ void merge_unique_tile(UniqueShared &sh, const JobDesc &j, uint32_t t,
+__device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j, uint32_t t,
                                                   const SplitDesc *usplits, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
-    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, R = T + 3;
-    uint64_t *s_key = sh.key;
-    uint8_t *s_tomb = sh.tomb;
-    uint32_t &s_bad = sh.bad;
+    constexpr uint32_t T = kUniqueTile, R = kUniqueRow;
+    static_assert(kUniqueThreads == kUniqueTile, "one merged element per thread");
+    uint32_t &s_bad = *(uint32_t *)lds;
+    uint64_t *s_key = (uint64_t *)(lds + 16);
+    uint8_t *s_tomb = lds + 16 + KL * R * 8;
     const uint32_t tid = threadIdx.x;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
     const SplitDesc s0 = usplits[j.usplit_base + t];
     const uint32_t ia0 = s0.i, ia1 = usplits[j.usplit_base + t + 1].i;
     const uint32_t jb0 = d0 - ia0, jb1 = d1 - ia1;
-    const uint32_t na = ia1 - ia0, nb = jb1 - jb0;
+    const uint32_t na = ia1 - ia0, nb = jb1 - jb0, m = na + nb;
     const uint32_t vs = j.value_size, ts = j.timestamp_offset;
     const bool drop = j.drop_tombstones != 0;
-    const uint32_t eb = na + 1; // first B entry (B[jb0 - 1])
+    const uint32_t eb = na + 1; // entry of B[jb0 - 1]
     if (tid == 0) s_bad = 0;
-    // Keys (and A tombstones) into LDS; pointers through cursors that start at
-    // the split's segments and only move forward.
-    SegCursor ca, cb;
-    ca.init(j.a, s0.seg_a);
-    cb.init(j.b, s0.seg_b);
-    for (uint32_t e = tid; e < na + nb + 3; e += NT) {
-        const bool is_a = e < eb;
-        const int64_t idx = is_a ? (int64_t)ia0 - 1 + e : (int64_t)jb0 - 1 + (e - eb);
-        const Stream &st = is_a ? j.a : j.b;
+    auto put_entry = [&](uint32_t e, const Key<KL> &k) {
+#pragma unroll
+        for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
+    };
+    // This thread's element: its value's first 32 bytes into registers, its key into LDS.
+    const bool has = tid < m, is_a = tid < na;
+    const uint32_t idx = is_a ? ia0 + tid : jb0 + (tid - na);
+    const uint8_t *src = nullptr;
+    u32x4 v0 = {0, 0, 0, 0}, v1 = {0, 0, 0, 0};
+    if (has) {
+        SegCursor c;
+        c.init(is_a ? j.a : j.b, is_a ? s0.seg_a : s0.seg_b);
+        src = c.elem(idx, vs);
+        v0 = gld<u32x4>(src);
+        if (vs >= 32) v1 = gld<u32x4>(src + 16);
+        put_entry(is_a ? 1 + tid : tid + 2, load_key<KIND>(src, ts));
+        if (is_a) s_tomb[1 + tid] = (uint8_t)load_tomb(src, ts);
+    }
+    // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (sentinel: all ones).
+    if (tid < 3) {
+        const bool bside = tid != 0;
+        const Stream &st = bside ? j.b : j.a;
+        const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
+        const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
         Key<KL> k;
 #pragma unroll
         for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
         uint8_t tb = 0;
-        if (idx >= 0 && idx < (int64_t)st.n) {
-            const uint32_t i = (uint32_t)idx;
-            const uint8_t *p = elem_ptr(st, seg_search(st, i), i, vs);
+        if (bi >= 0 && bi < (int64_t)st.n) {
+            SegCursor c;
+            c.init(st, bside ? s0.seg_b : s0.seg_a);
+            const uint8_t *p = c.elem((uint32_t)bi, vs);
             k = load_key<KIND>(p, ts);
-            if (is_a) tb = (uint8_t)load_tomb(p, ts);
+            if (!bside) tb = (uint8_t)load_tomb(p, ts);
         }
-#pragma unroll
-        for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
-        if (is_a) s_tomb[e] = tb;
+        put_entry(e, k);
+        if (!bside) s_tomb[0] = tb;
     }
     __syncthreads();
     auto entry = [&](uint32_t e) {
@@ -295,12 +317,10 @@ __device__ __forceinline__ void merge_unique_tile(UniqueShared &sh, const JobDes
         return k;
     };
     bool bad = false;
-    const uint32_t vcm = j.vcm, chunks = vs >> 4;
-    for (uint32_t e = tid; e < na + nb; e += NT) {
-        const bool is_a = e < na;
+    if (has) {
         uint32_t pos;
-        const uint8_t *src;
         if (is_a) {
+            const uint32_t e = tid;
             const Key<KL> ka = entry(1 + e);
             // |{B in the tile < ka}|: lower bound over entries [eb + 1, eb + 1 + nb).
             uint32_t lo = 0, hi = nb;
@@ -315,11 +335,8 @@ __device__ __forceinline__ void merge_unique_tile(UniqueShared &sh, const JobDes
             bad |= b_there && key_eq(entry(eb + 1 + lo), ka);
             bad |= (ia0 + e > 0) && key_eq(entry(e), ka);
             bad |= drop && s_tomb[1 + e];
-            const uint32_t i = ia0 + e;
-            ca.advance(i);
-            src = ca.elem(i, vs);
         } else {
-            const uint32_t b = e - na;
+            const uint32_t b = tid - na;
             const Key<KL> kb = entry(eb + 1 + b);
             // |{A in the tile <= kb}|: upper bound over entries [1, 1 + na).
             uint32_t lo = 0, hi = na;
@@ -330,14 +347,13 @@ __device__ __forceinline__ void merge_unique_tile(UniqueShared &sh, const JobDes
             }
             pos = b + lo;
             bad |= (jb0 + b > 0) && key_eq(entry(eb + b), kb);
-            const uint32_t i = jb0 + b;
-            cb.advance(i);
-            src = cb.elem(i, vs);
         }
-        const uint32_t g = d0 + pos;
+        const uint32_t g = d0 + pos, vcm = j.vcm;
         const uint32_t k = g / vcm;
         uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(g - k * vcm) * vs;
-        for (uint32_t c = 0; c < chunks; c++) gst<u32x4>(dst + 16 * c, gld<u32x4>(src + 16 * c));
+        gst<u32x4>(dst, v0);
+        if (vs >= 32) gst<u32x4>(dst + 16, v1);
+        for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src + c));
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
     __syncthreads();
@@ -349,17 +365,17 @@ __device__ __forceinline__ void merge_unique_tile(UniqueShared &sh, const JobDes
 
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
                                                                  const SplitDesc *usplits, JobResultDev *res) {
-    __shared__ UniqueShared sh;
+    extern __shared__ __attribute__((aligned(16))) uint8_t unique_lds[];
     const uint32_t g = blockIdx.x;
     const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
     const JobDesc &j = jobs[ji];
     if (!j.unique || g - j.utile_base >= j.utile_count) return; // uniform
     const uint32_t t = g - j.utile_base;
     switch (j.key_kind) {
-    case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(sh, j, t, usplits, res); break;
-    case kKeyIdU128: merge_unique_tile<kKeyIdU128>(sh, j, t, usplits, res); break;
-    case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(sh, j, t, usplits, res); break;
-    default: merge_unique_tile<kKeyCompositeU128>(sh, j, t, usplits, res); break;
+    case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
+    case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
+    case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
+    default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
     }
 }
 
@@ -375,7 +391,11 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
                        d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
-    hipLaunchKernelGGL(k_merge_unique, dim3(ntiles), dim3(kUniqueThreads), 0, s, d_jobs, njobs, ntiles,
+    int kl = 1; // the widest key among the launch's speculated jobs
+    for (int i = 0; i < njobs; i++)
+        if (h_jobs[i].unique) kl = std::max(kl, h_jobs[i].key_kind == kKeyTimestamp ? 1 : h_jobs[i].key_kind == kKeyCompositeU128 ? 3 : 2);
+    hipLaunchKernelGGL(k_merge_unique, dim3(ntiles), dim3(kUniqueThreads), unique_lds_bytes(kl), s, d_jobs, njobs,
+                       ntiles,
                        (const SplitDesc *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");

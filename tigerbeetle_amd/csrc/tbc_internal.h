@@ -96,11 +96,11 @@ struct JobDesc {
     uint32_t seal, pad2;
 };
 
-// Merged positions per tile of k_merge_unique: the tile's keys (plus three
-// neighbours) fit in 12.1 KiB of LDS for 24-byte keys, so its workgroups fit
-// beside chain workgroups that hold 140 KiB of a CU's 160.
+// Merged positions per tile of k_merge_unique (one per thread): the tile's
+// keys (plus three neighbours) take 8.6 KiB of LDS for 16-byte keys, so two
+// of its workgroups fit beside a chain workgroup's 136 KiB of a CU's 160.
 constexpr uint32_t kUniqueTile = 512;
-constexpr uint32_t kUniqueThreads = 256;
+constexpr uint32_t kUniqueThreads = 512; // one merged element per thread
 
 struct SplitDesc {
     uint32_t i;     // A elements before the tile boundary (merge path)

@@ -8,12 +8,14 @@ O=gpurun_out/r04${TAG:-}
 mkdir -p $O
 fatal() { [ "$1" -ge 124 ]; }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_overlap.py tests/test_gpu_unique.py tests/test_gpu_engine.py tests/test_manifest.py -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests_new.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_overlap.py tests/test_gpu_unique.py tests/test_gpu_engine.py tests/test_manifest.py ${EXTRA_TESTS:-} -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests_new.log 2>&1
   rc=$?; tail -2 $O/tests_new.log
   if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)|Error|assert" $O/tests_new.log | head -20; exit $rc; fi
+  if [ -z "$SKIP_ALL" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests_all.log 2>&1
   rc=$?; tail -2 $O/tests_all.log
   if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)|Error|assert" $O/tests_all.log | head -20; exit $rc; fi
+  fi
 fi
 run() { # name env... -- args
   local name=$1; shift
@@ -23,7 +25,7 @@ run() { # name env... -- args
 import json,sys
 for l in sys.stdin:
     d=json.loads(l); k=d.get('kernels_us_per_step',{}); p=d.get('pcie',{})
-    print(' ms/step', d['ms_per_step'], 'MB/s', d['value'], 'frac', d['roofline']['frac'], 'dom', d['roofline']['kernel'], {a:b for a,b in k.items()}, 'd2h', p.get('d2h',{}).get('GBps'), 'h2d', p.get('h2d',{}).get('GBps'), 'incl', p.get('pcie_inclusive_MBps'), 'staged', p.get('staged'))
+    print(' ms/step', d['ms_per_step'], 'MB/s', d['value'], 'frac', d['roofline']['frac'], 'dom', d['roofline'].get('kernel') or d['roofline']['dominant_kernel']['kernel'], {a:b for a,b in k.items()}, 'd2h', p.get('d2h',{}).get('GBps'), 'h2d', p.get('h2d',{}).get('GBps'), 'incl', p.get('pcie_inclusive_MBps'), 'staged', p.get('staged'))
 "
   if [ $brc -ne 0 ]; then tail -15 $O/bench_$name.log; fi
   return $brc
@@ -39,6 +41,8 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     t16) run t16 TBC_TAIL_CHAINS=16 $B --depth 3 --no-cpu-baseline ;;
     t4) run t4 TBC_TAIL_CHAINS=4 $B --depth 3 --no-cpu-baseline ;;
     tv) run tv TBC_TAIL_STEP=valu $B --depth 3 --no-cpu-baseline ;;
+    p1) run p1 $B --depth 1 --pipeline on --no-cpu-baseline ;;
+    p3) run p3 $B --depth 3 --pipeline on --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
