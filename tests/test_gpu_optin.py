@@ -1,9 +1,8 @@
 """The engine's opt-in paths, measured slower and off by default (DESIGN.md
 §3/§4.2), stay bit-exact: the staged merge (TBC_STAGED=1: grid batches,
 pipelined groups, the throughput regime, values-only), the bar-end sort on
-its own stream (TBC_SORT_STREAM=1: pending-sort waits), tails at the
-highest stream priority (TBC_TAIL_PRIORITY=1) and the tails' chains on the
-half (64 KiB, 16-replica) T-table layout (TBC_TAIL_TABLES=64). The library reads these once
+its own stream (TBC_SORT_STREAM=1: pending-sort waits) and tails at the
+highest stream priority (TBC_TAIL_PRIORITY=1). The library reads these once
 per process, so one child process runs the tests that exercise those paths
 with all three set; each of those tests compares with the oracle."""
 import os
@@ -21,32 +20,15 @@ SELECT = " or ".join([
     "test_two_half_bars_chained_through_the_grid",   # grid batches: staged merge in the front
     "test_pipelined_grid_batches_in_flight",
     "test_values_only_bodies_equal_full_compaction",  # VALUES_ONLY: staged bodies
-    "test_speculated_batches_pipelined_three_in_flight",  # pipelined tails (chain-only kernel)
 ])
 
 
 @pytest.mark.gpu
 def test_opt_in_paths_bit_exact():
-    env = dict(os.environ, TBC_STAGED="1", TBC_SORT_STREAM="1", TBC_TAIL_PRIORITY="1", TBC_TAIL_TABLES="64")
+    env = dict(os.environ, TBC_STAGED="1", TBC_SORT_STREAM="1", TBC_TAIL_PRIORITY="1")
     files = [os.path.join(HERE, f) for f in ("test_gpu_parity.py", "test_gpu_grid.py", "test_gpu_engine.py",
-                                              "test_gpu_split.py", "test_gpu_overlap.py")]
+                                              "test_gpu_split.py")]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", "-k", SELECT,
-                        *files], env=env, capture_output=True, text=True, timeout=200)
-    tail = (r.stdout + r.stderr)[-3000:]
-    assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " failed" not in r.stdout, tail
-
-
-@pytest.mark.gpu
-def test_half_table_tails_bit_exact():
-    """TBC_TAIL_TABLES=64 alone: every tail chain kernel on the 16-replica
-    layout (latency-regime tails of pipelined speculated batches, and the
-    throughput regime's groups), compared with the oracle."""
-    env = dict(os.environ, TBC_TAIL_TABLES="64")
-    sel = " or ".join(["test_compaction_parity_throughput_regime", "test_speculated_batches_pipelined_three_in_flight",
-                       "test_back_to_back_batches_share_outputs"])
-    files = [os.path.join(HERE, f) for f in ("test_gpu_parity.py", "test_gpu_overlap.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", "-k", sel,
                         *files], env=env, capture_output=True, text=True, timeout=200)
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail

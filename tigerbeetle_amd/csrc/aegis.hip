@@ -145,35 +145,25 @@ __device__ __forceinline__ uint32_t bpermute(uint32_t byte_addr, uint32_t v) {
 //     (r >> 1) * 64 KiB + b * 256 + (r & 1) * 128 + k * 4,
 // so one v_perm_b32 builds the address {k*4, b, region, 0} from the state
 // column and a per-lane base, and the (r & 1) half is the ds_read offset.
-//
-// Half layout (Rep = 16, 64 KiB, the chain-only tail kernels): 16 replicas,
-// T_r[b] for lane k = lane & 15 at b * 256 + r * 64 + k * 4 (ds_read offset
-// r * 64). Lanes l and l + 16 of a group read one replica: 2-way bank
-// conflicts (4 LDS cycles per lookup instead of 2), in exchange for 64 KiB of
-// the CU left to the fronts that run beside the tails.
 constexpr uint32_t kTableBytes = 131072;
 constexpr uint32_t kTableDwords = kTableBytes / 4;
-template <int Rep> constexpr uint32_t table_dwords() { return Rep == 32 ? kTableDwords : kTableDwords / 2; }
 
-template <int Rep = 32> __device__ __forceinline__ void load_tables(uint32_t *sT) {
-    static_assert(Rep == 32 || Rep == 16, "32 or 16 replicas");
-    for (uint32_t i = threadIdx.x; i < table_dwords<Rep>(); i += blockDim.x) {
-        const uint32_t r = Rep == 32 ? (((i >> 14) << 1) | ((i >> 5) & 1)) : ((i >> 4) & 3);
+__device__ __forceinline__ void load_tables(uint32_t *sT) {
+    for (uint32_t i = threadIdx.x; i < kTableDwords; i += blockDim.x) {
+        const uint32_t r = ((i >> 14) << 1) | ((i >> 5) & 1);
         const uint32_t b = (i >> 6) & 255;
         sT[i] = c_aes.t[r][b];
     }
 }
 
-template <int Rep = 32> struct TableBaseT {
-    uint32_t lo, hi; // {k*4, -, 0, 0} and {k*4, -, 1, 0} (Rep 16: both {k*4, -, 0, 0})
-    static constexpr uint32_t off1 = Rep == 32 ? 128 : 64, off2 = Rep == 32 ? 0 : 128, off3 = Rep == 32 ? 128 : 192;
-    __device__ __forceinline__ TableBaseT() {
-        const uint32_t k = threadIdx.x & (Rep - 1);
+struct TableBase {
+    uint32_t lo, hi; // {k*4, -, 0, 0} and {k*4, -, 1, 0}
+    __device__ __forceinline__ TableBase() {
+        const uint32_t k = threadIdx.x & 31;
         lo = k * 4;
-        hi = Rep == 32 ? (k * 4 | 0x10000u) : k * 4;
+        hi = k * 4 | 0x10000u;
     }
 };
-using TableBase = TableBaseT<32>;
 
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t *sT, uint32_t byte_off) {
     return *(const uint32_t *)((const char *)sT + byte_off);
@@ -184,18 +174,16 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *sT, uint32_t byte_of
 // and the quad exchanges the partial products. `acc` (the round key, already
 // xored with the message word) is folded in first so the chain ends with the
 // last lookup to return.
-template <int Rep>
-__device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, const TableBaseT<Rep> &tb, uint32_t x, uint32_t acc) {
-    using TB = TableBaseT<Rep>;
+__device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, const TableBase &tb, uint32_t x, uint32_t acc) {
     // v_perm_b32 selector bytes: 0-3 pick src1 (base), 4-7 pick src0 (x).
     const uint32_t a0 = __builtin_amdgcn_perm(x, tb.lo, 0x03020400u);
     const uint32_t a1 = __builtin_amdgcn_perm(x, tb.lo, 0x03020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, tb.hi, 0x03020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, tb.hi, 0x03020700u);
     const uint32_t t0 = lds_u32(sT, a0);
-    const uint32_t t1 = lds_u32(sT, a1 + TB::off1);
-    const uint32_t t2 = lds_u32(sT, a2 + TB::off2);
-    const uint32_t t3 = lds_u32(sT, a3 + TB::off3);
+    const uint32_t t1 = lds_u32(sT, a1 + 128);
+    const uint32_t t2 = lds_u32(sT, a2);
+    const uint32_t t3 = lds_u32(sT, a3 + 128);
     uint32_t r = acc ^ t0;
     r ^= quad_perm<1, 2, 3, 0>(t1);
     r ^= quad_perm<2, 3, 0, 1>(t2);
@@ -206,8 +194,7 @@ __device__ __forceinline__ uint32_t aes_col(const uint32_t *sT, const TableBaseT
 // One AEGIS update step of lane (p, c): S'[label+1] = AESRound(S[label]) ^
 // S[label+1] ^ m, with the round key S[label+1] = x of quad p+1.
 struct StepBpermute {
-    template <int Rep>
-    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBaseT<Rep> &tb, uint32_t key_src,
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t key_src,
                                                     uint32_t x, uint32_t m) {
         const uint32_t key = bpermute(key_src, x);
         return aes_col(sT, tb, x, key ^ m);
@@ -322,18 +309,16 @@ __device__ __forceinline__ uint32_t key_valu(uint32_t x) {
 }
 
 struct StepValuKey {
-    template <int Rep>
-    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBaseT<Rep> &tb, uint32_t, uint32_t x,
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t, uint32_t x,
                                                     uint32_t m) {
-        using TB = TableBaseT<Rep>;
         const uint32_t a0 = __builtin_amdgcn_perm(x, tb.lo, 0x03020400u);
         const uint32_t a1 = __builtin_amdgcn_perm(x, tb.lo, 0x03020500u);
         const uint32_t a2 = __builtin_amdgcn_perm(x, tb.hi, 0x03020600u);
         const uint32_t a3 = __builtin_amdgcn_perm(x, tb.hi, 0x03020700u);
         const uint32_t t0 = lds_u32(sT, a0);
-        const uint32_t t1 = lds_u32(sT, a1 + TB::off1);
-        const uint32_t t2 = lds_u32(sT, a2 + TB::off2);
-        const uint32_t t3 = lds_u32(sT, a3 + TB::off3);
+        const uint32_t t1 = lds_u32(sT, a1 + 128);
+        const uint32_t t2 = lds_u32(sT, a2);
+        const uint32_t t3 = lds_u32(sT, a3 + 128);
         uint32_t r = (key_valu(x) ^ m) ^ t0;
         r ^= quad_perm<1, 2, 3, 0>(t1);
         r ^= quad_perm<2, 3, 0, 1>(t2);
@@ -364,14 +349,14 @@ template <class S> struct StepMasked<S, decltype((void)S::kMaskedMsg)> {
 // continues in the lean loop (the finished group's lanes compute junk, its
 // tag is already captured) and ends the same way. Every load stays inside
 // its own group's message (addresses are clamped to it).
-template <class Msg, class Step = StepValuKey, int Rep = 32>
+template <class Msg, class Step = StepValuKey>
 __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &msg) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t g = lane & 31, half = lane & 32;
     const uint32_t p = g >> 2, c = g & 3;
     const uint32_t key_src = (half + (((p + 1) & 7) << 2) + c) << 2; // quad p+1, same column
 
-    const TableBaseT<Rep> tb;
+    const TableBase tb;
     uint32_t x = c_seed.s[p][c];
     const uint32_t len = msg.len; // this group's length
     const uint32_t n_abs = (len + 31) >> 5;
@@ -731,7 +716,6 @@ __device__ __forceinline__ uint32_t header_dword(const HeaderFields &h, uint32_t
 
 // Fill a 256-byte header in LDS (hdr: 64 dwords), checksum [16, 256), and
 // return the header checksum column in every lane.
-template <int Rep = 32>
 __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *hdr, const HeaderFields &h,
                                                   uint32_t body_tag) {
     const uint32_t lane = threadIdx.x & 63, g = lane & 31;
@@ -741,7 +725,7 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     LdsMsg m(hdr + 4, kHeaderSize - 16);
-    uint32_t tag = aegis_mac32<LdsMsg, StepValuKey, Rep>(sT, m);
+    uint32_t tag = aegis_mac32(sT, m);
     return tag;
 }
 
@@ -895,7 +879,6 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
 // Data block k of job j, body checksummed (`body_tag`: column lane & 3 of
 // the tag, per 32-lane group): header fields, header checksum, the header
 // and the zeroed sector tail stored by the `writer` group.
-template <int Rep = 32>
 __device__ __forceinline__ void finish_data_block(const uint32_t *sT, uint32_t *hdr, const JobDesc &j, uint32_t k,
                                                   uint32_t cnt, uint32_t body_tag, bool writer) {
     const uint32_t slot = data_block_slot(k, j.dbcm);
@@ -912,7 +895,7 @@ __device__ __forceinline__ void finish_data_block(const uint32_t *sT, uint32_t *
     h.meta2 = j.value_size; // .value_size
     h.meta3 = j.tree_id;    // .tree_id (u16), reserved = 0
     h.block_type = 5;       // BlockType.data (schema.zig:65)
-    const uint32_t hdr_tag = finish_header<Rep>(sT, hdr, h, body_tag);
+    const uint32_t hdr_tag = finish_header(sT, hdr, h, body_tag);
     const uint32_t g = threadIdx.x & 31;
     if (g < 4) hdr[g] = hdr_tag;
     __builtin_amdgcn_wave_barrier();
@@ -1475,15 +1458,14 @@ constexpr uint32_t kMaxChainOnlyWaves = 16;
 // Above this many chain waves (2 per SIMD) the two-pass path wins.
 constexpr uint32_t kFusedMaxChainWaves = 2048;
 
-template <bool Fused, class ChainStep = StepBpermute, int Rep = 32>
+template <bool Fused, class ChainStep = StepBpermute>
 __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res,
                                             const uint64_t *status, const uint64_t *masks,
                                             const uint32_t *block_tile, const SplitDesc *splits,
                                             uint32_t chain_waves, const uint32_t *ready, const SplitDesc *bsplits,
                                             uint32_t phase) {
     constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
-    static_assert(Rep == 32 || !Fused, "the fused kernel keeps the conflict-free tables");
-    __shared__ uint32_t sT[table_dwords<Rep>()];
+    __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
     __shared__ uint32_t sCons[2 * kMaxChainWaves]; // the chains' positions (body bytes needed so far)
@@ -1504,7 +1486,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         const bool mine = threadIdx.x < 2 * C && locate(2 * blockIdx.x * C + threadIdx.x, ji_, k_);
         if (!__syncthreads_or(mine)) return;
     }
-    load_tables<Rep>(sT);
+    load_tables(sT);
     if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = sCons[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t wave_in_block = threadIdx.x >> 6;
@@ -1599,20 +1581,20 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
             __hip_atomic_load(ready + j.dblock_base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
             gst<uint32_t>(const_cast<uint32_t *>(&res[j.job_index].invariant), 0xdeafu);
         GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
-        body_tag = aegis_mac32<GlobalMsg, ChainStep, Rep>(sT, body);
+        body_tag = aegis_mac32<GlobalMsg, ChainStep>(sT, body);
     }
 
     (void)size;
-    finish_data_block<Rep>(sT, sHdr[wave_in_block][upper ? 1 : 0], j, k, cnt, body_tag, writer);
+    finish_data_block(sT, sHdr[wave_in_block][upper ? 1 : 0], j, k, cnt, body_tag, writer);
 }
 
-template <bool Fused, class ChainStep = StepBpermute, int Rep = 32>
+template <bool Fused, class ChainStep = StepBpermute>
 __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data_blocks(
     const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res, const uint64_t *status,
     const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
     const uint32_t *ready, const SplitDesc *bsplits, uint32_t phase) {
-    data_blocks<Fused, ChainStep, Rep>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready,
-                                       bsplits, phase);
+    data_blocks<Fused, ChainStep>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready,
+                                  bsplits, phase);
 }
 
 // The recomputation of broken speculations (phase 1) in its own symbol, so
@@ -2162,21 +2144,6 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
                        void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t waves = (total_dblocks + 1) / 2;
-    // TBC_TAIL_TABLES=64 (A/B measurement): the half table layout (64 KiB,
-    // 2-way bank conflicts), leaving the fronts beside the tails 88 KiB of
-    // each chain CU instead of 24.
-    static const bool half_tables = getenv("TBC_TAIL_TABLES") && atoi(getenv("TBC_TAIL_TABLES")) == 64;
-    auto launch_chains = [&](auto step, uint32_t c) {
-        using Step = decltype(step);
-        if (half_tables)
-            hipLaunchKernelGGL((k_data_blocks<false, Step, 16>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs,
-                               njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
-                               d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
-        else
-            hipLaunchKernelGGL((k_data_blocks<false, Step, 32>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs,
-                               njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
-                               d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
-    };
     if (total_dblocks) {
         if (waves <= 1024) { // latency regime: one chain per SIMD, round keys by VALU lane moves
             // A chain workgroup holds a whole CU's LDS (the tables), so
@@ -2194,11 +2161,20 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
             // throughput regime does. TBC_TAIL_STEP=valu|bperm (A/B only).
             static const char *step_env = getenv("TBC_TAIL_STEP");
             const bool bperm = step_env ? step_env[0] == 'b' : c >= 8;
-            if (bperm) launch_chains(StepBpermute{}, c);
-            else launch_chains(StepValuKey{}, c);
+            if (bperm)
+                hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                                   d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                                   d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
+            else
+                hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                                   d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                                   d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         } else {
             const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
-            launch_chains(StepBpermute{}, (waves + 256 * rounds - 1) / (256 * rounds));
+            const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
+            hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                               d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+                               d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         }
         if (hipGetLastError() != hipSuccess) return -1;
     }
