@@ -1592,7 +1592,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // tile splits, then (speculated jobs) one split per data block, then the
     // unique-tile splits (pipelined speculated batches)
     const uint64_t sz_splits =
-        align_up(sizeof(SplitDesc) * ((uint64_t)splits + (any_unique ? dblocks : 0) + usplits), 256);
+        align_up(sizeof(SplitDesc) * ((uint64_t)splits + (any_unique ? dblocks : 0)) + sizeof(UniqueSplit) * usplits,
+                 256);
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     // tile status, block tiles, per-block landed counts, the assembling
     // merge's look-back words (one per tile) and its ticket counters

@@ -204,7 +204,7 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 // recomputed through the merge path by the batch's phase 1.
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, int njobs, uint32_t nsplits,
-                                                          SplitDesc *usplits, JobResultDev *res) {
+                                                          UniqueSplit *usplits, JobResultDev *res) {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= nsplits) return;
     const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.usplit_base; });
@@ -220,12 +220,18 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
     case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
     default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
     }
-    SplitDesc s;
+    UniqueSplit s;
     s.i = lo;
-    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
-    const uint32_t jb = d - lo;
-    s.seg_b = nb ? seg_search(j.b, jb > 0 ? jb - 1 : 0) : 0;
     s.pad = 0;
+    const uint32_t jb = d - lo;
+    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
+    s.seg_b = nb ? seg_search(j.b, jb > 0 ? jb - 1 : 0) : 0;
+    s.a_ptr = na ? gld<uint64_t>(j.a.seg_ptr + s.seg_a) : 0;
+    s.a_lo = na ? gld<uint32_t>(j.a.seg_pre + s.seg_a) : 0;
+    s.a_hi = na ? gld<uint32_t>(j.a.seg_pre + s.seg_a + 1) : 0;
+    s.b_ptr = nb ? gld<uint64_t>(j.b.seg_ptr + s.seg_b) : 0;
+    s.b_lo = nb ? gld<uint32_t>(j.b.seg_pre + s.seg_b) : 0;
+    s.b_hi = nb ? gld<uint32_t>(j.b.seg_pre + s.seg_b + 1) : 0;
     usplits[g] = s;
     if (t == 0) { // speculative results (write_blocks' shape for n values, compaction.zig:806-850)
         JobResultDev &r = res[j.job_index];
@@ -241,29 +247,40 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
 // key (dynamic): the tile's broken flag, then KL key limbs per entry (limb l
 // of entry e at key[l * kUniqueRow + e]; entries [0, na + 1) = A[ia0 - 1 ..
 // ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1]), then the A tombstones.
-// A u128 id tree's tile takes 8.6 KiB, so two workgroups fit beside an AEGIS
-// chain workgroup's T-tables on one CU (a 3-limb static layout fit one).
+// A u128 id tree's tile takes 16.6 KiB, so a workgroup fits beside an AEGIS
+// chain workgroup's T-tables on one CU.
 constexpr uint32_t kUniqueRow = kUniqueTile + 3;
 static inline uint32_t unique_lds_bytes(int kl) { return 16 + (uint32_t)kl * kUniqueRow * 8 + kUniqueTile + 1; }
 
-// One tile, one merged element per thread (tile order: its A elements, then
-// its B elements). The element's value is loaded with its key, before the
-// workgroup's barrier, so its HBM latency overlaps the ranking; every
-// pointer comes from a cursor started at the split's segments (a tile spans
-// one or two input blocks), not a search of the segment table.
+// Element idx of a stream whose split resolved segment [lo, hi) at ptr: in
+// that segment, or (a tile crossing an input block boundary) found by walking
+// the segment table forward from it.
+__device__ __forceinline__ const uint8_t *unique_elem(const Stream &st, uint32_t seg, uint64_t ptr, uint32_t lo,
+                                                      uint32_t hi, uint32_t idx, uint32_t vs) {
+    if (idx < hi || seg + 1 >= st.nseg) return (const uint8_t *)(uintptr_t)ptr + (size_t)(idx - lo) * vs;
+    SegCursor c;
+    c.init(st, seg + 1);
+    return c.elem(idx, vs);
+}
+
+// One tile, two merged elements per thread (tile order: its A elements, then
+// its B elements; thread t owns elements t and t + 512). Both values are
+// loaded with their keys before the workgroup's barrier, so their HBM latency
+// overlaps the ranking; pointers come from the split's resolved segments (a
+// tile spans one or two input blocks), not a search of the segment tables.
 template <int KIND>
 __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j, uint32_t t,
-                                                  const SplitDesc *usplits, JobResultDev *res) {
+                                                  const UniqueSplit *usplits, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
-    constexpr uint32_t T = kUniqueTile, R = kUniqueRow;
-    static_assert(kUniqueThreads == kUniqueTile, "one merged element per thread");
+    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, R = kUniqueRow, E = T / NT;
+    static_assert(T == E * NT, "whole elements per thread");
     uint32_t &s_bad = *(uint32_t *)lds;
     uint64_t *s_key = (uint64_t *)(lds + 16);
     uint8_t *s_tomb = lds + 16 + KL * R * 8;
     const uint32_t tid = threadIdx.x;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
-    const SplitDesc s0 = usplits[j.usplit_base + t];
+    const UniqueSplit s0 = usplits[j.usplit_base + t];
     const uint32_t ia0 = s0.i, ia1 = usplits[j.usplit_base + t + 1].i;
     const uint32_t jb0 = d0 - ia0, jb1 = d1 - ia1;
     const uint32_t na = ia1 - ia0, nb = jb1 - jb0, m = na + nb;
@@ -275,19 +292,31 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
 #pragma unroll
         for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
     };
-    // This thread's element: its value's first 32 bytes into registers, its key into LDS.
-    const bool has = tid < m, is_a = tid < na;
-    const uint32_t idx = is_a ? ia0 + tid : jb0 + (tid - na);
-    const uint8_t *src = nullptr;
-    u32x4 v0 = {0, 0, 0, 0}, v1 = {0, 0, 0, 0};
-    if (has) {
-        SegCursor c;
-        c.init(is_a ? j.a : j.b, is_a ? s0.seg_a : s0.seg_b);
-        src = c.elem(idx, vs);
-        v0 = gld<u32x4>(src);
-        if (vs >= 32) v1 = gld<u32x4>(src + 16);
-        put_entry(is_a ? 1 + tid : tid + 2, load_key<KIND>(src, ts));
-        if (is_a) s_tomb[1 + tid] = (uint8_t)load_tomb(src, ts);
+    auto elem_of = [&](bool is_a, uint32_t idx) {
+        return is_a ? unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, idx, vs)
+                    : unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, idx, vs);
+    };
+    // This thread's elements: their values' first 32 bytes into registers, keys into LDS.
+    const uint8_t *src[E];
+    u32x4 v0[E], v1[E];
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        const bool is_a = e < na;
+        src[q] = e < m ? elem_of(is_a, is_a ? ia0 + e : jb0 + (e - na)) : nullptr;
+        v0[q] = v1[q] = u32x4{0, 0, 0, 0};
+        if (e < m) {
+            v0[q] = gld<u32x4>(src[q]);
+            if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
+        }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        if (e >= m) continue;
+        const bool is_a = e < na;
+        put_entry(is_a ? 1 + e : e + 2, load_key<KIND>(src[q], ts));
+        if (is_a) s_tomb[1 + e] = (uint8_t)load_tomb(src[q], ts);
     }
     // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (sentinel: all ones).
     if (tid < 3) {
@@ -300,9 +329,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
         uint8_t tb = 0;
         if (bi >= 0 && bi < (int64_t)st.n) {
-            SegCursor c;
-            c.init(st, bside ? s0.seg_b : s0.seg_a);
-            const uint8_t *p = c.elem((uint32_t)bi, vs);
+            const uint8_t *p = elem_of(!bside, (uint32_t)bi);
             k = load_key<KIND>(p, ts);
             if (!bside) tb = (uint8_t)load_tomb(p, ts);
         }
@@ -317,10 +344,13 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         return k;
     };
     bool bad = false;
-    if (has) {
+    const uint32_t vcm = j.vcm;
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        if (e >= m) continue;
         uint32_t pos;
-        if (is_a) {
-            const uint32_t e = tid;
+        if (e < na) {
             const Key<KL> ka = entry(1 + e);
             // |{B in the tile < ka}|: lower bound over entries [eb + 1, eb + 1 + nb).
             uint32_t lo = 0, hi = nb;
@@ -336,7 +366,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             bad |= (ia0 + e > 0) && key_eq(entry(e), ka);
             bad |= drop && s_tomb[1 + e];
         } else {
-            const uint32_t b = tid - na;
+            const uint32_t b = e - na;
             const Key<KL> kb = entry(eb + 1 + b);
             // |{A in the tile <= kb}|: upper bound over entries [1, 1 + na).
             uint32_t lo = 0, hi = na;
@@ -348,12 +378,12 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             pos = b + lo;
             bad |= (jb0 + b > 0) && key_eq(entry(eb + b), kb);
         }
-        const uint32_t g = d0 + pos, vcm = j.vcm;
+        const uint32_t g = d0 + pos;
         const uint32_t k = g / vcm;
         uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(g - k * vcm) * vs;
-        gst<u32x4>(dst, v0);
-        if (vs >= 32) gst<u32x4>(dst + 16, v1);
-        for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src + c));
+        gst<u32x4>(dst, v0[q]);
+        if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
+        for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
     __syncthreads();
@@ -364,7 +394,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
 }
 
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
-                                                                 const SplitDesc *usplits, JobResultDev *res) {
+                                                                 const UniqueSplit *usplits, JobResultDev *res) {
     extern __shared__ __attribute__((aligned(16))) uint8_t unique_lds[];
     const uint32_t g = blockIdx.x;
     const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
@@ -388,15 +418,14 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     const uint32_t ntiles = l.utile_base + l.utile_count;
     if (!nsplits || !ntiles) return 0;
     hipLaunchKernelGGL(k_partition_unique, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
-                       d_usplits, d_results);
+                       (UniqueSplit *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
     int kl = 1; // the widest key among the launch's speculated jobs
     for (int i = 0; i < njobs; i++)
         if (h_jobs[i].unique) kl = std::max(kl, h_jobs[i].key_kind == kKeyTimestamp ? 1 : h_jobs[i].key_kind == kKeyCompositeU128 ? 3 : 2);
     hipLaunchKernelGGL(k_merge_unique, dim3(ntiles), dim3(kUniqueThreads), unique_lds_bytes(kl), s, d_jobs, njobs,
-                       ntiles,
-                       (const SplitDesc *)d_usplits, d_results);
+                       ntiles, (const UniqueSplit *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;

@@ -96,11 +96,11 @@ struct JobDesc {
     uint32_t seal, pad2;
 };
 
-// Merged positions per tile of k_merge_unique (one per thread): the tile's
-// keys (plus three neighbours) take 8.6 KiB of LDS for 16-byte keys, so two
-// of its workgroups fit beside a chain workgroup's 136 KiB of a CU's 160.
-constexpr uint32_t kUniqueTile = 512;
-constexpr uint32_t kUniqueThreads = 512; // one merged element per thread
+// Merged positions per tile of k_merge_unique (two per thread): the tile's
+// keys (plus three neighbours) take 16.6 KiB of LDS for 16-byte keys, so a
+// workgroup fits beside a chain workgroup's 136 KiB of a CU's 160.
+constexpr uint32_t kUniqueTile = 1024;
+constexpr uint32_t kUniqueThreads = 512;
 
 struct SplitDesc {
     uint32_t i;     // A elements before the tile boundary (merge path)
@@ -108,6 +108,20 @@ struct SplitDesc {
     uint32_t seg_b; // segment of B[min(d-i, nb-1)]
     uint32_t pad;
 };
+
+// A k_merge_unique tile boundary: the merge-path split plus the input
+// segment each side's first element lies in, resolved (pointer and element
+// range), so a tile's loads start without walking the segment tables. Three
+// SplitDesc slots of the batch scratch per boundary.
+struct UniqueSplit {
+    uint32_t i;            // A elements before the boundary
+    uint32_t seg_a, seg_b; // segments of A[max(i-1, 0)] and B[max(d-i-1, 0)]
+    uint32_t pad;
+    uint64_t a_ptr, b_ptr; // their first elements
+    uint32_t a_lo, a_hi;   // element range [lo, hi) of segment seg_a
+    uint32_t b_lo, b_hi;
+};
+static_assert(sizeof(UniqueSplit) == 3 * sizeof(SplitDesc), "three split slots");
 
 // One entry of the batch's tile order: tiles of the jobs of one key kind,
 // interleaved round-robin (job index into the batch's JobDesc array, tile).

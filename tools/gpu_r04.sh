@@ -43,6 +43,13 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     tv) run tv TBC_TAIL_STEP=valu $B --depth 3 --no-cpu-baseline ;;
     p1) run p1 $B --depth 1 --pipeline on --no-cpu-baseline ;;
     p3) run p3 $B --depth 3 --pipeline on --no-cpu-baseline ;;
+    h3) run h3 TBC_TAIL_TABLES=64 $B --depth 3 --no-cpu-baseline ;;
+    h8) run h8 TBC_TAIL_TABLES=64 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
+    h16) run h16 TBC_TAIL_TABLES=64 TBC_TAIL_CHAINS=16 $B --depth 3 --no-cpu-baseline ;;
+    h4) run h4 TBC_TAIL_TABLES=64 TBC_TAIL_CHAINS=4 $B --depth 3 --no-cpu-baseline ;;
+    c5h) run c5h TBC_TAIL_TABLES=64 $B --depth 3 --config 5 --no-cpu-baseline ;;
+    c1) run c1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    c1h) run c1h TBC_TAIL_TABLES=64 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
