@@ -1735,7 +1735,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // speculations recomputed by the merge path (phase 1) before the
         // index block layout reads the final shapes.
         if (ok && unique_tiles)
-            ok = launch_merge_unique((const JobDesc *)d_in, sj.data(), (int)count, d_usplits, d_res, s, mark_cb, b) == 0;
+            ok = launch_merge_unique((const JobDesc *)d_in, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s,
+                                     mark_cb, b) == 0;
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
                               d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
@@ -1823,7 +1824,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // chains of every data block, the index blocks, the results.
         const JobDesc *dj = (const JobDesc *)d_in;
         if (unique_tiles) {
-            ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, s, mark_cb, b) == 0;
+            ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s, mark_cb,
+                                           b) == 0;
         } else {
             ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
             mark_cb(b, "partition_blocks");

@@ -333,7 +333,8 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 // value survives) with the speculation checks (a broken job is marked for
 // the recomputation phase).
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
-                        JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+                        JobResultDev *d_results, uint32_t *d_ticket, void *stream, void (*mark)(void *, const char *),
+                        void *mark_ctx);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
