@@ -1494,12 +1494,12 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // opt-in: TBC_STAGED=1 (A/B measurement and its parity tests).
     uint64_t dblocks_all = 0;
     for (uint32_t i = 0; i < count; i++) dblocks_all += hj[i].dblock_max;
-    static const bool staged_on = getenv("TBC_STAGED") != nullptr;
+    const bool staged_on = staged_variant() != 0;
     const bool staged = staged_on && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
                                       (dblocks_all + 1) / 2 > fused_max_chain_waves());
     for (uint32_t i = 0; i < count; i++) {
         JobDesc &d = hj[i];
-        if (staged) d.merge_tile = staged_tile(d.value_size);
+        if (staged) d.merge_tile = staged_variant() == 2 ? 1024u : staged_tile(d.value_size);
         const uint64_t n = (uint64_t)d.a.n + d.b.n;
         d.tile_count = (uint32_t)((n + d.merge_tile - 1) / d.merge_tile);
     }

@@ -50,6 +50,12 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     c5h) run c5h TBC_TAIL_TABLES=64 $B --depth 3 --config 5 --no-cpu-baseline ;;
     c1) run c1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c1h) run c1h TBC_TAIL_TABLES=64 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    c5s) run c5s TBC_STAGED=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
+    c1s) run c1s TBC_STAGED=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    c5a) run c5a TBC_STAGED=2 $B --depth 3 --config 5 --no-cpu-baseline ;;
+    c1a) run c1a TBC_STAGED=2 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    c3a) run c3a TBC_STAGED=2 $B --depth 3 --config 3 --no-cpu-baseline ;;
+    c4a) run c4a TBC_STAGED=2 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
