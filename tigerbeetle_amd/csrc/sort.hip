@@ -707,7 +707,6 @@ __device__ __forceinline__ bool key_before(const uint64_t a[3], uint32_t ia, con
     return ia < ib;
 }
 
-template <bool NtGather>
 __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32_t *tile_seg, const uint64_t *words0,
                                                      const uint64_t *words1) {
     const uint32_t tile = blockIdx.x / (kSortTile / kFinishItems);
@@ -729,11 +728,7 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++) {
                 const uint32_t j = j0 + q * vpr + jl;
-                if (j < last) {
-                    const uint8_t *p = S.copy + (size_t)(uint32_t)(wv[j] & imask) * vs + 16 * part;
-                    if constexpr (NtGather) v[q] = __builtin_nontemporal_load((const TBC_GLOBAL u32x4 *)p);
-                    else v[q] = gld<u32x4>(p);
-                }
+                if (j < last) v[q] = gld<u32x4>(S.copy + (size_t)(uint32_t)(wv[j] & imask) * vs + 16 * part);
             }
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++) {
@@ -1033,14 +1028,8 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
                            ntiles, words0, words1, bins, status, *epoch, counters, counters + kMaxPasses);
         *epoch += kMaxPasses;
     }
-    // TBC_SORT_GATHER_NT=1 (A/B measurement): the gather's loads nontemporal.
-    static const bool nt_gather = getenv("TBC_SORT_GATHER_NT") != nullptr;
-    if (nt_gather)
-        hipLaunchKernelGGL(k_sort_finish<true>, dim3(ntiles * (kSortTile / kFinishItems)), dim3(256), 0, s, d_segs,
-                           (const uint32_t *)d_tile, (const uint64_t *)words0, (const uint64_t *)words1);
-    else
-        hipLaunchKernelGGL(k_sort_finish<false>, dim3(ntiles * (kSortTile / kFinishItems)), dim3(256), 0, s, d_segs,
-                           (const uint32_t *)d_tile, (const uint64_t *)words0, (const uint64_t *)words1);
+    hipLaunchKernelGGL(k_sort_finish, dim3(ntiles * (kSortTile / kFinishItems)), dim3(256), 0, s, d_segs,
+                       (const uint32_t *)d_tile, (const uint64_t *)words0, (const uint64_t *)words1);
     hipLaunchKernelGGL(k_sort_rescue, dim3(nseg), dim3(256), 0, s, d_segs, (const SortBatch *)d_batch, N, keys0,
                        keys1, idx0, idx1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
