@@ -269,23 +269,6 @@ __device__ __forceinline__ const uint8_t *unique_elem(const Stream &st, uint32_t
     return c.elem(idx, vs);
 }
 
-// Persistent workgroups over the tiles, taken in ticket order, three in
-// flight per workgroup: while tile t is ranked and stored, tile t+1's values
-// are already loading into registers (its split was read during tile t-1)
-// and tile t+2's split is loading. Two merged elements per thread (tile
-// order: its A elements, then its B elements; thread i owns elements i and
-// i + 512). A workgroup's HBM latency is thus hidden behind its own work,
-// which is what matters beside the tails' chain workgroups (one merge
-// workgroup per such CU: the chain's T-tables leave 24 KiB of LDS).
-constexpr uint32_t kUniqueE = kUniqueTile / kUniqueThreads;
-
-struct UniqueSide { // a tile's inputs as a thread sees them (every field uniform)
-    int ji;         // job, or -1 (no tile)
-    uint32_t t;     // tile of the job
-    UniqueSplit s0; // its split
-    uint32_t ia1;   // the next split's A count
-};
-
 // Byte offset of key limb l in a value (keys.h load_key's order).
 template <int KIND> __device__ __forceinline__ uint32_t key_limb_off(int l, uint32_t ts) {
     if constexpr (KIND == kKeyTimestamp) return ts;
@@ -294,32 +277,95 @@ template <int KIND> __device__ __forceinline__ uint32_t key_limb_off(int l, uint
     else return l == 0 ? 16u : 8u * (l - 1);
 }
 
+// The 8-byte word at byte `off` (< 32, a multiple of 8) of a value whose first
+// 32 bytes are v0, v1.
 __device__ __forceinline__ uint64_t word_of(const u32x4 &v0, const u32x4 &v1, uint32_t off) {
     const u32x4 &v = off < 16 ? v0 : v1;
     return (off & 8) ? ((uint64_t)v.w << 32 | v.z) : ((uint64_t)v.y << 32 | v.x);
 }
 
+// One tile, two merged elements per thread (tile order: its A elements, then
+// its B elements; thread t owns elements t and t + 512). Both values are
+// loaded with their keys before the workgroup's barrier, so their HBM latency
+// overlaps the ranking; pointers come from the split's resolved segments (a
+// tile spans one or two input blocks), not a search of the segment tables.
 template <int KIND>
-__device__ __forceinline__ void unique_rank_store(uint8_t *lds, const JobDesc &j, const UniqueSide &u,
-                                                  const uint8_t *const *src, const u32x4 *v0, const u32x4 *v1,
-                                                  bool &bad) {
+__device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j, uint32_t t,
+                                                  const UniqueSplit *usplits, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
-    constexpr uint32_t NT = kUniqueThreads, R = kUniqueRow, E = kUniqueE;
+    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, R = kUniqueRow, E = T / NT;
+    static_assert(T == E * NT, "whole elements per thread");
+    uint32_t &s_bad = *(uint32_t *)lds;
     uint64_t *s_key = (uint64_t *)(lds + 16);
-    const uint8_t *s_tomb = lds + 16 + KL * R * 8;
+    uint8_t *s_tomb = lds + 16 + KL * R * 8;
     const uint32_t tid = threadIdx.x;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
-    const uint32_t d0 = u.t * kUniqueTile, d1 = d0 + kUniqueTile < n ? d0 + kUniqueTile : n;
-    const uint32_t ia0 = u.s0.i, ia1 = u.ia1, jb0 = d0 - ia0, jb1 = d1 - ia1;
-    const uint32_t na = ia1 - ia0, nb = jb1 - jb0, m = na + nb, eb = na + 1;
-    const uint32_t vs = j.value_size, vcm = j.vcm;
+    const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
+    const UniqueSplit s0 = usplits[j.usplit_base + t];
+    const uint32_t ia0 = s0.i, ia1 = usplits[j.usplit_base + t + 1].i;
+    const uint32_t jb0 = d0 - ia0, jb1 = d1 - ia1;
+    const uint32_t na = ia1 - ia0, nb = jb1 - jb0, m = na + nb;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
     const bool drop = j.drop_tombstones != 0;
+    const uint32_t eb = na + 1; // entry of B[jb0 - 1]
+    if (tid == 0) s_bad = 0;
+    auto put_entry = [&](uint32_t e, const Key<KL> &k) {
+#pragma unroll
+        for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
+    };
+    auto elem_of = [&](bool is_a, uint32_t idx) {
+        return is_a ? unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, idx, vs)
+                    : unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, idx, vs);
+    };
+    // This thread's elements: their values' first 32 bytes into registers, keys into LDS.
+    const uint8_t *src[E];
+    u32x4 v0[E], v1[E];
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        const bool is_a = e < na;
+        src[q] = e < m ? elem_of(is_a, is_a ? ia0 + e : jb0 + (e - na)) : nullptr;
+        v0[q] = v1[q] = u32x4{0, 0, 0, 0};
+        if (e < m) {
+            v0[q] = gld<u32x4>(src[q]);
+            if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
+        }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        if (e >= m) continue;
+        const bool is_a = e < na;
+        put_entry(is_a ? 1 + e : e + 2, load_key<KIND>(src[q], ts));
+        if (is_a) s_tomb[1 + e] = (uint8_t)load_tomb(src[q], ts);
+    }
+    // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (sentinel: all ones).
+    if (tid < 3) {
+        const bool bside = tid != 0;
+        const Stream &st = bside ? j.b : j.a;
+        const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
+        const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
+        Key<KL> k;
+#pragma unroll
+        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
+        uint8_t tb = 0;
+        if (bi >= 0 && bi < (int64_t)st.n) {
+            const uint8_t *p = elem_of(!bside, (uint32_t)bi);
+            k = load_key<KIND>(p, ts);
+            if (!bside) tb = (uint8_t)load_tomb(p, ts);
+        }
+        put_entry(e, k);
+        if (!bside) s_tomb[0] = tb;
+    }
+    __syncthreads();
     auto entry = [&](uint32_t e) {
         Key<KL> k;
 #pragma unroll
         for (int l = 0; l < KL; l++) k.l[l] = s_key[l * R + e];
         return k;
     };
+    bool bad = false;
+    const uint32_t vcm = j.vcm;
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
@@ -360,188 +406,27 @@ __device__ __forceinline__ void unique_rank_store(uint8_t *lds, const JobDesc &j
         if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
         for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
     }
-}
-
-// Keys (and A tombstones) of the tile into LDS: its elements' from the
-// registers when the key lies in a value's first 32 bytes, and the three
-// boundary entries A[ia0 - 1], B[jb0 - 1], B[jb1] (sentinel: all ones).
-template <int KIND>
-__device__ __forceinline__ void unique_keys(uint8_t *lds, const JobDesc &j, const UniqueSide &u,
-                                            const uint8_t *const *src, const u32x4 *v0, const u32x4 *v1) {
-    constexpr int KL = KeyLimbs<KIND>::value;
-    constexpr uint32_t NT = kUniqueThreads, R = kUniqueRow, E = kUniqueE;
-    uint64_t *s_key = (uint64_t *)(lds + 16);
-    uint8_t *s_tomb = lds + 16 + KL * R * 8;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t n = j.a.n + j.b.n;
-    const uint32_t d0 = u.t * kUniqueTile, d1 = d0 + kUniqueTile < n ? d0 + kUniqueTile : n;
-    const uint32_t ia0 = u.s0.i, ia1 = u.ia1, jb0 = d0 - ia0, jb1 = d1 - ia1;
-    const uint32_t na = ia1 - ia0, nb = jb1 - jb0, m = na + nb, eb = na + 1;
-    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
-    const bool in_regs = vs >= 32 && ts + 8 <= 32; // every limb and the tombstone bit (uniform)
-    auto put_entry = [&](uint32_t e, const Key<KL> &k) {
-#pragma unroll
-        for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
-    };
-#pragma unroll
-    for (uint32_t q = 0; q < E; q++) {
-        const uint32_t e = tid + q * NT;
-        if (e >= m) continue;
-        const bool is_a = e < na;
-        Key<KL> k;
-        uint32_t tb;
-        if (in_regs) {
-#pragma unroll
-            for (int l = 0; l < KL; l++) {
-                k.l[l] = word_of(v0[q], v1[q], key_limb_off<KIND>(l, ts));
-                if (l == 0 && KIND != kKeyIdU128) k.l[l] &= ~kTombstoneBit;
-            }
-            tb = (uint32_t)(word_of(v0[q], v1[q], ts) >> 63);
-        } else {
-            k = load_key<KIND>(src[q], ts);
-            tb = load_tomb(src[q], ts);
-        }
-        put_entry(is_a ? 1 + e : e + 2, k);
-        if (is_a) s_tomb[1 + e] = (uint8_t)tb;
-    }
-    if (tid < 3) {
-        const bool bside = tid != 0;
-        const Stream &st = bside ? j.b : j.a;
-        const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
-        const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
-        uint8_t tb = 0;
-        if (bi >= 0 && bi < (int64_t)st.n) {
-            const uint8_t *p = bside ? unique_elem(j.b, u.s0.seg_b, u.s0.b_ptr, u.s0.b_lo, u.s0.b_hi, (uint32_t)bi, vs)
-                                     : unique_elem(j.a, u.s0.seg_a, u.s0.a_ptr, u.s0.a_lo, u.s0.a_hi, (uint32_t)bi, vs);
-            k = load_key<KIND>(p, ts);
-            if (!bside) tb = (uint8_t)load_tomb(p, ts);
-        }
-        put_entry(e, k);
-        if (!bside) s_tomb[0] = tb;
+    if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    if (tid == 0 && s_bad) {
+        __hip_atomic_store(&res[j.job_index].spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
-                                                                 const UniqueSplit *usplits, JobResultDev *res,
-                                                                 uint32_t *ticket, uint32_t zero) {
+                                                                 const UniqueSplit *usplits, JobResultDev *res) {
     extern __shared__ __attribute__((aligned(16))) uint8_t unique_lds[];
-    __shared__ uint32_t s_tk[2];
-    uint32_t &s_bad = *(uint32_t *)unique_lds;
-    constexpr uint32_t NT = kUniqueThreads, E = kUniqueE;
-    const uint32_t tid = threadIdx.x;
-    // A tile's job and split. The split is read with per-lane (vector) loads
-    // (`zero` keeps the address divergent to the compiler): a scalar load
-    // shares the LDS's wait counter and would stall the ranking loop.
-    auto side_of = [&](uint32_t g, UniqueSide &u) {
-        u.ji = -1;
-        if (g >= total) return;
-        const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
-        const JobDesc &j = jobs[ji];
-        if (!j.unique || g - j.utile_base >= j.utile_count) return;
-        u.ji = ji;
-        u.t = g - j.utile_base;
-        const UniqueSplit *sp = usplits + j.usplit_base + u.t + zero * tid;
-        u.s0 = sp[0];
-        u.ia1 = sp[1].i;
-    };
-    auto uniform = [](const UniqueSide &v) {
-        UniqueSide u;
-        u.ji = __builtin_amdgcn_readfirstlane(v.ji);
-        u.t = __builtin_amdgcn_readfirstlane(v.t);
-        u.ia1 = __builtin_amdgcn_readfirstlane(v.ia1);
-        const uint32_t *w = (const uint32_t *)&v.s0;
-        uint32_t *o = (uint32_t *)&u.s0;
-#pragma unroll
-        for (uint32_t i = 0; i < sizeof(UniqueSplit) / 4; i++) o[i] = __builtin_amdgcn_readfirstlane(w[i]);
-        return u;
-    };
-    // Issue the loads of a tile's values (first 32 bytes) into registers.
-    auto fetch = [&](const UniqueSide &u, const uint8_t **src, u32x4 *v0, u32x4 *v1) {
-#pragma unroll
-        for (uint32_t q = 0; q < E; q++) src[q] = nullptr;
-        if (u.ji < 0) return;
-        const JobDesc &j = jobs[u.ji];
-        const uint32_t n = j.a.n + j.b.n, vs = j.value_size;
-        const uint32_t d0 = u.t * kUniqueTile, d1 = d0 + kUniqueTile < n ? d0 + kUniqueTile : n;
-        const uint32_t ia0 = u.s0.i, na = u.ia1 - ia0, jb0 = d0 - ia0, m = d1 - d0;
-#pragma unroll
-        for (uint32_t q = 0; q < E; q++) {
-            const uint32_t e = tid + q * NT;
-            if (e >= m) continue;
-            src[q] = e < na ? unique_elem(j.a, u.s0.seg_a, u.s0.a_ptr, u.s0.a_lo, u.s0.a_hi, ia0 + e, vs)
-                            : unique_elem(j.b, u.s0.seg_b, u.s0.b_ptr, u.s0.b_lo, u.s0.b_hi, jb0 + (e - na), vs);
-            v0[q] = gld<u32x4>(src[q]);
-            if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
-        }
-    };
-
-    if (tid == 0) {
-        s_tk[0] = atomicAdd(ticket, 1u);
-        s_tk[1] = atomicAdd(ticket, 1u);
-    }
-    __syncthreads();
-    UniqueSide cur, nxt, nxt2;
-    side_of(s_tk[0], cur);
-    side_of(s_tk[1], nxt);
-    cur = uniform(cur);
-    nxt = uniform(nxt);
-    const uint8_t *src[E], *nsrc[E];
-    u32x4 v0[E], v1[E], n0[E], n1[E];
-#pragma unroll
-    for (uint32_t q = 0; q < E; q++) v0[q] = v1[q] = n0[q] = n1[q] = u32x4{0, 0, 0, 0};
-    uint32_t g_cur = s_tk[0], g_nxt = s_tk[1];
-    __syncthreads(); // every thread has its first two tickets
-    fetch(cur, src, v0, v1);
-    while (g_cur < total) {
-        // (The previous tile's readers of s_tk and LDS are past the closing barrier.)
-        if (tid == 0) {
-            s_tk[0] = atomicAdd(ticket, 1u);
-            s_bad = 0;
-        }
-        if (cur.ji >= 0) {
-            const JobDesc &j = jobs[cur.ji];
-            switch (j.key_kind) {
-            case kKeyTimestamp: unique_keys<kKeyTimestamp>(unique_lds, j, cur, src, v0, v1); break;
-            case kKeyIdU128: unique_keys<kKeyIdU128>(unique_lds, j, cur, src, v0, v1); break;
-            case kKeyCompositeU64: unique_keys<kKeyCompositeU64>(unique_lds, j, cur, src, v0, v1); break;
-            default: unique_keys<kKeyCompositeU128>(unique_lds, j, cur, src, v0, v1); break;
-            }
-        }
-        __syncthreads();
-        const uint32_t g_nxt2 = s_tk[0];
-        fetch(nxt, nsrc, n0, n1); // tile t+1's values: in flight during tile t's ranking
-        side_of(g_nxt2, nxt2);    // tile t+2's split
-        bool bad = false;
-        if (cur.ji >= 0) {
-            const JobDesc &j = jobs[cur.ji];
-            switch (j.key_kind) {
-            case kKeyTimestamp: unique_rank_store<kKeyTimestamp>(unique_lds, j, cur, src, v0, v1, bad); break;
-            case kKeyIdU128: unique_rank_store<kKeyIdU128>(unique_lds, j, cur, src, v0, v1, bad); break;
-            case kKeyCompositeU64: unique_rank_store<kKeyCompositeU64>(unique_lds, j, cur, src, v0, v1, bad); break;
-            default: unique_rank_store<kKeyCompositeU128>(unique_lds, j, cur, src, v0, v1, bad); break;
-            }
-        }
-        if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
-        __syncthreads();
-        if (tid == 0 && s_bad && cur.ji >= 0) {
-            const JobDesc &j = jobs[cur.ji];
-            __hip_atomic_store(&res[j.job_index].spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // Shift the pipeline: t+1 becomes current, t+2 next.
-        cur = nxt;
-        g_cur = g_nxt;
-#pragma unroll
-        for (uint32_t q = 0; q < E; q++) {
-            src[q] = nsrc[q];
-            v0[q] = n0[q];
-            v1[q] = n1[q];
-        }
-        nxt = uniform(nxt2); // its loads landed during the ranking: into scalar registers
-        g_nxt = g_nxt2;
+    const uint32_t g = blockIdx.x;
+    const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
+    const JobDesc &j = jobs[ji];
+    if (!j.unique || g - j.utile_base >= j.utile_count) return; // uniform
+    const uint32_t t = g - j.utile_base;
+    switch (j.key_kind) {
+    case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
+    case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
+    case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
+    default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
     }
 }
 
@@ -561,10 +446,9 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     int kl = 1; // the widest key among the launch's speculated jobs
     for (int i = 0; i < njobs; i++)
         if (h_jobs[i].unique) kl = std::max(kl, h_jobs[i].key_kind == kKeyTimestamp ? 1 : h_jobs[i].key_kind == kKeyCompositeU128 ? 3 : 2);
-    // Persistent: two workgroups per CU (registers), one beside a chain workgroup.
-    const uint32_t grid = ntiles < 512 ? ntiles : 512;
-    hipLaunchKernelGGL(k_merge_unique, dim3(grid), dim3(kUniqueThreads), unique_lds_bytes(kl), s, d_jobs, njobs,
-                       ntiles, (const UniqueSplit *)d_usplits, d_results, d_ticket, 0u);
+    (void)d_ticket;
+    hipLaunchKernelGGL(k_merge_unique, dim3(ntiles), dim3(kUniqueThreads), unique_lds_bytes(kl), s, d_jobs, njobs,
+                       ntiles, (const UniqueSplit *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;

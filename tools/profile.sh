@@ -12,8 +12,8 @@ TAG=${1:?usage: profile.sh TAG}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 CFG=${CONFIG:-2}
-ARGS="--config $CFG --steps 10 --warmup 3"
-SHORT="--config $CFG --steps 3 --warmup 1"
+ARGS="--config $CFG --steps 10 --warmup 3 ${BENCH_ARGS:-}"
+SHORT="--config $CFG --steps 3 --warmup 1 ${BENCH_ARGS:-}"
 timeout -k 10 240 python -u bench.py $ARGS > $OUT/bench.log 2>&1
 tail -1 $OUT/bench.log > $OUT/bench.json
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 -u bench.py $ARGS --no-cpu-baseline > $OUT/trace.log 2>&1
