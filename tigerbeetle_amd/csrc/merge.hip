@@ -35,6 +35,13 @@
 
 namespace tbc {
 
+// TBC_LB_BACKOFF (A/B measurement): 8-tick sleeps between the assembling
+// merge's look-back polls.
+static uint32_t lookback_backoff() {
+    static const uint32_t v = getenv("TBC_LB_BACKOFF") ? (uint32_t)atoi(getenv("TBC_LB_BACKOFF")) : 1u;
+    return v;
+}
+
 int staged_variant() {
     static const int v = getenv("TBC_STAGED") ? atoi(getenv("TBC_STAGED")) : 0;
     return v == 2 ? 2 : (v != 0 ? 1 : 0);
@@ -414,19 +421,25 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     }
 }
 
+// `per_wg` consecutive tiles per workgroup (fewer, longer-lived workgroups).
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
-                                                                 const UniqueSplit *usplits, JobResultDev *res) {
+                                                                 const UniqueSplit *usplits, JobResultDev *res,
+                                                                 uint32_t per_wg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t unique_lds[];
-    const uint32_t g = blockIdx.x;
-    const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
-    const JobDesc &j = jobs[ji];
-    if (!j.unique || g - j.utile_base >= j.utile_count) return; // uniform
-    const uint32_t t = g - j.utile_base;
-    switch (j.key_kind) {
-    case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
-    case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
-    case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
-    default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
+    for (uint32_t i = 0; i < per_wg; i++) {
+        const uint32_t g = blockIdx.x * per_wg + i;
+        if (g >= total) return;
+        const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
+        const JobDesc &j = jobs[ji];
+        if (!j.unique || g - j.utile_base >= j.utile_count) continue; // uniform
+        const uint32_t t = g - j.utile_base;
+        if (i) __syncthreads(); // the previous tile's LDS readers are done
+        switch (j.key_kind) {
+        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
+        case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
+        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
+        default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
+        }
     }
 }
 
@@ -447,8 +460,11 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     for (int i = 0; i < njobs; i++)
         if (h_jobs[i].unique) kl = std::max(kl, h_jobs[i].key_kind == kKeyTimestamp ? 1 : h_jobs[i].key_kind == kKeyCompositeU128 ? 3 : 2);
     (void)d_ticket;
-    hipLaunchKernelGGL(k_merge_unique, dim3(ntiles), dim3(kUniqueThreads), unique_lds_bytes(kl), s, d_jobs, njobs,
-                       ntiles, (const UniqueSplit *)d_usplits, d_results);
+    // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
+    static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
+    const uint32_t pw = per_wg < 1 ? 1 : per_wg;
+    hipLaunchKernelGGL(k_merge_unique, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads), unique_lds_bytes(kl), s,
+                       d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results, pw);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;
@@ -967,7 +983,7 @@ template <int KIND>
 __global__ __launch_bounds__(kAsmThreads) void k_merge_assemble(const JobDesc *jobs, const TileRef *order,
                                                                 uint32_t order_offset, const SplitDesc *splits,
                                                                 uint64_t *lookback, uint32_t *ticket, uint32_t *ready,
-                                                                JobResultDev *res) {
+                                                                JobResultDev *res, uint32_t backoff) {
     constexpr int KL = KeyLimbs<KIND>::value;
     constexpr uint32_t NT = kAsmThreads, E = kAsmE;
     __shared__ uint64_t s_key[KL][kAsmTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
@@ -1168,7 +1184,7 @@ __global__ __launch_bounds__(kAsmThreads) void k_merge_assemble(const JobDesc *j
                     if (lane == 0) gst<uint32_t>(&res[j.job_index].invariant, 0xbeefu);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                for (uint32_t z = 0; z < backoff; z++) __builtin_amdgcn_s_sleep(8); // spinning lanes poll HBM-side lines
                 continue;
             }
             uint64_t c = in ? (w & kCnt) : 0;
@@ -1317,7 +1333,7 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
     else if (ntiles && d_lookback && f.merge_tile == kAsmTile && staged_variant() == 2)
         hipLaunchKernelGGL((k_merge_assemble<KIND>), dim3(ntiles), dim3(kAsmThreads), 0, s, d_jobs, d_order, tile_off,
                            (const SplitDesc *)d_splits, d_lookback, d_ticket + KIND, d_ready,
-                           const_cast<JobResultDev *>(d_res));
+                           const_cast<JobResultDev *>(d_res), lookback_backoff());
     else if (ntiles && d_lookback)
         hipLaunchKernelGGL((k_merge_staged<KIND>), dim3(ntiles), dim3(kStagedThreads), 0, s, d_jobs, d_order, tile_off,
                            (const SplitDesc *)d_splits, d_lookback, d_ticket + KIND, d_ready,
