@@ -2147,13 +2147,15 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
     if (total_dblocks) {
         if (waves <= 1024) { // latency regime: one chain per SIMD, round keys by VALU lane moves
             // A chain workgroup holds a whole CU's LDS (the tables), so
-            // concurrent tails share the chip by CUs: pack four chains per
-            // CU (one per SIMD), more once a batch alone would take over a
-            // third of the CUs.
+            // concurrent tails share the chip by CUs: pack four chain waves
+            // per CU (one per SIMD), eight (two per SIMD, the chains' best
+            // throughput) once a batch alone would take over half the CUs,
+            // so that two consecutive batches' tails fill the chip (config 2:
+            // 8 vs 12 waves, 1.98–2.02 vs 2.01–2.05 ms per step over three
+            // calls, gpurun_out/r04).
             // TBC_TAIL_CHAINS (A/B measurement): chain waves per workgroup.
             static const uint32_t forced = getenv("TBC_TAIL_CHAINS") ? (uint32_t)atoi(getenv("TBC_TAIL_CHAINS")) : 0u;
-            uint32_t c = (waves + 85) / 86;
-            c = c < 4 ? 4 : (c > 16 ? 16 : (c + 3) & ~3u);
+            uint32_t c = waves > 512 ? 8u : 4u;
             if (forced) c = forced < 1 ? 1 : (forced > 16 ? 16 : forced);
             if (c > waves) c = waves;
             // Two or more chains per SIMD share its VALU issue: the round key by
