@@ -119,7 +119,7 @@ def test_back_to_back_speculated_batches_share_outputs(engine, oracle_lib):
 @pytest.mark.gpu
 def test_speculated_batches_pipelined_three_in_flight(engine, oracle_lib):
     """Round 4: a UNIQUE_KEYS batch submitted while an earlier batch's tail is
-    running is pipelined (bodies merged by k_produce_unique on the engine
+    running is pipelined (bodies merged by k_merge_unique on the engine
     stream, chains on a tail stream beside the earlier batches' chains).
     Three batches into three output sets, then a fourth into the first set
     (it must wait for the first batch's tail), submitted without waiting;

@@ -1,8 +1,10 @@
 """TBC_COMPACTION_UNIQUE_KEYS (include/tbc.h): the speculated block pass.
 
-A job flagged UNIQUE_KEYS skips the merge pass: each data block's producer
-merges its own positions while its AEGIS chain absorbs them (aegis.hip
-produce_unique). Whether the speculation holds (no repeated key, no dropped
+A job flagged UNIQUE_KEYS skips the merge pass: in the fused latency pass
+each data block's producer merges its own positions while its AEGIS chain
+absorbs them (aegis.hip produce_unique); in the pipelined pass the bodies
+are merged tile by tile on the engine stream (merge.hip k_merge_unique) and
+the chains run on a tail stream. Whether the speculation holds (no repeated key, no dropped
 tombstone: every value survives) or breaks (then the batch's second phase
 recomputes the job through the merge path), every output block's on-disk
 image and every TableInfo must equal the oracle's restatement of
@@ -22,7 +24,7 @@ pytestmark = pytest.mark.gpu
 def eng_small(request, engine_small, engine_small_pipe):
     """Both block passes of a speculated batch (engine.hip submit_impl): the
     fused latency pass (a batch alone), and the pipelined one (bodies merged
-    by k_produce_unique on the engine stream, chains on a tail stream)."""
+    by k_merge_unique on the engine stream, chains on a tail stream)."""
     return engine_small if request.param == "fused" else engine_small_pipe
 
 

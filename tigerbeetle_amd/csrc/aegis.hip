@@ -910,19 +910,6 @@ __device__ __forceinline__ void finish_data_block(const uint32_t *sT, uint32_t *
     __builtin_amdgcn_wave_barrier();
 }
 
-// Key of lane `src` (ds_bpermute of each 32-bit half; the whole wave active).
-template <int KL> __device__ __forceinline__ Key<KL> key_of_lane(const Key<KL> &k, uint32_t src) {
-    Key<KL> r;
-    const int addr = (int)(src << 2);
-#pragma unroll
-    for (int l = 0; l < KL; l++) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)k.l[l]);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(k.l[l] >> 32));
-        r.l[l] = (uint64_t)hi << 32 | lo;
-    }
-    return r;
-}
-
 // Producer of a speculated job (TBC_COMPACTION_UNIQUE_KEYS): no merge pass ran.
 // If no key occurs twice in A u B and no tombstone is dropped, every value
 // survives (compaction.zig:483-559 dedup and :757-798 merge rules all keep

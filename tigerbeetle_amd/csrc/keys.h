@@ -58,4 +58,17 @@ __device__ __forceinline__ Key<KeyLimbs<KIND>::value> load_key(const uint8_t *v,
     return k;
 }
 
+// Key of lane `src` (ds_bpermute of each 32-bit half; the whole wave active).
+template <int KL> __device__ __forceinline__ Key<KL> key_of_lane(const Key<KL> &k, uint32_t src) {
+    Key<KL> r;
+    const int addr = (int)(src << 2);
+#pragma unroll
+    for (int l = 0; l < KL; l++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)k.l[l]);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(k.l[l] >> 32));
+        r.l[l] = (uint64_t)hi << 32 | lo;
+    }
+    return r;
+}
+
 } // namespace tbc
