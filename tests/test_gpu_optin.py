@@ -48,18 +48,3 @@ def test_assembling_merge_bit_exact():
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout, tail
-
-
-@pytest.mark.gpu
-def test_wave_merge_bit_exact():
-    """TBC_UNIQUE_WAVE=1: speculated jobs' bodies by the wave merge
-    (k_merge_unique_wave: one wave per tile, 64-position windows, no LDS) in
-    pipelined and grid batches, held and broken speculations, compared with
-    the oracle."""
-    env = dict(os.environ, TBC_UNIQUE_WAVE="1")
-    files = [os.path.join(HERE, f) for f in ("test_gpu_unique.py", "test_gpu_overlap.py", "test_gpu_grid.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", *files],
-                       env=env, capture_output=True, text=True, timeout=230)
-    tail = (r.stdout + r.stderr)[-3000:]
-    assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " failed" not in r.stdout, tail

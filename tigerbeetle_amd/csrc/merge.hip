@@ -443,152 +443,6 @@ __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *
     }
 }
 
-// Wave merge (TBC_UNIQUE_WAVE=1, A/B): one wave per 1,024-position tile and
-// no LDS at all, so the front is not limited to the one workgroup a chain
-// workgroup's T-tables leave room for. The wave walks its tile in windows of
-// 64 merged positions from the tile's split: lane l holds the window's
-// candidates A[ia + l] and B[jb + l] (first 32 bytes of each value, its key
-// taken from them), ranks each against the other side's candidates by a
-// binary search over lanes (ds_bpermute), and stores the candidates whose
-// merged position falls in the window; the split then advances by the A and
-// B values stored. Speculation checks as merge_unique_tile's.
-template <int KIND>
-__device__ __forceinline__ void unique_wave_tile(const JobDesc &j, uint32_t t, const UniqueSplit *usplits,
-                                                 JobResultDev *res) {
-    constexpr int KL = KeyLimbs<KIND>::value;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
-    const uint32_t d0 = t * kUniqueTile, d1 = d0 + kUniqueTile < n ? d0 + kUniqueTile : n;
-    const UniqueSplit s0 = usplits[j.usplit_base + t];
-    const uint32_t ia_end = usplits[j.usplit_base + t + 1].i, jb_end = d1 - ia_end;
-    const uint32_t vs = j.value_size, ts = j.timestamp_offset, vcm = j.vcm;
-    const bool drop = j.drop_tombstones != 0;
-    constexpr uint32_t kMaxOff = KIND == kKeyTimestamp ? 0u : (KIND == kKeyCompositeU128 ? 16u : 8u);
-    const uint32_t reg_bytes = vs < 32 ? vs : 32u;
-    const bool in_regs = (KIND == kKeyTimestamp ? ts : (kMaxOff > ts ? kMaxOff : ts)) + 8 <= reg_bytes;
-    auto elem_a = [&](uint32_t i) { return unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, i, vs); };
-    auto elem_b = [&](uint32_t i) { return unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, i, vs); };
-    auto key_at = [&](const uint8_t *p, const u32x4 &v0, const u32x4 &v1) {
-        Key<KL> k;
-        if (in_regs) {
-#pragma unroll
-            for (int l = 0; l < KL; l++) {
-                k.l[l] = word_of(v0, v1, key_limb_off<KIND>(l, ts));
-                if (l == 0 && KIND != kKeyIdU128) k.l[l] &= ~kTombstoneBit;
-            }
-        } else {
-            k = load_key<KIND>(p, ts);
-        }
-        return k;
-    };
-    uint32_t ia = s0.i, jb = d0 - s0.i, p = d0;
-    // Keys before the tile on both sides, and the first B after it.
-    Key<KL> prev_a, prev_b, next_b;
-    const bool has_prev_a0 = ia > 0, has_prev_b0 = jb > 0, has_next_b = jb_end < nb_all;
-    if (has_prev_a0) prev_a = load_key<KIND>(elem_a(ia - 1), ts);
-    if (has_prev_b0) prev_b = load_key<KIND>(elem_b(jb - 1), ts);
-    if (has_next_b) next_b = load_key<KIND>(elem_b(jb_end), ts);
-    bool has_prev_a = has_prev_a0, has_prev_b = has_prev_b0;
-    bool bad = false;
-    while (p < d1) {
-        const uint32_t wsz = d1 - p < 64 ? d1 - p : 64;
-        const uint32_t nav = ia_end - ia < 64 ? ia_end - ia : 64, nbv = jb_end - jb < 64 ? jb_end - jb : 64;
-        const bool va = lane < nav, vb = lane < nbv;
-        const uint8_t *pa = va ? elem_a(ia + lane) : nullptr;
-        const uint8_t *pb = vb ? elem_b(jb + lane) : nullptr;
-        u32x4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0}, b0 = {0, 0, 0, 0}, b1 = {0, 0, 0, 0};
-        if (va) {
-            a0 = gld<u32x4>(pa);
-            if (vs >= 32) a1 = gld<u32x4>(pa + 16);
-        }
-        if (vb) {
-            b0 = gld<u32x4>(pb);
-            if (vs >= 32) b1 = gld<u32x4>(pb + 16);
-        }
-        Key<KL> ka, kb;
-#pragma unroll
-        for (int l = 0; l < KL; l++) ka.l[l] = kb.l[l] = ~0ull;
-        if (va) ka = key_at(pa, a0, a1);
-        if (vb) kb = key_at(pb, b0, b1);
-        // A's rank among the B candidates (lower bound), B's among the A
-        // candidates (upper bound: A first on equal keys); 7 halvings cover 64.
-        uint32_t lo_a = 0, hi_a = nbv, lo_b = 0, hi_b = nav;
-#pragma unroll
-        for (int step = 0; step < 7; step++) {
-            const uint32_t ma = (lo_a + hi_a) >> 1, mb = (lo_b + hi_b) >> 1;
-            const Key<KL> at_b = key_of_lane(kb, ma < 63 ? ma : 63);
-            const Key<KL> at_a = key_of_lane(ka, mb < 63 ? mb : 63);
-            if (lo_a < hi_a) {
-                if (key_lt(at_b, ka)) lo_a = ma + 1;
-                else hi_a = ma;
-            }
-            if (lo_b < hi_b) {
-                if (key_le(at_a, kb)) lo_b = mb + 1;
-                else hi_b = mb;
-            }
-        }
-        const uint32_t r_b = lo_a, r_a = lo_b;
-        const bool a_in = va && lane + r_b < wsz, b_in = vb && lane + r_a < wsz;
-        const uint32_t x = (uint32_t)__builtin_popcountll(__ballot(a_in)), y = wsz - x;
-        // Speculation checks of the window's outputs.
-        const Key<KL> b_at = key_of_lane(kb, r_b < 63 ? r_b : 63);
-        const Key<KL> a_left = key_of_lane(ka, lane ? lane - 1 : 0);
-        const Key<KL> b_left = key_of_lane(kb, lane ? lane - 1 : 0);
-        if (a_in) {
-            bad |= r_b < nbv ? key_eq(b_at, ka) : (has_next_b && key_eq(next_b, ka));
-            bad |= lane ? key_eq(a_left, ka) : (has_prev_a && key_eq(prev_a, ka));
-            bad |= drop && (in_regs ? (word_of(a0, a1, ts) >> 63) != 0 : load_tomb(pa, ts) != 0);
-        }
-        if (b_in) bad |= lane ? key_eq(b_left, kb) : (has_prev_b && key_eq(prev_b, kb));
-        // Stores.
-        auto put = [&](uint32_t g, const uint8_t *src, const u32x4 &v0, const u32x4 &v1) {
-            const uint32_t k = g / vcm;
-            uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(g - k * vcm) * vs;
-            gst<u32x4>(dst, v0);
-            if (vs >= 32) gst<u32x4>(dst + 16, v1);
-            for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src + c));
-        };
-        if (a_in) put(p + lane + r_b, pa, a0, a1);
-        if (b_in) put(p + lane + r_a, pb, b0, b1);
-        // The window's last stored A and B become the next window's left neighbours.
-        if (x) {
-            prev_a = key_of_lane(ka, x - 1);
-            has_prev_a = true;
-        }
-        if (y) {
-            prev_b = key_of_lane(kb, y - 1);
-            has_prev_b = true;
-        }
-        ia += x;
-        jb += y;
-        p += wsz;
-    }
-    if (__any(bad) && lane == 0) {
-        __hip_atomic_store(&res[j.job_index].spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-constexpr uint32_t kWaveMergeWaves = 4;
-
-__global__ __launch_bounds__(64 * kWaveMergeWaves) void k_merge_unique_wave(const JobDesc *jobs, int njobs,
-                                                                            uint32_t total,
-                                                                            const UniqueSplit *usplits,
-                                                                            JobResultDev *res) {
-    const uint32_t g = blockIdx.x * kWaveMergeWaves + (threadIdx.x >> 6);
-    if (g >= total) return; // wave-uniform; no workgroup barrier below
-    const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
-    const JobDesc &j = jobs[ji];
-    if (!j.unique || g - j.utile_base >= j.utile_count) return;
-    const uint32_t t = g - j.utile_base;
-    switch (j.key_kind) {
-    case kKeyTimestamp: unique_wave_tile<kKeyTimestamp>(j, t, usplits, res); break;
-    case kKeyIdU128: unique_wave_tile<kKeyIdU128>(j, t, usplits, res); break;
-    case kKeyCompositeU64: unique_wave_tile<kKeyCompositeU64>(j, t, usplits, res); break;
-    default: unique_wave_tile<kKeyCompositeU128>(j, t, usplits, res); break;
-    }
-}
-
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
                         JobResultDev *d_results, uint32_t *d_ticket, void *stream, void (*mark)(void *, const char *),
                         void *mark_ctx) {
@@ -606,16 +460,6 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     for (int i = 0; i < njobs; i++)
         if (h_jobs[i].unique) kl = std::max(kl, h_jobs[i].key_kind == kKeyTimestamp ? 1 : h_jobs[i].key_kind == kKeyCompositeU128 ? 3 : 2);
     (void)d_ticket;
-    // TBC_UNIQUE_WAVE=1 (A/B measurement): the wave merge.
-    static const bool wave = getenv("TBC_UNIQUE_WAVE") != nullptr;
-    if (wave) {
-        hipLaunchKernelGGL(k_merge_unique_wave, dim3((ntiles + kWaveMergeWaves - 1) / kWaveMergeWaves),
-                           dim3(64 * kWaveMergeWaves), 0, s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits,
-                           d_results);
-        if (hipGetLastError() != hipSuccess) return -1;
-        if (mark) mark(mark_ctx, "merge_unique");
-        return 0;
-    }
     // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
     static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
     const uint32_t pw = per_wg < 1 ? 1 : per_wg;

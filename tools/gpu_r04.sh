@@ -61,9 +61,6 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     t8w2) run t8w2 TBC_UNIQUE_PER_WG=2 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
     t8w4) run t8w4 TBC_UNIQUE_PER_WG=4 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
     c5ab8) run c5ab8 TBC_STAGED=2 TBC_LB_BACKOFF=8 $B --depth 3 --config 5 --no-cpu-baseline ;;
-    p1v) run p1v TBC_UNIQUE_WAVE=1 $B --depth 1 --pipeline on --no-cpu-baseline ;;
-    d3v) run d3v TBC_UNIQUE_WAVE=1 $B --depth 3 --no-cpu-baseline ;;
-    c1v) run c1v TBC_UNIQUE_WAVE=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
