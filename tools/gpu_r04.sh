@@ -61,6 +61,9 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     t8w2) run t8w2 TBC_UNIQUE_PER_WG=2 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
     t8w4) run t8w4 TBC_UNIQUE_PER_WG=4 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
     c5ab8) run c5ab8 TBC_STAGED=2 TBC_LB_BACKOFF=8 $B --depth 3 --config 5 --no-cpu-baseline ;;
+    fp3) run fp3 TBC_FRONT_PRIORITY=1 $B --depth 3 --no-cpu-baseline ;;
+    fp5) run fp5 TBC_FRONT_PRIORITY=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
+    d4p) run d4p $B --depth 4 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
