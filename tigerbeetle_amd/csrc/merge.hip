@@ -256,14 +256,14 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
     }
 }
 
-// LDS of a k_merge_unique workgroup, sized per launch by the batch's widest
-// key (dynamic): the tile's broken flag, then KL key limbs per entry (limb l
-// of entry e at key[l * kUniqueRow + e]; entries [0, na + 1) = A[ia0 - 1 ..
-// ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1]), then the A tombstones.
-// A u128 id tree's tile takes 16.6 KiB, so a workgroup fits beside an AEGIS
-// chain workgroup's T-tables on one CU.
+// LDS of a k_merge_unique workgroup: the tile's broken flag, then the MOST
+// SIGNIFICANT 64 bits of every entry's key (entries [0, na + 1) = A[ia0 - 1
+// .. ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1]): 16.4 KiB for 2,048
+// positions whatever the key width, so a workgroup fits beside an AEGIS chain
+// workgroup's T-tables on one CU. Keys equal in those bits are compared in
+// full from the values (global, L2-hot: the tile has just read them).
 constexpr uint32_t kUniqueRow = kUniqueTile + 3;
-static inline uint32_t unique_lds_bytes(int kl) { return 16 + (uint32_t)kl * kUniqueRow * 8 + kUniqueTile + 1; }
+static inline uint32_t unique_lds_bytes() { return 16 + kUniqueRow * 8; }
 
 // Element idx of a stream whose split resolved segment [lo, hi) at ptr: in
 // that segment, or (a tile crossing an input block boundary) found by walking
@@ -291,20 +291,19 @@ __device__ __forceinline__ uint64_t word_of(const u32x4 &v0, const u32x4 &v1, ui
     return (off & 8) ? ((uint64_t)v.w << 32 | v.z) : ((uint64_t)v.y << 32 | v.x);
 }
 
-// One tile, two merged elements per thread (tile order: its A elements, then
-// its B elements; thread t owns elements t and t + 512). Both values are
-// loaded with their keys before the workgroup's barrier, so their HBM latency
-// overlaps the ranking; pointers come from the split's resolved segments (a
-// tile spans one or two input blocks), not a search of the segment tables.
+// One tile, kUniqueTile / kUniqueThreads merged elements per thread (tile
+// order: its A elements, then its B elements; thread i owns elements i, i +
+// 512, ...). Each value's first 32 bytes and key are loaded together before
+// the barrier, so their HBM latency overlaps the ranking; pointers come from
+// the split's resolved segments (a tile spans one or two input blocks).
 template <int KIND>
 __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j, uint32_t t,
                                                   const UniqueSplit *usplits, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
-    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, R = kUniqueRow, E = T / NT;
+    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, E = T / NT;
     static_assert(T == E * NT, "whole elements per thread");
     uint32_t &s_bad = *(uint32_t *)lds;
-    uint64_t *s_key = (uint64_t *)(lds + 16);
-    uint8_t *s_tomb = lds + 16 + KL * R * 8;
+    uint64_t *s_hi = (uint64_t *)(lds + 16);
     const uint32_t tid = threadIdx.x;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
@@ -315,23 +314,26 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     const uint32_t vs = j.value_size, ts = j.timestamp_offset;
     const bool drop = j.drop_tombstones != 0;
     const uint32_t eb = na + 1; // entry of B[jb0 - 1]
+    constexpr uint32_t kMaxOff = KIND == kKeyTimestamp ? 0u : (KIND == kKeyCompositeU128 ? 16u : 8u);
+    const uint32_t reg_bytes = vs < 32 ? vs : 32u;
+    const bool in_regs = (KIND == kKeyTimestamp ? ts : (kMaxOff > ts ? kMaxOff : ts)) + 8 <= reg_bytes;
     if (tid == 0) s_bad = 0;
-    auto put_entry = [&](uint32_t e, const Key<KL> &k) {
-#pragma unroll
-        for (int l = 0; l < KL; l++) s_key[l * R + e] = k.l[l];
+    auto elem_a = [&](uint32_t i) { return unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, i, vs); };
+    auto elem_b = [&](uint32_t i) { return unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, i, vs); };
+    // Entry e's full key (A entries 0..na, B entries eb..eb+nb+1), from the input.
+    auto full_key = [&](uint32_t e) {
+        const uint8_t *p = e < eb ? elem_a(ia0 - 1 + e) : elem_b(jb0 - 1 + (e - eb));
+        return load_key<KIND>(p, ts);
     };
-    auto elem_of = [&](bool is_a, uint32_t idx) {
-        return is_a ? unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, idx, vs)
-                    : unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, idx, vs);
-    };
-    // This thread's elements: their values' first 32 bytes into registers, keys into LDS.
+    // This thread's elements: their values' first 32 bytes and keys into registers.
     const uint8_t *src[E];
     u32x4 v0[E], v1[E];
+    Key<KL> key[E];
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
         const bool is_a = e < na;
-        src[q] = e < m ? elem_of(is_a, is_a ? ia0 + e : jb0 + (e - na)) : nullptr;
+        src[q] = e < m ? (is_a ? elem_a(ia0 + e) : elem_b(jb0 + (e - na))) : nullptr;
         v0[q] = v1[q] = u32x4{0, 0, 0, 0};
         if (e < m) {
             v0[q] = gld<u32x4>(src[q]);
@@ -341,35 +343,40 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
+#pragma unroll
+        for (int l = 0; l < KL; l++) key[q].l[l] = ~0ull;
         if (e >= m) continue;
-        const bool is_a = e < na;
-        put_entry(is_a ? 1 + e : e + 2, load_key<KIND>(src[q], ts));
-        if (is_a) s_tomb[1 + e] = (uint8_t)load_tomb(src[q], ts);
+        if (in_regs) {
+#pragma unroll
+            for (int l = 0; l < KL; l++) {
+                key[q].l[l] = word_of(v0[q], v1[q], key_limb_off<KIND>(l, ts));
+                if (l == 0 && KIND != kKeyIdU128) key[q].l[l] &= ~kTombstoneBit;
+            }
+        } else {
+            key[q] = load_key<KIND>(src[q], ts);
+        }
+        s_hi[e < na ? 1 + e : e + 2] = key[q].l[KL - 1];
     }
-    // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (sentinel: all ones).
+    // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (absent: all ones,
+    // never compared in full).
     if (tid < 3) {
         const bool bside = tid != 0;
         const Stream &st = bside ? j.b : j.a;
         const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
         const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
-        uint8_t tb = 0;
-        if (bi >= 0 && bi < (int64_t)st.n) {
-            const uint8_t *p = elem_of(!bside, (uint32_t)bi);
-            k = load_key<KIND>(p, ts);
-            if (!bside) tb = (uint8_t)load_tomb(p, ts);
-        }
-        put_entry(e, k);
-        if (!bside) s_tomb[0] = tb;
+        uint64_t hi = ~0ull;
+        if (bi >= 0 && bi < (int64_t)st.n) hi = load_key<KIND>(bside ? elem_b((uint32_t)bi) : elem_a((uint32_t)bi), ts).l[KL - 1];
+        s_hi[e] = hi;
     }
     __syncthreads();
-    auto entry = [&](uint32_t e) {
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = s_key[l * R + e];
-        return k;
+    // Order of entry e against key k: -1 below, 0 equal, 1 above; the most
+    // significant limb from LDS, the rest (rarely) in full.
+    auto cmp = [&](uint32_t e, const Key<KL> &k) -> int {
+        const uint64_t h = s_hi[e];
+        if (h != k.l[KL - 1]) return h < k.l[KL - 1] ? -1 : 1;
+        if constexpr (KL == 1) return 0;
+        const Key<KL> f = full_key(e);
+        return key_lt(f, k) ? -1 : (key_eq(f, k) ? 0 : 1);
     };
     bool bad = false;
     const uint32_t vcm = j.vcm;
@@ -377,38 +384,37 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
         if (e >= m) continue;
+        const Key<KL> &k = key[q];
         uint32_t pos;
         if (e < na) {
-            const Key<KL> ka = entry(1 + e);
-            // |{B in the tile < ka}|: lower bound over entries [eb + 1, eb + 1 + nb).
+            // |{B in the tile < k}|: lower bound over entries [eb + 1, eb + 1 + nb).
             uint32_t lo = 0, hi = nb;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (key_lt(entry(eb + 1 + mid), ka)) lo = mid + 1;
+                if (cmp(eb + 1 + mid, k) < 0) lo = mid + 1;
                 else hi = mid;
             }
             pos = e + lo;
             // The B at the lower bound (inside the tile, or the first after it).
             const bool b_there = lo < nb || jb1 < nb_all;
-            bad |= b_there && key_eq(entry(eb + 1 + lo), ka);
-            bad |= (ia0 + e > 0) && key_eq(entry(e), ka);
-            bad |= drop && s_tomb[1 + e];
+            bad |= b_there && cmp(eb + 1 + lo, k) == 0;
+            bad |= (ia0 + e > 0) && cmp(e, k) == 0;
+            bad |= drop && (in_regs ? (word_of(v0[q], v1[q], ts) >> 63) != 0 : load_tomb(src[q], ts) != 0);
         } else {
             const uint32_t b = e - na;
-            const Key<KL> kb = entry(eb + 1 + b);
-            // |{A in the tile <= kb}|: upper bound over entries [1, 1 + na).
+            // |{A in the tile <= k}|: upper bound over entries [1, 1 + na).
             uint32_t lo = 0, hi = na;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (key_le(entry(1 + mid), kb)) lo = mid + 1;
+                if (cmp(1 + mid, k) <= 0) lo = mid + 1;
                 else hi = mid;
             }
             pos = b + lo;
-            bad |= (jb0 + b > 0) && key_eq(entry(eb + b), kb);
+            bad |= (jb0 + b > 0) && cmp(eb + b, k) == 0;
         }
         const uint32_t g = d0 + pos;
-        const uint32_t k = g / vcm;
-        uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(g - k * vcm) * vs;
+        const uint32_t kb = g / vcm;
+        uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
         gst<u32x4>(dst, v0[q]);
         if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
         for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
@@ -456,14 +462,11 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
                        (UniqueSplit *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
-    int kl = 1; // the widest key among the launch's speculated jobs
-    for (int i = 0; i < njobs; i++)
-        if (h_jobs[i].unique) kl = std::max(kl, h_jobs[i].key_kind == kKeyTimestamp ? 1 : h_jobs[i].key_kind == kKeyCompositeU128 ? 3 : 2);
     (void)d_ticket;
     // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
     static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
     const uint32_t pw = per_wg < 1 ? 1 : per_wg;
-    hipLaunchKernelGGL(k_merge_unique, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads), unique_lds_bytes(kl), s,
+    hipLaunchKernelGGL(k_merge_unique, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads), unique_lds_bytes(), s,
                        d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results, pw);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");

@@ -100,10 +100,11 @@ struct JobDesc {
     uint32_t seal, pad2;
 };
 
-// Merged positions per tile of k_merge_unique (two per thread): the tile's
-// keys (plus three neighbours) take 16.6 KiB of LDS for 16-byte keys, so a
-// workgroup fits beside a chain workgroup's 136 KiB of a CU's 160.
-constexpr uint32_t kUniqueTile = 1024;
+// Merged positions per tile of k_merge_unique (four per thread): the most
+// significant 64 bits of the tile's keys (plus three neighbours) take 16.4
+// KiB of LDS, so a workgroup fits beside a chain workgroup's 136 KiB of a
+// CU's 160.
+constexpr uint32_t kUniqueTile = 2048;
 constexpr uint32_t kUniqueThreads = 512;
 
 struct SplitDesc {
