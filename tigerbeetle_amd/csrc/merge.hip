@@ -325,10 +325,23 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         const uint8_t *p = e < eb ? elem_a(ia0 - 1 + e) : elem_b(jb0 - 1 + (e - eb));
         return load_key<KIND>(p, ts);
     };
-    // This thread's elements: their values' first 32 bytes and keys into registers.
+    // This thread's elements: their values' first 32 bytes into registers
+    // (their keys are taken from there when they lie in them).
     const uint8_t *src[E];
     u32x4 v0[E], v1[E];
-    Key<KL> key[E];
+    auto key_of = [&](uint32_t q) {
+        Key<KL> k;
+        if (in_regs) {
+#pragma unroll
+            for (int l = 0; l < KL; l++) {
+                k.l[l] = word_of(v0[q], v1[q], key_limb_off<KIND>(l, ts));
+                if (l == 0 && KIND != kKeyIdU128) k.l[l] &= ~kTombstoneBit;
+            }
+        } else {
+            k = load_key<KIND>(src[q], ts);
+        }
+        return k;
+    };
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
@@ -343,19 +356,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
-#pragma unroll
-        for (int l = 0; l < KL; l++) key[q].l[l] = ~0ull;
-        if (e >= m) continue;
-        if (in_regs) {
-#pragma unroll
-            for (int l = 0; l < KL; l++) {
-                key[q].l[l] = word_of(v0[q], v1[q], key_limb_off<KIND>(l, ts));
-                if (l == 0 && KIND != kKeyIdU128) key[q].l[l] &= ~kTombstoneBit;
-            }
-        } else {
-            key[q] = load_key<KIND>(src[q], ts);
-        }
-        s_hi[e < na ? 1 + e : e + 2] = key[q].l[KL - 1];
+        if (e < m) s_hi[e < na ? 1 + e : e + 2] = key_of(q).l[KL - 1];
     }
     // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (absent: all ones,
     // never compared in full).
@@ -384,7 +385,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
         if (e >= m) continue;
-        const Key<KL> &k = key[q];
+        const Key<KL> k = key_of(q);
         uint32_t pos;
         if (e < na) {
             // |{B in the tile < k}|: lower bound over entries [eb + 1, eb + 1 + nb).
