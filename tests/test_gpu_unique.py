@@ -109,6 +109,20 @@ def test_unique_broken_small_blocks(oracle_lib, eng_small, name):
     _run(oracle_lib, eng_small, cases, 4096, seed=12)
 
 
+@pytest.mark.parametrize("name", ["transfers.id", "transfers.debit_account_id"])
+def test_unique_most_significant_limb_ties(oracle_lib, eng_small, name):
+    """Keys whose most significant 64 bits take only three values (field_max):
+    the pipelined merge keeps only those bits in LDS, so nearly every
+    comparison falls back to the full keys read from the values. Held and
+    broken speculations must still give the merge path's blocks."""
+    cases = [
+        (name, dict(n_a=3000, b_table_sizes=[2000, 1500], a_immutable=False, overlap=0.0, field_max=3), U, HELD),
+        (name, dict(n_a=2500, b_table_sizes=[2500], a_immutable=True, overlap=0.0, field_max=3), U, HELD),
+        (name, dict(n_a=3000, b_table_sizes=[2000], a_immutable=False, overlap=0.02, field_max=3), U, BROKEN),
+    ]
+    _run(oracle_lib, eng_small, cases, 4096, seed=14)
+
+
 def _repeat_at_block_start(spec, vcm, block: int, first_in_a: bool, seed: int) -> workloads.JobInputs:
     """Inputs whose merged order (A-first tie break) has exactly one repeated
     key, at merged positions (block*vcm - 1, block*vcm): the last value of data
