@@ -64,6 +64,8 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     fp3) run fp3 TBC_FRONT_PRIORITY=1 $B --depth 3 --no-cpu-baseline ;;
     fp5) run fp5 TBC_FRONT_PRIORITY=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
     d4p) run d4p $B --depth 4 --no-cpu-baseline ;;
+    c5a1) run c5a1 TBC_STAGED=2 $B --depth 1 --config 5 --no-cpu-baseline ;;
+    c51) run c51 $B --depth 1 --config 5 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
