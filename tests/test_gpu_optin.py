@@ -48,3 +48,17 @@ def test_assembling_merge_bit_exact():
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout, tail
+
+
+@pytest.mark.gpu
+def test_lean_unique_merge_bit_exact():
+    """TBC_UNIQUE_STAGE=0: the lean k_merge_unique (ranks by entry index,
+    values copied after the search) in pipelined and grid batches, held and
+    broken speculations and most-significant-limb ties, against the oracle."""
+    env = dict(os.environ, TBC_UNIQUE_STAGE="0")
+    files = [os.path.join(HERE, f) for f in ("test_gpu_unique.py", "test_gpu_overlap.py", "test_gpu_grid.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", *files],
+                       env=env, capture_output=True, text=True, timeout=230)
+    tail = (r.stdout + r.stderr)[-3000:]
+    assert r.returncode == 0, tail
+    assert " passed" in r.stdout and " failed" not in r.stdout, tail

@@ -428,7 +428,111 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     }
 }
 
+// Lean variant (TBC_UNIQUE_STAGE=0, A/B): nothing but the top key limb is
+// read before the barrier, and an element keeps no key or value in
+// registers across it: its rank is searched by entry index (top limbs in
+// LDS, full keys read on a tie), then its value is copied from the input
+// (L2: the tile has just read its lines). Few registers, so more
+// workgroups per CU.
+template <int KIND>
+__device__ __forceinline__ void merge_unique_tile_lean(uint8_t *lds, const JobDesc &j, uint32_t t,
+                                                       const UniqueSplit *usplits, JobResultDev *res) {
+    constexpr int KL = KeyLimbs<KIND>::value;
+    constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, E = T / NT;
+    uint32_t &s_bad = *(uint32_t *)lds;
+    uint64_t *s_hi = (uint64_t *)(lds + 16);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
+    const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
+    const UniqueSplit s0 = usplits[j.usplit_base + t];
+    const uint32_t ia0 = s0.i, ia1 = usplits[j.usplit_base + t + 1].i;
+    const uint32_t jb0 = d0 - ia0, jb1 = d1 - ia1;
+    const uint32_t na = ia1 - ia0, nb = jb1 - jb0, m = na + nb;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
+    const bool drop = j.drop_tombstones != 0;
+    const uint32_t eb = na + 1;
+    const uint32_t top = key_limb_off<KIND>(KL - 1, ts);
+    if (tid == 0) s_bad = 0;
+    auto elem_a = [&](uint32_t i) { return unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, i, vs); };
+    auto elem_b = [&](uint32_t i) { return unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, i, vs); };
+    // Entry e's value (A entries 0..na = A[ia0 - 1 ..], B entries eb.. = B[jb0 - 1 ..]).
+    auto entry_ptr = [&](uint32_t e) { return e < eb ? elem_a(ia0 - 1 + e) : elem_b(jb0 - 1 + (e - eb)); };
+    auto top_of = [&](const uint8_t *p) {
+        uint64_t h = gld<uint64_t>(p + top);
+        if (KL == 1 && KIND != kKeyIdU128) h &= ~kTombstoneBit;
+        return h;
+    };
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        if (e < m) {
+            const uint32_t en = e < na ? 1 + e : e + 2;
+            s_hi[en] = top_of(entry_ptr(en));
+        }
+    }
+    if (tid < 3) {
+        const bool bside = tid != 0;
+        const Stream &st = bside ? j.b : j.a;
+        const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
+        const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
+        s_hi[e] = bi >= 0 && bi < (int64_t)st.n ? top_of(entry_ptr(e)) : ~0ull;
+    }
+    __syncthreads();
+    // Order of entry x against entry y: -1, 0, 1 (top limbs, then full keys).
+    auto cmp = [&](uint32_t x, uint32_t y) -> int {
+        const uint64_t hx = s_hi[x], hy = s_hi[y];
+        if (hx != hy) return hx < hy ? -1 : 1;
+        if constexpr (KL == 1) return 0;
+        const Key<KL> kx = load_key<KIND>(entry_ptr(x), ts), ky = load_key<KIND>(entry_ptr(y), ts);
+        return key_lt(kx, ky) ? -1 : (key_eq(kx, ky) ? 0 : 1);
+    };
+    bool bad = false;
+    const uint32_t vcm = j.vcm;
+#pragma unroll 1
+    for (uint32_t q = 0; q < E; q++) {
+        const uint32_t e = tid + q * NT;
+        if (e >= m) break;
+        const uint32_t me = e < na ? 1 + e : e + 2;
+        uint32_t pos;
+        if (e < na) {
+            uint32_t lo = 0, hi = nb;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (cmp(eb + 1 + mid, me) < 0) lo = mid + 1;
+                else hi = mid;
+            }
+            pos = e + lo;
+            const bool b_there = lo < nb || jb1 < nb_all;
+            bad |= b_there && cmp(eb + 1 + lo, me) == 0;
+            bad |= (ia0 + e > 0) && cmp(e, me) == 0;
+            bad |= drop && load_tomb(entry_ptr(me), ts) != 0;
+        } else {
+            const uint32_t b = e - na;
+            uint32_t lo = 0, hi = na;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (cmp(1 + mid, me) <= 0) lo = mid + 1;
+                else hi = mid;
+            }
+            pos = b + lo;
+            bad |= (jb0 + b > 0) && cmp(eb + b, me) == 0;
+        }
+        const uint32_t g = d0 + pos;
+        const uint32_t kb = g / vcm;
+        uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
+        const uint8_t *src = entry_ptr(me);
+        for (uint32_t c = 0; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src + c));
+    }
+    if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    if (tid == 0 && s_bad) {
+        __hip_atomic_store(&res[j.job_index].spec, kSpecBroken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // `per_wg` consecutive tiles per workgroup (fewer, longer-lived workgroups).
+template <bool Lean>
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
                                                                  const UniqueSplit *usplits, JobResultDev *res,
                                                                  uint32_t per_wg) {
@@ -442,10 +546,10 @@ __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *
         const uint32_t t = g - j.utile_base;
         if (i) __syncthreads(); // the previous tile's LDS readers are done
         switch (j.key_kind) {
-        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
-        case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
-        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
-        default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
+        case kKeyTimestamp: (Lean ? merge_unique_tile_lean<kKeyTimestamp>(unique_lds, j, t, usplits, res) : merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res)); break;
+        case kKeyIdU128: (Lean ? merge_unique_tile_lean<kKeyIdU128>(unique_lds, j, t, usplits, res) : merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res)); break;
+        case kKeyCompositeU64: (Lean ? merge_unique_tile_lean<kKeyCompositeU64>(unique_lds, j, t, usplits, res) : merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res)); break;
+        default: (Lean ? merge_unique_tile_lean<kKeyCompositeU128>(unique_lds, j, t, usplits, res) : merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res)); break;
         }
     }
 }
@@ -467,8 +571,16 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
     static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
     const uint32_t pw = per_wg < 1 ? 1 : per_wg;
-    hipLaunchKernelGGL(k_merge_unique, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads), unique_lds_bytes(), s,
-                       d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results, pw);
+    // TBC_UNIQUE_STAGE=0 (A/B measurement): the lean variant.
+    static const bool lean = getenv("TBC_UNIQUE_STAGE") && atoi(getenv("TBC_UNIQUE_STAGE")) == 0;
+    if (lean)
+        hipLaunchKernelGGL(k_merge_unique<true>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
+                           unique_lds_bytes(), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results,
+                           pw);
+    else
+        hipLaunchKernelGGL(k_merge_unique<false>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
+                           unique_lds_bytes(), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results,
+                           pw);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;

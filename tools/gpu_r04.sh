@@ -66,6 +66,9 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     d4p) run d4p $B --depth 4 --no-cpu-baseline ;;
     c5a1) run c5a1 TBC_STAGED=2 $B --depth 1 --config 5 --no-cpu-baseline ;;
     c51) run c51 $B --depth 1 --config 5 --no-cpu-baseline ;;
+    p1s0) run p1s0 TBC_UNIQUE_STAGE=0 $B --depth 1 --pipeline on --no-cpu-baseline ;;
+    d3s0) run d3s0 TBC_UNIQUE_STAGE=0 $B --depth 3 --no-cpu-baseline ;;
+    c1s0) run c1s0 TBC_UNIQUE_STAGE=0 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
