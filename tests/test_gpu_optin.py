@@ -33,32 +33,3 @@ def test_opt_in_paths_bit_exact():
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout, tail
-
-
-@pytest.mark.gpu
-def test_assembling_merge_bit_exact():
-    """TBC_STAGED=2: the assembling merge (k_merge_assemble, 1,024-position
-    tiles, look-back offsets) in every path the staged merge serves,
-    compared with the oracle."""
-    env = dict(os.environ, TBC_STAGED="2")
-    files = [os.path.join(HERE, f) for f in ("test_gpu_parity.py", "test_gpu_grid.py", "test_gpu_engine.py",
-                                              "test_gpu_split.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", "-k", SELECT,
-                        *files], env=env, capture_output=True, text=True, timeout=200)
-    tail = (r.stdout + r.stderr)[-3000:]
-    assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " failed" not in r.stdout, tail
-
-
-@pytest.mark.gpu
-def test_lean_unique_merge_bit_exact():
-    """TBC_UNIQUE_STAGE=0: the lean k_merge_unique (ranks by entry index,
-    values copied after the search) in pipelined and grid batches, held and
-    broken speculations and most-significant-limb ties, against the oracle."""
-    env = dict(os.environ, TBC_UNIQUE_STAGE="0")
-    files = [os.path.join(HERE, f) for f in ("test_gpu_unique.py", "test_gpu_overlap.py", "test_gpu_grid.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", *files],
-                       env=env, capture_output=True, text=True, timeout=230)
-    tail = (r.stdout + r.stderr)[-3000:]
-    assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " failed" not in r.stdout, tail

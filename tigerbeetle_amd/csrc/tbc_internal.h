@@ -35,9 +35,8 @@ constexpr uint32_t kMergeThreads = kMergeTile / 4;
 __host__ __device__ inline uint32_t staged_tile(uint32_t value_size) {
     return value_size <= 64 ? 1024u : 65536u / value_size;
 }
-// TBC_STAGED (A/B measurement): 0 = mask merge + k_assemble, 1 = the staged
-// merge (k_merge_staged), 2 = the assembling merge (k_merge_assemble,
-// 1,024-position tiles).
+// TBC_STAGED=1 (A/B measurement): the staged merge (k_merge_staged) instead
+// of the mask merge + k_assemble.
 int staged_variant();
 
 enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };

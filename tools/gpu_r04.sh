@@ -52,23 +52,15 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     c1h) run c1h TBC_TAIL_TABLES=64 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c5s) run c5s TBC_STAGED=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
     c1s) run c1s TBC_STAGED=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
-    c5a) run c5a TBC_STAGED=2 $B --depth 3 --config 5 --no-cpu-baseline ;;
-    c1a) run c1a TBC_STAGED=2 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
-    c3a) run c3a TBC_STAGED=2 $B --depth 3 --config 3 --no-cpu-baseline ;;
-    c4a) run c4a TBC_STAGED=2 $B --depth 3 --config 4 --no-cpu-baseline ;;
     p1w2) run p1w2 TBC_UNIQUE_PER_WG=2 $B --depth 1 --pipeline on --no-cpu-baseline ;;
     p1w4) run p1w4 TBC_UNIQUE_PER_WG=4 $B --depth 1 --pipeline on --no-cpu-baseline ;;
     t8w2) run t8w2 TBC_UNIQUE_PER_WG=2 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
     t8w4) run t8w4 TBC_UNIQUE_PER_WG=4 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
-    c5ab8) run c5ab8 TBC_STAGED=2 TBC_LB_BACKOFF=8 $B --depth 3 --config 5 --no-cpu-baseline ;;
     fp3) run fp3 TBC_FRONT_PRIORITY=1 $B --depth 3 --no-cpu-baseline ;;
     fp5) run fp5 TBC_FRONT_PRIORITY=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
     d4p) run d4p $B --depth 4 --no-cpu-baseline ;;
-    c5a1) run c5a1 TBC_STAGED=2 $B --depth 1 --config 5 --no-cpu-baseline ;;
     c51) run c51 $B --depth 1 --config 5 --no-cpu-baseline ;;
-    p1s0) run p1s0 TBC_UNIQUE_STAGE=0 $B --depth 1 --pipeline on --no-cpu-baseline ;;
-    d3s0) run d3s0 TBC_UNIQUE_STAGE=0 $B --depth 3 --no-cpu-baseline ;;
-    c1s0) run c1s0 TBC_UNIQUE_STAGE=0 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    p1c) run p1c TBC_PROBE_CONTIG_STORE=1 $B --depth 1 --pipeline on --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
