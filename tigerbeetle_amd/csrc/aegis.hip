@@ -1692,9 +1692,15 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
         ca.init(j.a, sp.seg_a);
         cb.init(j.b, sp.seg_b);
         const uint32_t cpv_log = __builtin_ctz(vs >> 4);
+        // The next word's masks are loaded while this word is copied.
+        uint64_t sm_n = wv < W ? gld<uint64_t>(m + wv) : 0, am_n = wv < W ? gld<uint64_t>(m + W + wv) : 0;
         for (uint32_t w = wv; w < W; w += 4) {
             if (t * kMergeTile + 64 * w >= n) break;
-            const uint64_t sm = gld<uint64_t>(m + w), am = gld<uint64_t>(m + W + w);
+            const uint64_t sm = sm_n, am = am_n;
+            if (w + 4 < W) {
+                sm_n = gld<uint64_t>(m + w + 4);
+                am_n = gld<uint64_t>(m + W + w + 4);
+            }
             const uint32_t ns = __builtin_popcountll(sm);
             if (ns == 0) continue;
             const uint64_t valid = valid_of(w);
