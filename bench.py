@@ -252,9 +252,11 @@ class ReplayWorkload:
         self.batches = sum(1 for kind, *_ in self.executor.record if kind == "batch")
         self.sorts = sum(1 for kind, *_ in self.executor.record if kind == "sort")
         self.moves = sum(1 for _, cs in self.forest.history for _, c in cs if c.move)
+        self.submit_s: list = []
 
     def step(self, eng: Engine, ktimes: dict | None = None):
         live = []
+        t_submit = time.perf_counter()
         for kind, *rest in self.executor.record:
             if kind == "sort":
                 jobs, landings = rest
@@ -269,6 +271,8 @@ class ReplayWorkload:
                 manifest.close_on_grid(self.grid, images, addresses, prev, None if prev else 0)
             else:
                 live.append(eng.submit(rest[0]))
+        # Host time to enqueue the whole record (ops with a host wait included).
+        self.submit_s.append(time.perf_counter() - t_submit)
         for b in live:
             b.wait()
             b.check_results()  # every replayed compaction ends TBC_OK (block checks, invariants)
@@ -826,6 +830,8 @@ def main_config1(args, eng, rank, world, local, dist, backend, bs) -> None:
                          "frac": round(job_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
                          "terms": {"R": wl.input_bytes, "W": wl.output_bytes, "S": wl.sort_bytes}},
         "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},
+        # host time to enqueue a step's whole record (timed steps; no wait but the checkpoint's)
+        "host_enqueue_ms": round(1e3 * sum(wl.submit_s[-args.steps:]) / max(1, args.steps), 3),
         "pcie_inclusive": {"what": "the recording pass: host generation of every op, memtable puts streamed "
                                    "H2D (tbc_memtable_put), all sorts and compactions",
                            "seconds": round(wl.record_s, 3), "puts_bytes": wl.puts_bytes,

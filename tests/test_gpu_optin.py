@@ -33,18 +33,3 @@ def test_opt_in_paths_bit_exact():
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout, tail
-
-
-@pytest.mark.gpu
-def test_coalesced_unique_merge_bit_exact():
-    """TBC_UNIQUE_COALESCE=1: k_merge_unique writing its tiles in merged
-    order (an LDS map from position to entry, sources read again), in
-    pipelined and grid batches, held and broken speculations, against the
-    oracle."""
-    env = dict(os.environ, TBC_UNIQUE_COALESCE="1")
-    files = [os.path.join(HERE, f) for f in ("test_gpu_unique.py", "test_gpu_overlap.py", "test_gpu_grid.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", *files],
-                       env=env, capture_output=True, text=True, timeout=230)
-    tail = (r.stdout + r.stderr)[-3000:]
-    assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " failed" not in r.stdout, tail

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
 // workgroup's T-tables on one CU. Keys equal in those bits are compared in
 // full from the values (global, L2-hot: the tile has just read them).
 constexpr uint32_t kUniqueRow = kUniqueTile + 3;
-static inline uint32_t unique_lds_bytes(bool coalesce) { return 16 + kUniqueRow * 8 + (coalesce ? 2 * kUniqueTile : 0); }
+static inline uint32_t unique_lds_bytes() { return 16 + kUniqueRow * 8; }
 
 // Element idx of a stream whose split resolved segment [lo, hi) at ptr: in
 // that segment, or (a tile crossing an input block boundary) found by walking
@@ -289,7 +289,7 @@ __device__ __forceinline__ uint64_t word_of(const u32x4 &v0, const u32x4 &v1, ui
 // 512, ...). Each value's first 32 bytes and key are loaded together before
 // the barrier, so their HBM latency overlaps the ranking; pointers come from
 // the split's resolved segments (a tile spans one or two input blocks).
-template <int KIND, bool Coalesce = false>
+template <int KIND>
 __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j, uint32_t t,
                                                   const UniqueSplit *usplits, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
@@ -297,7 +297,6 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     static_assert(T == E * NT, "whole elements per thread");
     uint32_t &s_bad = *(uint32_t *)lds;
     uint64_t *s_hi = (uint64_t *)(lds + 16);
-    uint16_t *s_idx = (uint16_t *)(lds + 16 + kUniqueRow * 8); // Coalesce: entry at each merged position
     const uint32_t tid = threadIdx.x;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
@@ -407,33 +406,12 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             pos = b + lo;
             bad |= (jb0 + b > 0) && cmp(eb + b, k) == 0;
         }
-        if constexpr (Coalesce) {
-            s_idx[pos] = (uint16_t)(e < na ? 1 + e : e + 2); // merged position -> entry
-        } else {
-            const uint32_t g = d0 + pos;
-            const uint32_t kb = g / vcm;
-            uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
-            gst<u32x4>(dst, v0[q]);
-            if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
-            for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
-        }
-    }
-    if constexpr (Coalesce) {
-        // Position-ordered copies: thread i writes merged positions i, i +
-        // 512, ... of the tile, so a wave's stores cover whole lines; the
-        // sources are read again (the tile has just brought their lines into L2).
-        __syncthreads();
-#pragma unroll
-        for (uint32_t q = 0; q < E; q++) {
-            const uint32_t i = tid + q * NT;
-            if (i >= m) continue;
-            const uint32_t en = s_idx[i];
-            const uint8_t *sp = en < eb ? elem_a(ia0 - 1 + en) : elem_b(jb0 - 1 + (en - eb));
-            const uint32_t g = d0 + i;
-            const uint32_t kb = g / vcm;
-            uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
-            for (uint32_t c = 0; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(sp + c));
-        }
+        const uint32_t g = d0 + pos;
+        const uint32_t kb = g / vcm;
+        uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
+        gst<u32x4>(dst, v0[q]);
+        if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
+        for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
     __syncthreads();
@@ -444,7 +422,6 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
 }
 
 // `per_wg` consecutive tiles per workgroup (fewer, longer-lived workgroups).
-template <bool Coalesce>
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
                                                                  const UniqueSplit *usplits, JobResultDev *res,
                                                                  uint32_t per_wg) {
@@ -458,10 +435,10 @@ __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *
         const uint32_t t = g - j.utile_base;
         if (i) __syncthreads(); // the previous tile's LDS readers are done
         switch (j.key_kind) {
-        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp, Coalesce>(unique_lds, j, t, usplits, res); break;
-        case kKeyIdU128: merge_unique_tile<kKeyIdU128, Coalesce>(unique_lds, j, t, usplits, res); break;
-        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64, Coalesce>(unique_lds, j, t, usplits, res); break;
-        default: merge_unique_tile<kKeyCompositeU128, Coalesce>(unique_lds, j, t, usplits, res); break;
+        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
+        case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
+        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
+        default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
         }
     }
 }
@@ -483,16 +460,8 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
     static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
     const uint32_t pw = per_wg < 1 ? 1 : per_wg;
-    // TBC_UNIQUE_COALESCE=1 (A/B measurement): position-ordered copies.
-    static const bool coalesce = getenv("TBC_UNIQUE_COALESCE") != nullptr;
-    if (coalesce)
-        hipLaunchKernelGGL(k_merge_unique<true>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
-                           unique_lds_bytes(true), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits,
-                           d_results, pw);
-    else
-        hipLaunchKernelGGL(k_merge_unique<false>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
-                           unique_lds_bytes(false), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits,
-                           d_results, pw);
+    hipLaunchKernelGGL(k_merge_unique, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads), unique_lds_bytes(), s,
+                       d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results, pw);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;

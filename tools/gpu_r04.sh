@@ -60,9 +60,6 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     fp5) run fp5 TBC_FRONT_PRIORITY=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
     d4p) run d4p $B --depth 4 --no-cpu-baseline ;;
     c51) run c51 $B --depth 1 --config 5 --no-cpu-baseline ;;
-    p1c) run p1c TBC_UNIQUE_COALESCE=1 $B --depth 1 --pipeline on --no-cpu-baseline ;;
-    d3c) run d3c TBC_UNIQUE_COALESCE=1 $B --depth 3 --no-cpu-baseline ;;
-    c1c) run c1c TBC_UNIQUE_COALESCE=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
