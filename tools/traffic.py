@@ -33,11 +33,16 @@ def find(root: str, pattern: str) -> str:
     return hits[0]
 
 
+def inst(name: str) -> str:
+    """The instantiation: the short name with its template arguments."""
+    return name.split("(")[0].replace("void ", "").replace("tbc::", "").strip()
+
+
 def counters(root: str, counter: str) -> dict:
     per = collections.defaultdict(list)
     for row in csv.DictReader(open(find(root, "*counter_collection.csv"))):
         if row["Counter_Name"] == counter:
-            per[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+            per[inst(row["Kernel_Name"])].append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in per.items()}
 
 
@@ -51,13 +56,15 @@ def main() -> None:
     stats = find(os.path.join(src, "trace"), "*kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
-    # Instantiations of one kernel share a short name: keep the heaviest.
-    avg_ns, tot_ns, calls = {}, {}, {}
+    # Every instantiation has its own entry (e.g. the fused and the chain-only
+    # k_data_blocks); the short name carries the heaviest instantiation's
+    # numbers, durations and counters alike (bench.py looks kernels up by it).
+    avg_ns, tot_ns, calls, heaviest = {}, {}, {}, {}
     for r in csv.DictReader(open(stats)):
-        k = short(r["Name"])
-        calls[k] = calls.get(k, 0) + int(r["Calls"])  # every instantiation's launches
-        if float(r["TotalDurationNs"]) > tot_ns.get(k, -1.0):
-            avg_ns[k], tot_ns[k] = float(r["AverageNs"]), float(r["TotalDurationNs"])
+        i, k = inst(r["Name"]), short(r["Name"])
+        avg_ns[i], tot_ns[i], calls[i] = float(r["AverageNs"]), float(r["TotalDurationNs"]), int(r["Calls"])
+        if k not in heaviest or tot_ns[i] > tot_ns[heaviest[k]]:
+            heaviest[k] = i
     fetch = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(src, "write"), "WRITE_SIZE")
     md5 = open(os.path.join(src, "lib.md5")).read().split()[0]
@@ -73,18 +80,22 @@ def main() -> None:
                 sq.setdefault(k, {})[c] = v
     out = {"lib_md5": md5, "baseline_config": bench_cfg, "note": "bytes per launch; fetch = 2 x FETCH_SIZE KiB (gfx950 correction), "
                                    "write = WRITE_SIZE KiB", "kernels": {}}
-    for k in sorted(avg_ns):
-        f = fetch.get(k, 0.0) * 1024 * 2
-        w = write.get(k, 0.0) * 1024
-        out["kernels"][k] = {"avg_ns": avg_ns[k], "calls": calls[k], "fetch_bytes": round(f), "write_bytes": round(w),
+    names = sorted(set(avg_ns) | set(heaviest))
+    for k in names:
+        i = heaviest.get(k, k)  # a short name: its heaviest instantiation
+        f = fetch.get(i, 0.0) * 1024 * 2
+        w = write.get(i, 0.0) * 1024
+        out["kernels"][k] = {"avg_ns": avg_ns[i], "calls": calls[i], "fetch_bytes": round(f), "write_bytes": round(w),
                              "traffic_bytes": round(f + w),
-                             "traffic_gbs": round((f + w) / avg_ns[k], 1) if avg_ns[k] else None}
-        if k in sq:
-            s = dict(sq[k])
+                             "traffic_gbs": round((f + w) / avg_ns[i], 1) if avg_ns[i] else None}
+        if k != i:
+            out["kernels"][k]["instantiation"] = i
+        if i in sq:
+            s = dict(sq[i])
             # Rates against the chip: a wave64 VALU instruction holds a SIMD-32 for 2 cycles
             # (1,024 SIMDs); LDS instructions per CU-cycle (256 CUs). Busy cycles are per-SE
             # sums (SQ counters count quad-cycles for WAVE/WAIT/ACTIVE: MI355X_MICROARCH.md).
-            ns = avg_ns[k]
+            ns = avg_ns[i]
             if ns:
                 s["valu_instr_per_ns"] = round(s.get("SQ_INSTS_VALU", 0) / ns, 2)
                 s["valu_issue_frac"] = round(s.get("SQ_INSTS_VALU", 0) * 2 / (1024 * 2.4 * ns), 4)
