@@ -253,11 +253,14 @@ class ReplayWorkload:
         self.sorts = sum(1 for kind, *_ in self.executor.record if kind == "sort")
         self.moves = sum(1 for _, cs in self.forest.history for _, c in cs if c.move)
         self.submit_s: list = []
+        self.host_s: dict = {}  # host seconds per op kind, over every step
 
     def step(self, eng: Engine, ktimes: dict | None = None):
         live = []
         t_submit = time.perf_counter()
+        host = self.host_s
         for kind, *rest in self.executor.record:
+            t = time.perf_counter()
             if kind == "sort":
                 jobs, landings = rest
                 eng.copy_device_batch(landings)
@@ -271,6 +274,7 @@ class ReplayWorkload:
                 manifest.close_on_grid(self.grid, images, addresses, prev, None if prev else 0)
             else:
                 live.append(eng.submit(rest[0]))
+            host[kind] = host.get(kind, 0.0) + time.perf_counter() - t
         # Host time to enqueue the whole record (ops with a host wait included).
         self.submit_s.append(time.perf_counter() - t_submit)
         for b in live:
@@ -832,6 +836,7 @@ def main_config1(args, eng, rank, world, local, dist, backend, bs) -> None:
         "kernels_us_per_step": {k: round(v, 1) for k, v in per_step.items()},
         # host time to enqueue a step's whole record (timed steps; no wait but the checkpoint's)
         "host_enqueue_ms": round(1e3 * sum(wl.submit_s[-args.steps:]) / max(1, args.steps), 3),
+        "host_enqueue_ms_by_op": {k: round(1e3 * v / max(1, len(wl.submit_s)), 3) for k, v in wl.host_s.items()},
         "pcie_inclusive": {"what": "the recording pass: host generation of every op, memtable puts streamed "
                                    "H2D (tbc_memtable_put), all sorts and compactions",
                            "seconds": round(wl.record_s, 3), "puts_bytes": wl.puts_bytes,
