@@ -111,14 +111,29 @@ bool compute_layout(const tbc_tree *t, uint32_t block_size, Layout *L) {
 // from storage): the host copies into a slot, the engine stream copies the
 // slot to the device; a slot is reused once its copy's event has passed, so
 // a producer only waits when it runs kSlots slots ahead of the device.
-struct Staging {
-    static constexpr int kSlots = 8;
-    static constexpr uint64_t kSlotBytes = 8ull << 20;
+template <int N, uint64_t B> struct Ring {
+    static constexpr int kSlots = N;
+    static constexpr uint64_t kSlotBytes = B;
     uint8_t *base = nullptr;
     hipEvent_t ev[kSlots] = {};
     bool used[kSlots] = {};
     int next = 0;
+    // The next slot, once the stream has passed its previous user.
+    uint8_t *take(int *slot) {
+        const int k = next;
+        next = (next + 1) % kSlots;
+        if (used[k] && hipEventSynchronize(ev[k]) != hipSuccess) return nullptr;
+        *slot = k;
+        return base + (uint64_t)k * kSlotBytes;
+    }
 };
+// Bulk host<->device staging (blocks, puts).
+using Staging = Ring<8, 8ull << 20>;
+// Small descriptors (copy lists, sort plans, manifest addresses): many small
+// slots, so the host may run many bar-end sorts ahead of the engine stream
+// before it waits for a slot (with the bulk ring's 8 slots it waited on the
+// sort four ops back: config 1's host spent 28 ms of a step there).
+using DescRing = Ring<128, 64ull << 10>;
 
 struct tbc_engine {
     int device = 0;
@@ -136,6 +151,7 @@ struct tbc_engine {
     int ntails = 3;
     hipStream_t tail[kMaxTails] = {};
     hipEvent_t tail_ev[kMaxTails] = {}; // the last batch finished on each tail
+    DescRing desc;
     // Caller-provided output ranges [lo, hi) of non-grid batches whose tails
     // may still read them, with an event recorded after each such tail: a
     // later batch writing into one of them waits for that event
@@ -519,6 +535,10 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
              hipEventCreateWithFlags(&e->sort_last, hipEventDisableTiming) == hipSuccess;
     for (int s = 0; ok && s < Staging::kSlots; s++)
         ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipHostMalloc((void **)&e->desc.base, DescRing::kSlots * DescRing::kSlotBytes, hipHostMallocDefault) ==
+                   hipSuccess;
+    for (int s = 0; ok && s < DescRing::kSlots; s++)
+        ok = hipEventCreateWithFlags(&e->desc.ev[s], hipEventDisableTiming) == hipSuccess;
     // The merge's mask buffer, sized up front for batches of up to 2^28
     // values (64 MiB of HBM), so submitting never waits on the device to grow
     // it; a larger batch still grows it (after a stream synchronize).
@@ -547,6 +567,9 @@ void tbc_engine_deinit(tbc_engine *e) {
     for (int s = 0; s < Staging::kSlots; s++)
         if (e->staging.ev[s]) hipEventDestroy(e->staging.ev[s]);
     if (e->staging.base) hipHostFree(e->staging.base);
+    for (int s = 0; s < DescRing::kSlots; s++)
+        if (e->desc.ev[s]) hipEventDestroy(e->desc.ev[s]);
+    if (e->desc.base) hipHostFree(e->desc.base);
     hipHostFree(e->host.base);
     hipFree(e->dev.base);
     if (e->masks) hipFree(e->masks);
@@ -881,19 +904,19 @@ tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t
         if (hipMalloc((void **)&e->copy_desc, want) != hipSuccess) return TBC_ERR_OUT_OF_MEMORY;
         e->copy_desc_size = want;
     }
-    // The descriptors go through a pinned staging slot, reusable once the
-    // stream has passed this copy.
-    Staging &st = e->staging;
-    const int slot = st.next;
-    st.next = (st.next + 1) % Staging::kSlots;
-    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
-    uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    // The descriptors go through a pinned slot (a small one when they fit),
+    // reusable once the stream has passed this copy.
+    const bool small = need <= DescRing::kSlotBytes;
+    int slot = 0;
+    uint8_t *host = small ? e->desc.take(&slot) : e->staging.take(&slot);
+    if (!host) return TBC_ERR_DEVICE;
     memcpy(host, items.data(), need);
     bool ok = hipMemcpyAsync(e->copy_desc, host, need, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
               launch_copy_batch((const CopyItem *)e->copy_desc, (uint32_t)items.size(), (uint32_t)chunks,
                                 e->stream) == 0;
-    ok = hipEventRecord(st.ev[slot], e->stream) == hipSuccess && ok;
-    st.used[slot] = true;
+    hipEvent_t &ev = small ? e->desc.ev[slot] : e->staging.ev[slot];
+    ok = hipEventRecord(ev, e->stream) == hipSuccess && ok;
+    (small ? e->desc.used[slot] : e->staging.used[slot]) = true;
     return ok ? TBC_OK : TBC_ERR_DEVICE;
 }
 
@@ -1041,13 +1064,13 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
             return TBC_ERR_DEVICE;
         e->sort_status_words = want;
     }
-    // The descriptors go through a pinned staging slot, reusable once the
-    // stream has passed this sort.
-    Staging &st = e->staging;
-    const int slot = st.next;
-    st.next = (st.next + 1) % Staging::kSlots;
-    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
-    uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
+    // The descriptors go through a pinned slot (a small one when they fit),
+    // reusable once the stream has passed this sort.
+    const bool small = host_need <= DescRing::kSlotBytes;
+    int slot = 0;
+    uint8_t *host = small ? e->desc.take(&slot) : e->staging.take(&slot);
+    if (!host) return TBC_ERR_DEVICE;
+    hipEvent_t &slot_ev = small ? e->desc.ev[slot] : e->staging.ev[slot];
     retire_sorts(e);
     if (ss != e->stream) { // after everything enqueued so far (the tables' puts and landings)
         hipEvent_t fork = take_event(e);
@@ -1058,8 +1081,8 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     }
     int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, e->sort_status,
                                e->sort_status_words, &e->sort_epoch, host, ss);
-    if (hipEventRecord(st.ev[slot], ss) != hipSuccess) rc = -1;
-    st.used[slot] = true;
+    if (hipEventRecord(slot_ev, ss) != hipSuccess) rc = -1;
+    (small ? e->desc.used[slot] : e->staging.used[slot]) = true;
     if (ss != e->stream && rc == 0) {
         tbc_engine::PendingSort ps;
         ps.done = take_event(e);
