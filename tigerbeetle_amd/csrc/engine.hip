@@ -911,7 +911,7 @@ tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t
     uint8_t *host = small ? e->desc.take(&slot) : e->staging.take(&slot);
     if (!host) return TBC_ERR_DEVICE;
     memcpy(host, items.data(), need);
-    bool ok = hipMemcpyAsync(e->copy_desc, host, need, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
+    bool ok = launch_upload(e->copy_desc, host, need, e->stream) == 0 &&
               launch_copy_batch((const CopyItem *)e->copy_desc, (uint32_t)items.size(), (uint32_t)chunks,
                                 e->stream) == 0;
     hipEvent_t &ev = small ? e->desc.ev[slot] : e->staging.ev[slot];
@@ -1740,7 +1740,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                 for (const auto &g : seg_in[2 * (size_t)i + side])
                     if (g.first && !(ok = wait_sorts(e, g.first, g.first + (uint64_t)g.second * hj[i].value_size)))
                         break;
-    ok = ok && hipMemcpyAsync(d_in, h_in, sz_in, hipMemcpyHostToDevice, s) == hipSuccess;
+    ok = ok && launch_upload(d_in, h_in, sz_in, s) == 0;
     // Tile status, block tiles and results start zeroed (contiguous).
     ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
     mark_cb(b, "start");

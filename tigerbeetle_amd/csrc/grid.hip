@@ -21,6 +21,8 @@
 //                   once its input checks passed.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "tbc_internal.h"
 
 namespace tbc {
@@ -195,5 +197,35 @@ int launch_copy_batch(const CopyItem *d_items, uint32_t count, uint32_t chunks, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 uint64_t copy_chunk_bytes() { return kCopyChunk; }
+
+// Host-to-device upload of a pinned (device-mapped) host buffer by a compute
+// kernel on the caller's stream: each batch's descriptor image, a sort's plan
+// and a device-copy list are read over PCIe by the kernel itself instead of a
+// DMA copy, so the engine stream never hands off to a copy engine between
+// two half-bars (TBC_UPLOAD_COPY=1 restores hipMemcpyAsync, A/B only).
+// The host rewrites a slot once the stream has passed its previous upload,
+// so the source is read at system scope (no cache may hold the old bytes).
+__global__ __launch_bounds__(256) void k_upload(uint64_t *dst, const uint64_t *src, uint64_t n8, uint8_t *dst_tail,
+                                               const uint8_t *src_tail, uint32_t tail) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (blockIdx.x == 0 && threadIdx.x < tail)
+        dst_tail[threadIdx.x] = __hip_atomic_load(src_tail + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    static const bool copy = getenv("TBC_UPLOAD_COPY") != nullptr;
+    if (!bytes) return 0;
+    if (copy || (((uintptr_t)dst | (uintptr_t)host_src) & 7))
+        return hipMemcpyAsync(dst, host_src, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
+    const uint64_t n8 = bytes / 8;
+    const uint32_t tail = (uint32_t)(bytes - 8 * n8);
+    const uint64_t blocks = (n8 + 255) / 256;
+    hipLaunchKernelGGL(k_upload, dim3((uint32_t)(blocks < 512 ? (blocks ? blocks : 1) : 512)), dim3(256), 0, s,
+                       (uint64_t *)dst, (const uint64_t *)host_src, n8, (uint8_t *)dst + 8 * n8,
+                       (const uint8_t *)host_src + 8 * n8, tail);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 } // namespace tbc

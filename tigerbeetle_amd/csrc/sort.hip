@@ -996,7 +996,7 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     uint32_t *hist = (uint32_t *)(base + L.hist), *bins = (uint32_t *)(base + L.bins);
     uint32_t *counters = (uint32_t *)(base + L.counters);
     SortBatch *d_batch = (SortBatch *)(base + L.batch);
-    if (hipMemcpyAsync(base, hbase, L.hist, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (launch_upload(base, hbase, L.hist, s) != 0 ||
         hipMemsetAsync(hist, 0, L.bins - L.hist, s) != hipSuccess)
         return -1;
     hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile);

@@ -336,6 +336,9 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 // merge of each tile writing every value straight to its output slot (every
 // value survives) with the speculation checks (a broken job is marked for
 // the recomputation phase).
+// A pinned host buffer to device memory by a compute kernel on `stream`
+// (grid.hip k_upload).
+int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream);
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
                         JobResultDev *d_results, uint32_t *d_ticket, void *stream, void (*mark)(void *, const char *),
                         void *mark_ctx);
