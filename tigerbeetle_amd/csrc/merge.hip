@@ -258,6 +258,25 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
 constexpr uint32_t kUniqueRow = kUniqueTile + 3;
 static inline uint32_t unique_lds_bytes() { return 16 + kUniqueRow * 8; }
 
+// Bytes [32, vs) of a value: every 16-byte chunk loaded before any is
+// stored (a load-store loop keeps one load in flight: a 128-byte value's six
+// chunks were six dependent round trips), then the rare bytes past 128.
+__device__ __forceinline__ void copy_rest(uint8_t *dst, const uint8_t *src, uint32_t vs) {
+    constexpr uint32_t kChunks = 6; // bytes [32, 128)
+    if (vs <= 32) return;
+    // No hoisting of a later element's chunks above these: one element's
+    // chunks live at a time (a caller's unrolled loop kept them all).
+    asm volatile("" ::: "memory");
+    u32x4 r[kChunks];
+#pragma unroll
+    for (uint32_t c = 0; c < kChunks; c++)
+        if (32 + 16 * c < vs) r[c] = gld<u32x4>(src + 32 + 16 * c);
+#pragma unroll
+    for (uint32_t c = 0; c < kChunks; c++)
+        if (32 + 16 * c < vs) gst<u32x4>(dst + 32 + 16 * c, r[c]);
+    for (uint32_t c = 128; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src + c));
+}
+
 // Element idx of a stream whose split resolved segment [lo, hi) at ptr: in
 // that segment, or (a tile crossing an input block boundary) found by walking
 // the segment table forward from it.
@@ -411,6 +430,8 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
         gst<u32x4>(dst, v0[q]);
         if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
+        // (copy_rest's six chunks in flight cost this kernel 90 VGPRs: the
+        // id trees' values are 32 bytes, so a wide value copies in sequence.)
         for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
@@ -1213,7 +1234,7 @@ __global__ __launch_bounds__(kAsmThreads) void k_merge_assemble(const JobDesc *j
         uint8_t *p = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(o - (uint64_t)k * vcm) * vs;
         gst<u32x4>(p, v0[q]);
         if (vs >= 32) gst<u32x4>(p + 16, v1[q]);
-        for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(p + c, gld<u32x4>(src[q] + c));
+        copy_rest(p, src[q], vs);
     }
     // Survivors landed per data block (the chain kernel checks them), and the
     // job's shape from its last tile (k_tile_scan's).
