@@ -1522,7 +1522,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                       (dblocks_all + 1) / 2 > fused_max_chain_waves());
     for (uint32_t i = 0; i < count; i++) {
         JobDesc &d = hj[i];
-        if (staged) d.merge_tile = staged_variant() == 2 ? 1024u : staged_tile(d.value_size);
+        if (staged) d.merge_tile = staged_tile(d.value_size);
         const uint64_t n = (uint64_t)d.a.n + d.b.n;
         d.tile_count = (uint32_t)((n + d.merge_tile - 1) / d.merge_tile);
     }

@@ -36,7 +36,7 @@
 namespace tbc {
 
 int staged_variant() {
-    static const int v = getenv("TBC_STAGED") ? (atoi(getenv("TBC_STAGED")) == 2 ? 2 : 1) : 0;
+    static const int v = getenv("TBC_STAGED") ? 1 : 0;
     return v;
 }
 
@@ -258,25 +258,6 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
 constexpr uint32_t kUniqueRow = kUniqueTile + 3;
 static inline uint32_t unique_lds_bytes() { return 16 + kUniqueRow * 8; }
 
-// Bytes [32, vs) of a value: every 16-byte chunk loaded before any is
-// stored (a load-store loop keeps one load in flight: a 128-byte value's six
-// chunks were six dependent round trips), then the rare bytes past 128.
-__device__ __forceinline__ void copy_rest(uint8_t *dst, const uint8_t *src, uint32_t vs) {
-    constexpr uint32_t kChunks = 6; // bytes [32, 128)
-    if (vs <= 32) return;
-    // No hoisting of a later element's chunks above these: one element's
-    // chunks live at a time (a caller's unrolled loop kept them all).
-    asm volatile("" ::: "memory");
-    u32x4 r[kChunks];
-#pragma unroll
-    for (uint32_t c = 0; c < kChunks; c++)
-        if (32 + 16 * c < vs) r[c] = gld<u32x4>(src + 32 + 16 * c);
-#pragma unroll
-    for (uint32_t c = 0; c < kChunks; c++)
-        if (32 + 16 * c < vs) gst<u32x4>(dst + 32 + 16 * c, r[c]);
-    for (uint32_t c = 128; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src + c));
-}
-
 // Element idx of a stream whose split resolved segment [lo, hi) at ptr: in
 // that segment, or (a tile crossing an input block boundary) found by walking
 // the segment table forward from it.
@@ -430,8 +411,8 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
         gst<u32x4>(dst, v0[q]);
         if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
-        // (copy_rest's six chunks in flight cost this kernel 90 VGPRs: the
-        // id trees' values are 32 bytes, so a wide value copies in sequence.)
+        // (Loading a wide value's chunks together cost this kernel 90 VGPRs:
+        // the id trees' values are 32 bytes, so a wide value copies in sequence.)
         for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
@@ -986,282 +967,6 @@ __global__ __launch_bounds__(kStagedThreads) void k_merge_staged(const JobDesc *
     }
 }
 
-// Assembling merge, round 4 (TBC_STAGED=2, A/B against k_merge_staged): the
-// staged merge's R + W shape, sized to run beside the tails' chain
-// workgroups (24 KiB of LDS left on their CUs): 1,024 merged positions per
-// tile and 512 threads, each owning two input elements (tile order: A, then
-// B) whose first 32 bytes it holds in registers from the kernel's start (the
-// keys come from them when they lie there); the rest of a longer value is
-// re-read at store time from the lines the first load brought into L2. LDS:
-// the keys (KL limbs), A tombstones and a 4-byte output rank per element —
-// 13.5 KiB for 8-byte keys, 21.7 KiB for 16-byte keys.
-constexpr uint32_t kAsmTile = 1024, kAsmThreads = 512, kAsmE = kAsmTile / kAsmThreads;
-
-template <int KIND>
-__global__ __launch_bounds__(kAsmThreads) void k_merge_assemble(const JobDesc *jobs, const TileRef *order,
-                                                                uint32_t order_offset, const SplitDesc *splits,
-                                                                uint64_t *lookback, uint32_t *ticket, uint32_t *ready,
-                                                                JobResultDev *res, uint32_t probe) {
-    constexpr int KL = KeyLimbs<KIND>::value;
-    constexpr uint32_t NT = kAsmThreads, E = kAsmE;
-    __shared__ uint64_t s_key[KL][kAsmTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
-    __shared__ uint8_t s_tomb[kAsmTile + 4];
-    __shared__ uint32_t s_dst[kAsmTile];         // per element: tile-local output rank, or ~0
-    __shared__ uint32_t s_wsum[NT / 64];
-    __shared__ uint32_t s_ticket, s_excl;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_ticket = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const TileRef ref = order[order_offset + s_ticket];
-    const JobDesc &j = jobs[ref.job];
-    const uint32_t t = ref.tile, T = j.merge_tile; // == kAsmTile
-    const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
-    const uint32_t d0 = t * T, d1 = (d0 + T) < n ? d0 + T : n;
-    const SplitDesc s0 = splits[j.split_base + t];
-    const uint32_t i0 = s0.i, i1 = splits[j.split_base + t + 1].i;
-    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
-    const uint32_t na = i1 - i0, nb = j1 - j0, slots = na + nb;
-    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
-    const bool immutable = j.a_immutable != 0, secondary = j.usage == 1, drop = j.drop_tombstones != 0;
-    const uint32_t ea = na + 2;
-    const bool in_regs = vs >= 32 && ts + 8 <= 32;
-
-    // 1. This thread's elements: pointers from cursors at the split's
-    //    segments, the first 32 bytes of each value into registers.
-    SegCursor ca, cb;
-    ca.init(j.a, s0.seg_a);
-    cb.init(j.b, s0.seg_b);
-    const uint8_t *src[E];
-    u32x4 v0[E], v1[E];
-#pragma unroll
-    for (uint32_t q = 0; q < E; q++) {
-        const uint32_t e = tid + q * NT;
-        src[q] = nullptr;
-        v0[q] = v1[q] = u32x4{0, 0, 0, 0};
-        if (e < slots) {
-            src[q] = e < na ? ca.elem(i0 + e, vs) : cb.elem(j0 + (e - na), vs);
-            v0[q] = gld<u32x4>(src[q]);
-            if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
-        }
-    }
-    // Boundary keys: A[i0 - 1], A[i1], B[j1] (max when absent).
-    if (tid < 3) {
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
-        uint32_t tb = 0, entry;
-        const uint8_t *p = nullptr;
-        if (tid == 0) {
-            entry = 0;
-            if (i0 >= 1) p = ca.elem(i0 - 1, vs); // the split's A segment holds A[i0 - 1]
-        } else if (tid == 1) {
-            entry = na + 1;
-            if (i1 < na_all) p = ca.elem(i1, vs);
-        } else {
-            entry = ea + nb;
-            if (j1 < nb_all) p = cb.elem(j1, vs);
-        }
-        if (p) {
-            k = load_key<KIND>(p, ts);
-            if (tid < 2) tb = load_tomb(p, ts);
-        }
-#pragma unroll
-        for (int l = 0; l < KL; l++) s_key[l][entry] = k.l[l];
-        if (entry < ea) s_tomb[entry] = (uint8_t)tb;
-    }
-    // Keys (and A tombstones) of the elements.
-#pragma unroll
-    for (uint32_t q = 0; q < E; q++) {
-        const uint32_t e = tid + q * NT;
-        if (e >= slots) continue;
-        const uint32_t entry = e < na ? e + 1 : ea + (e - na);
-        Key<KL> k;
-        uint32_t tb;
-        if (in_regs) {
-#pragma unroll
-            for (int l = 0; l < KL; l++) {
-                k.l[l] = word_of(v0[q], v1[q], key_limb_off<KIND>(l, ts));
-                if (l == 0 && KIND != kKeyIdU128) k.l[l] &= ~kTombstoneBit;
-            }
-            tb = (uint32_t)(word_of(v0[q], v1[q], ts) >> 63);
-        } else {
-            k = load_key<KIND>(src[q], ts);
-            tb = load_tomb(src[q], ts);
-        }
-#pragma unroll
-        for (int l = 0; l < KL; l++) s_key[l][entry] = k.l[l];
-        if (e < na) s_tomb[entry] = (uint8_t)tb;
-    }
-    __syncthreads();
-
-    auto entry_key = [&](uint32_t e) {
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = s_key[l][e];
-        return k;
-    };
-    auto run_len = [&](uint32_t ia) { // run of equal keys ending at A[ia] (secondary-index dedup)
-        const Key<KL> k = entry_key(ia - i0 + 1);
-        uint32_t len = 1;
-        int64_t idx = (int64_t)ia - 1;
-        while (idx >= 0) {
-            Key<KL> kk;
-            if (idx >= (int64_t)i0 - 1) kk = entry_key((uint32_t)(idx - ((int64_t)i0 - 1)));
-            else kk = load_key<KIND>(elem_ptr(j.a, seg_search(j.a, (uint32_t)idx), (uint32_t)idx, vs), ts);
-            if (!key_eq(kk, k)) break;
-            len++;
-            idx--;
-        }
-        return len;
-    };
-
-    // 2. Survivor rules (merge_tile's), two merged positions per thread.
-    constexpr uint32_t kPer = kAsmTile / kAsmThreads;
-    const uint32_t dd = kPer * tid < slots ? kPer * tid : slots;
-    uint32_t a, b;
-    {
-        uint32_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (key_le(entry_key(1 + mid), entry_key(ea + dd - 1 - mid))) lo = mid + 1;
-            else hi = mid;
-        }
-        a = lo;
-        b = dd - lo;
-    }
-    uint32_t slot_of[kPer], surv_bits = 0, mine = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; k++) {
-        slot_of[k] = ~0u;
-        if (dd + k >= slots) continue;
-        const bool take_a = a < na && (b >= nb || key_le(entry_key(1 + a), entry_key(ea + b)));
-        bool surv;
-        if (take_a) {
-            const uint32_t ia = i0 + a, e = a + 1;
-            const Key<KL> ka = entry_key(e);
-            bool dedup = true;
-            if (immutable) {
-                dedup = !((ia + 1 < na_all) && key_eq(entry_key(e + 1), ka));
-                if (dedup && secondary) dedup = (run_len(ia) & 1) != 0;
-            }
-            const bool eq_b = (b < nb || j1 < nb_all) && key_eq(entry_key(ea + b), ka);
-            surv = dedup && !(drop && s_tomb[e]) && !(secondary && eq_b);
-            slot_of[k] = a;
-            a++;
-        } else {
-            const Key<KL> kb = entry_key(ea + b);
-            bool a_exists = (i0 + a) >= 1 && key_eq(entry_key(a), kb);
-            if (a_exists && immutable && secondary) a_exists = (run_len(i0 + a - 1) & 1) != 0;
-            surv = !a_exists;
-            slot_of[k] = na + b;
-            b++;
-        }
-        surv_bits |= (surv ? 1u : 0u) << k;
-        mine += surv ? 1u : 0u;
-    }
-    // Tile-local ranks: exclusive scan of the per-thread survivor counts.
-    uint32_t incl = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    uint32_t woff = 0, cnt = 0;
-    for (uint32_t w = 0; w < NT / 64; w++) {
-        woff += w < wave ? s_wsum[w] : 0u;
-        cnt += s_wsum[w];
-    }
-    uint32_t rank = woff + incl - mine;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; k++) {
-        if (slot_of[k] == ~0u) continue;
-        const bool sv = (surv_bits >> k) & 1u;
-        s_dst[slot_of[k]] = sv ? rank : ~0u;
-        rank += sv ? 1u : 0u;
-    }
-
-    // 3. The job's survivors before this tile: decoupled look-back, wave 0
-    //    reading 64 predecessors per round trip (nearest first).
-    constexpr uint64_t kAgg = 1ull << 62, kPre = 2ull << 62, kCnt = (1ull << 62) - 1;
-    if (probe == 1) { // timing probe only (wrong outputs): no look-back, every tile at offset 0
-        if (tid == 0) s_excl = 0;
-    } else if (wave == 0) {
-        uint64_t *lb = lookback + j.tile_base;
-        if (lane == 0) __hip_atomic_store(&lb[t], (t == 0 ? kPre : kAgg) | cnt, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t excl = 0;
-        int64_t top = (int64_t)t - 1;
-        for (uint32_t spins = 0; t > 0;) {
-            const int64_t idx = top - (int64_t)lane;
-            const uint64_t w = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kPre;
-            const uint64_t fl = w >> 62;
-            const uint64_t pre = __ballot(fl == 2);
-            const uint32_t stop = pre ? __builtin_ctzll(pre) : 64u; // nearest inclusive prefix
-            const bool in = lane <= stop;
-            if (__ballot(in && fl == 0)) { // a tile up to the prefix has not published yet
-                if (++spins > (1u << 22)) { // bounded: report instead of hanging
-                    if (lane == 0) gst<uint32_t>(&res[j.job_index].invariant, 0xbeefu);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            uint64_t c = in ? (w & kCnt) : 0;
-            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-            excl += c;
-            if (stop < 64) break;
-            top -= 64;
-        }
-        if (lane == 0) {
-            if (t > 0) __hip_atomic_store(&lb[t], kPre | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_excl = (uint32_t)excl;
-        }
-    }
-    __syncthreads();
-    const uint32_t out0 = s_excl, vcm = j.vcm;
-
-    // 4. Survivors to their output slots: the first 32 bytes from registers,
-    //    the rest re-read.
-#pragma unroll
-    for (uint32_t q = 0; q < E; q++) {
-        const uint32_t e = tid + q * NT;
-        if (e >= slots) continue;
-        const uint32_t dst = s_dst[e];
-        if (dst == ~0u) continue;
-        const uint64_t o = (uint64_t)j.out_offset + out0 + dst;
-        const uint32_t k = (uint32_t)(o / vcm);
-        uint8_t *p = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(o - (uint64_t)k * vcm) * vs;
-        gst<u32x4>(p, v0[q]);
-        if (vs >= 32) gst<u32x4>(p + 16, v1[q]);
-        copy_rest(p, src[q], vs);
-    }
-    // Survivors landed per data block (the chain kernel checks them), and the
-    // job's shape from its last tile (k_tile_scan's).
-    if (tid == 0) {
-        if (j.out_offset == 0) {
-            uint32_t o = out0;
-            const uint32_t end = out0 + cnt;
-            while (o < end) {
-                const uint32_t k = o / vcm;
-                const uint32_t e = (k + 1) * vcm < end ? (k + 1) * vcm : end;
-                __hip_atomic_fetch_add(ready + j.dblock_base + k, e - o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                o = e;
-            }
-        }
-        if (t + 1 == j.tile_count) {
-            const uint64_t total = (uint64_t)out0 + cnt;
-            const uint32_t db = (uint32_t)((total + vcm - 1) / vcm);
-            const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
-            JobResultDev &rr = res[j.job_index];
-            rr.value_count = total;
-            rr.data_block_count = db;
-            rr.table_count = tables;
-            rr.block_count = db + tables;
-        }
-    }
-}
-
 // The recomputation phase of a speculating batch: a small grid strides over
 // the tiles (most leave at once, all of them while no speculation broke).
 template <int KIND>
@@ -1350,10 +1055,6 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
     if (ntiles && phase)
         hipLaunchKernelGGL((k_merge_tile_redo<KIND>), dim3(std::min<uint32_t>(ntiles, 1024)), dim3(kMergeThreads), 0,
                            s, d_jobs, d_order, tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_res, ntiles);
-    else if (ntiles && d_lookback && f.merge_tile == kAsmTile && staged_variant() == 2)
-        hipLaunchKernelGGL((k_merge_assemble<KIND>), dim3(ntiles), dim3(kAsmThreads), 0, s, d_jobs, d_order, tile_off,
-                           (const SplitDesc *)d_splits, d_lookback, d_ticket + KIND, d_ready,
-                           const_cast<JobResultDev *>(d_res), getenv("TBC_PROBE_NO_LOOKBACK") ? 1u : 0u);
     else if (ntiles && d_lookback)
         hipLaunchKernelGGL((k_merge_staged<KIND>), dim3(ntiles), dim3(kStagedThreads), 0, s, d_jobs, d_order, tile_off,
                            (const SplitDesc *)d_splits, d_lookback, d_ticket + KIND, d_ready,
