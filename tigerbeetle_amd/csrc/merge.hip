@@ -289,7 +289,11 @@ __device__ __forceinline__ uint64_t word_of(const u32x4 &v0, const u32x4 &v1, ui
 // 512, ...). Each value's first 32 bytes and key are loaded together before
 // the barrier, so their HBM latency overlaps the ranking; pointers come from
 // the split's resolved segments (a tile spans one or two input blocks).
-template <int KIND>
+// Wide (values over 32 bytes: the object trees): no value bytes held across
+// the barrier (keys read apart); each stored value's chunks are loaded
+// together, one element at a time. A launch of its own, so the narrow
+// kernel keeps its registers.
+template <int KIND, bool Wide>
 __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j, uint32_t t,
                                                   const UniqueSplit *usplits, JobResultDev *res) {
     constexpr int KL = KeyLimbs<KIND>::value;
@@ -309,7 +313,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     const uint32_t eb = na + 1; // entry of B[jb0 - 1]
     constexpr uint32_t kMaxOff = KIND == kKeyTimestamp ? 0u : (KIND == kKeyCompositeU128 ? 16u : 8u);
     const uint32_t reg_bytes = vs < 32 ? vs : 32u;
-    const bool in_regs = (KIND == kKeyTimestamp ? ts : (kMaxOff > ts ? kMaxOff : ts)) + 8 <= reg_bytes;
+    const bool in_regs = !Wide && (KIND == kKeyTimestamp ? ts : (kMaxOff > ts ? kMaxOff : ts)) + 8 <= reg_bytes;
     if (tid == 0) s_bad = 0;
     auto elem_a = [&](uint32_t i) { return unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, i, vs); };
     auto elem_b = [&](uint32_t i) { return unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, i, vs); };
@@ -341,7 +345,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         const bool is_a = e < na;
         src[q] = e < m ? (is_a ? elem_a(ia0 + e) : elem_b(jb0 + (e - na))) : nullptr;
         v0[q] = v1[q] = u32x4{0, 0, 0, 0};
-        if (e < m) {
+        if (!Wide && e < m) {
             v0[q] = gld<u32x4>(src[q]);
             if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
         }
@@ -409,11 +413,22 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         const uint32_t g = d0 + pos;
         const uint32_t kb = g / vcm;
         uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
-        gst<u32x4>(dst, v0[q]);
-        if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
-        // (Loading a wide value's chunks together cost this kernel 90 VGPRs:
-        // the id trees' values are 32 bytes, so a wide value copies in sequence.)
-        for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
+        if constexpr (Wide) {
+            asm volatile("" ::: "memory"); // one element's chunks live at a time
+            constexpr uint32_t kChunks = 8;   // 128 bytes
+            u32x4 r[kChunks];
+#pragma unroll
+            for (uint32_t c = 0; c < kChunks; c++)
+                if (16 * c < vs) r[c] = gld<u32x4>(src[q] + 16 * c);
+#pragma unroll
+            for (uint32_t c = 0; c < kChunks; c++)
+                if (16 * c < vs) gst<u32x4>(dst + 16 * c, r[c]);
+            for (uint32_t c = 16 * kChunks; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
+        } else {
+            gst<u32x4>(dst, v0[q]);
+            if (vs >= 32) gst<u32x4>(dst + 16, v1[q]);
+            for (uint32_t c = 32; c < vs; c += 16) gst<u32x4>(dst + c, gld<u32x4>(src[q] + c));
+        }
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(&s_bad, 1u);
     __syncthreads();
@@ -424,6 +439,9 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
 }
 
 // `per_wg` consecutive tiles per workgroup (fewer, longer-lived workgroups).
+// Wide: the tiles of jobs whose values exceed 32 bytes (the other launch
+// takes the rest).
+template <bool Wide>
 __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
                                                                  const UniqueSplit *usplits, JobResultDev *res,
                                                                  uint32_t per_wg) {
@@ -433,14 +451,14 @@ __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *
         if (g >= total) return;
         const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
         const JobDesc &j = jobs[ji];
-        if (!j.unique || g - j.utile_base >= j.utile_count) continue; // uniform
+        if (!j.unique || g - j.utile_base >= j.utile_count || (j.value_size > 32) != Wide) continue; // uniform
         const uint32_t t = g - j.utile_base;
         if (i) __syncthreads(); // the previous tile's LDS readers are done
         switch (j.key_kind) {
-        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp>(unique_lds, j, t, usplits, res); break;
-        case kKeyIdU128: merge_unique_tile<kKeyIdU128>(unique_lds, j, t, usplits, res); break;
-        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64>(unique_lds, j, t, usplits, res); break;
-        default: merge_unique_tile<kKeyCompositeU128>(unique_lds, j, t, usplits, res); break;
+        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp, Wide>(unique_lds, j, t, usplits, res); break;
+        case kKeyIdU128: merge_unique_tile<kKeyIdU128, Wide>(unique_lds, j, t, usplits, res); break;
+        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64, Wide>(unique_lds, j, t, usplits, res); break;
+        default: merge_unique_tile<kKeyCompositeU128, Wide>(unique_lds, j, t, usplits, res); break;
         }
     }
 }
@@ -462,8 +480,17 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
     static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
     const uint32_t pw = per_wg < 1 ? 1 : per_wg;
-    hipLaunchKernelGGL(k_merge_unique, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads), unique_lds_bytes(), s,
-                       d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results, pw);
+    bool narrow = false, wide = false;
+    for (int i = 0; i < njobs; i++)
+        if (h_jobs[i].unique) (h_jobs[i].value_size > 32 ? wide : narrow) = true;
+    if (narrow)
+        hipLaunchKernelGGL(k_merge_unique<false>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
+                           unique_lds_bytes(), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results,
+                           pw);
+    if (wide)
+        hipLaunchKernelGGL(k_merge_unique<true>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
+                           unique_lds_bytes(), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results,
+                           pw);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;
