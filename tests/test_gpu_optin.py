@@ -33,3 +33,17 @@ def test_opt_in_paths_bit_exact():
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout, tail
+
+
+@pytest.mark.gpu
+def test_grid_speculation_bit_exact():
+    """TBC_GRID_SPECULATION=1: grid batches merge their UNIQUE_KEYS jobs tile
+    by tile (k_merge_unique), broken speculations recomputed in the front —
+    the grid tests and the 11-bar config-1 lockstep against the oracle."""
+    env = dict(os.environ, TBC_GRID_SPECULATION="1")
+    files = [os.path.join(HERE, f) for f in ("test_gpu_grid.py", "test_gpu_config1.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", *files],
+                       env=env, capture_output=True, text=True, timeout=230)
+    tail = (r.stdout + r.stderr)[-3000:]
+    assert r.returncode == 0, tail
+    assert " passed" in r.stdout and " failed" not in r.stdout, tail

@@ -1565,7 +1565,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // and 4 within noise); TBC_NO_TAIL_FORK=1 keeps them on the engine stream.
     static const bool no_tail_fork = getenv("TBC_NO_TAIL_FORK") != nullptr; // A/B measurement only
     // Pipelined speculated batch (round 4): the speculated bodies are merged
-    // on the engine stream (k_produce_unique) and the chains run on a tail
+    // on the engine stream (k_merge_unique) and the chains run on a tail
     // stream, packed on a share of the CUs, so chains of batches in flight
     // together share the chip (throughput), instead of one fused block pass
     // on the engine stream holding every SIMD (latency: 2,016 chains at once
@@ -1574,13 +1574,17 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // pipelines), or always / never with TBC_CONFIG_PIPELINE / _LATENCY.
     const bool spec_pipe = spec_regime && !(e->flags & TBC_CONFIG_LATENCY) &&
                            ((e->flags & TBC_CONFIG_PIPELINE) || !e->tail_out.empty());
+    // Grid batches may merge speculated jobs tile by tile too (k_merge_unique:
+    // bodies written once, R + W instead of the mask merge + assembly's R +
+    // 2 W), but config 1 measured slower that way (54.2 vs 52.1 ms per step,
+    // one box): its half-bars are small, and the speculation's extra
+    // launches and recompute phase cost more than the assembly they save.
+    // TBC_GRID_SPECULATION=1 turns it on (A/B and its parity tests).
+    static const bool grid_spec = getenv("TBC_GRID_SPECULATION") != nullptr;
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
-        // Grid batches (pipelined fronts) merge speculated jobs tile by tile
-        // (k_merge_unique): bodies written once, R + W instead of the mask
-        // merge + assembly's R + 2 W.
-        d.unique = (spec_regime || (grid_mode && !staged)) && !no_spec &&
+        d.unique = (spec_regime || (grid_mode && !staged && grid_spec)) && !no_spec &&
                    (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) && d.dblock_max > 0;
         any_unique |= d.unique != 0;
     }

@@ -62,6 +62,7 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     c51) run c51 $B --depth 1 --config 5 --no-cpu-baseline ;;
     c1ns) run c1ns TBC_NO_SPECULATION=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c1u) run c1u TBC_UPLOAD_COPY=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    c1gs) run c1gs TBC_GRID_SPECULATION=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c3) run c3 $B --depth 3 --config 3 --no-cpu-baseline ;;
     c4) run c4 $B --depth 3 --config 4 --no-cpu-baseline ;;
     c5) run c5 $B --depth 3 --config 5 --no-cpu-baseline ;;
