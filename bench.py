@@ -417,9 +417,13 @@ def pmc_traffic(kernel: str, config: int = 2):
 
 
 def pmc_step_traffic(config: int, per_step_kernel: str):
-    """PMC HBM bytes of one whole step (every kernel of the profile, weighted
-    by its launches per step; `per_step_kernel` is launched once per step)
-    from the committed profile of this very libtbc.so and config."""
+    """PMC HBM bytes of one steady pipelined step from the committed profile
+    of this very libtbc.so and config: `per_step_kernel` is launched once per
+    such step, every other instantiation counts with its launches per step
+    (rounded). Short-name aliases of an instantiation (tools/traffic.py) are
+    skipped so nothing counts twice, and kernels launched in fewer steps than
+    `per_step_kernel` (the fused first steps of the warmup, which run no
+    k_merge_unique) are left out."""
     import glob
     import hashlib
     from tigerbeetle_amd import abi
@@ -435,7 +439,14 @@ def pmc_step_traffic(config: int, per_step_kernel: str):
         steps = ks[per_step_kernel].get("calls")
         if not steps or any("calls" not in k for k in ks.values()):
             continue
-        return round(sum(k["traffic_bytes"] * k["calls"] for k in ks.values()) / steps), os.path.relpath(f, ROOT)
+        insts = {n for n in ks if "<" in n}
+        total = 0
+        for n, k in ks.items():
+            if "<" not in n and any(i.startswith(n + "<") for i in insts):
+                continue  # alias of its heaviest instantiation
+            if k["calls"] >= steps:
+                total += k["traffic_bytes"] * round(k["calls"] / steps)
+        return total, os.path.relpath(f, ROOT)
     return None, None
 
 
