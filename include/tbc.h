@@ -256,8 +256,10 @@ tbc_status tbc_grid_block_pointer(const tbc_grid *grid, uint64_t address, void *
 /* grid.read_block from storage: stage `count` host block images (block_size
  * bytes each, the on-disk image [0, sector_ceil(size)) is what matters) into
  * the grid, enqueued on the engine stream (no host wait beyond the pinned
- * staging copy). The blocks are marked unverified until a batch validates
- * them. */
+ * staging copy; images in a range registered with tbc_host_register are
+ * copied by DMA, and the call waits for those copies, so every host buffer
+ * may be reused as soon as it returns). The blocks are marked unverified
+ * (before any image lands) until a batch validates them. */
 tbc_status tbc_grid_put_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_blocks,
                                uint32_t count);
 /* grid.write_block towards storage: copy `count` blocks' images
@@ -285,7 +287,9 @@ tbc_status tbc_grid_get_blocks(tbc_grid *grid, const uint64_t *addresses, void *
  * `previous_checksum` is NULL, the block at `previous_address` must be a
  * verified manifest block of this grid (closed by an earlier call); if it is
  * not, nothing is linked: the new blocks keep a zero header checksum (every
- * later read fails validation) and stay unverified.
+ * later read fails validation), are marked unverified, and the next
+ * tbc_synchronize returns TBC_ERR_BLOCK_INVALID (the device found it after
+ * this call returned).
  * TBC_ERR_INVALID_ARGUMENT if a packed header contradicts its address, the
  * chain or ManifestNode.metadata's asserts (schema.zig:534-554). */
 tbc_status tbc_manifest_close_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_images,
@@ -335,6 +339,9 @@ typedef struct tbc_copy {
 } tbc_copy;
 tbc_status tbc_copy_device_batch(tbc_engine *engine, const tbc_copy *copies, uint32_t count);
 tbc_status tbc_memset_device(tbc_engine *engine, void *dst, int value, uint64_t bytes);
+/* Waits for every enqueued call; TBC_ERR_BLOCK_INVALID (once) if the device
+ * found an error in a call that had already returned (a refused manifest
+ * close). */
 tbc_status tbc_synchronize(tbc_engine *engine);
 
 /* ---- vsr.checksum (src/vsr/checksum.zig:50-59) ------------------------------ */

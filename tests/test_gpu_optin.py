@@ -1,10 +1,9 @@
 """The engine's opt-in paths, measured slower and off by default (DESIGN.md
-§3/§4.2), stay bit-exact: the staged merge (TBC_STAGED=1: grid batches,
-pipelined groups, the throughput regime, values-only), the bar-end sort on
-its own stream (TBC_SORT_STREAM=1: pending-sort waits) and tails at the
-highest stream priority (TBC_TAIL_PRIORITY=1). The library reads these once
-per process, so one child process runs the tests that exercise those paths
-with all three set; each of those tests compares with the oracle."""
+§3), stay bit-exact: the bar-end sort on its own stream (TBC_SORT_STREAM=1:
+pending-sort waits) and tails at the highest stream priority
+(TBC_TAIL_PRIORITY=1). The library reads these once per process, so one
+child process runs the tests that exercise those paths with both set; each
+of those tests compares with the oracle."""
 import os
 import subprocess
 import sys
@@ -14,18 +13,18 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SELECT = " or ".join([
-    "test_compaction_parity_throughput_regime",      # throughput regime: staged merge + 4 groups
+    "test_compaction_parity_throughput_regime",      # throughput regime: 4 pipelined groups
     "test_immutable_compaction_after_device_sort",   # sort stream, then a batch that waits on it
     "test_sort_values_batch_of_memtables",
-    "test_two_half_bars_chained_through_the_grid",   # grid batches: staged merge in the front
+    "test_two_half_bars_chained_through_the_grid",   # grid batches
     "test_pipelined_grid_batches_in_flight",
-    "test_values_only_bodies_equal_full_compaction",  # VALUES_ONLY: staged bodies
+    "test_values_only_bodies_equal_full_compaction",  # VALUES_ONLY bodies
 ])
 
 
 @pytest.mark.gpu
 def test_opt_in_paths_bit_exact():
-    env = dict(os.environ, TBC_STAGED="1", TBC_SORT_STREAM="1", TBC_TAIL_PRIORITY="1")
+    env = dict(os.environ, TBC_SORT_STREAM="1", TBC_TAIL_PRIORITY="1")
     files = [os.path.join(HERE, f) for f in ("test_gpu_parity.py", "test_gpu_grid.py", "test_gpu_engine.py",
                                               "test_gpu_split.py")]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", "-k", SELECT,

@@ -99,7 +99,7 @@ def test_gpu_manifest_refuses_to_link_an_untrusted_block():
     A previous address holding a block staged from storage (unverified) or a
     non-manifest block leaves the new blocks unlinked with a zero header
     checksum, so validating them fails; a trusted one links as the oracle."""
-    from tigerbeetle_amd import Engine, Grid
+    from tigerbeetle_amd import Engine, Grid, abi
     bs = 4096
     with Engine(device=0, block_size=bs) as eng:
         grid = Grid(eng, 16)
@@ -109,10 +109,26 @@ def test_gpu_manifest_refuses_to_link_an_untrusted_block():
             for prev in (3, 7):  # 3: staged from storage (unverified); 7: never written (not a manifest block)
                 images = manifest.pack_blocks(_infos(31, 2), [9, 10], CLUSTER, bs, previous_address=prev)
                 manifest.close_on_grid(grid, images, [9, 10], previous_address=prev, previous_checksum=None)
+                with pytest.raises(abi.TbcError) as err:  # the refusal is reported
+                    eng.synchronize()
+                assert err.value.status == abi.TBC_ERR_BLOCK_INVALID
+                eng.synchronize()  # reported once
                 got = grid.get_blocks([9, 10])
                 assert not got[:, :16].any(), prev  # header checksums left zero
                 res = eng.validate_blocks([grid.pointer(9), grid.pointer(10)], [0, 0], [9, 10])
                 assert all(r == 1 for r in res), res  # invalid_checksum
+            # an address reused after a checkpoint, verified from
+            # its earlier block (6, closed above), refused again: its verified
+            # byte is cleared, so a later close cannot link onto it.
+            images = manifest.pack_blocks(_infos(31, 3), [6], CLUSTER, bs, previous_address=7)
+            manifest.close_on_grid(grid, images, [6], previous_address=7, previous_checksum=None)
+            with pytest.raises(abi.TbcError):
+                eng.synchronize()
+            images = manifest.pack_blocks(_infos(31, 4), [11], CLUSTER, bs, previous_address=6)
+            manifest.close_on_grid(grid, images, [11], previous_address=6, previous_checksum=None)
+            with pytest.raises(abi.TbcError):  # 6 is no longer trusted: refused
+                eng.synchronize()
+            assert not grid.get_blocks([6, 11])[:, :16].any()
         finally:
             grid.close()
 

@@ -549,19 +549,25 @@ __global__ __launch_bounds__(1024) void k_manifest_bodies(const uint64_t *addres
 // The grid's previous block is only linked if it is a verified manifest block
 // (BlockType.manifest = 3, schema.zig:63): otherwise nothing is chained, the
 // closed blocks keep a zero header checksum (so any later read fails
-// read_block_validate) and stay unverified. Linked blocks are marked verified
-// here, one store per block.
+// read_block_validate), their verified bytes are cleared (an address reused
+// after a checkpoint may still be marked from its earlier block) and the
+// refusal is reported in the engine's error word (tbc_synchronize returns
+// TBC_ERR_BLOCK_INVALID). Linked blocks are marked verified here, one store
+// per block.
 __global__ __launch_bounds__(64) void k_manifest_chain(const uint64_t *addresses, uint32_t count, uint8_t *grid_base,
                                                        uint32_t block_size, uint64_t previous_address,
-                                                       const uint64_t *previous_checksum, uint8_t *verified) {
+                                                       const uint64_t *previous_checksum, uint8_t *verified,
+                                                       uint32_t *error) {
     __shared__ uint32_t sT[kTableDwords];
     __shared__ uint32_t hdr[64];
     const uint32_t lane = threadIdx.x;
     if (!previous_checksum && previous_address) {
         const uint8_t *pb = grid_base + (size_t)(previous_address - 1) * block_size;
         if (!verified[previous_address - 1] || pb[240] != 3) { // not a trusted manifest block: refuse to link
+            for (uint32_t i = lane; i < count; i += 64) verified[addresses[i] - 1] = 0;
             for (uint32_t i = 0; i < count; i++)
                 if (lane < 4) gst<uint32_t>(grid_base + (size_t)(addresses[i] - 1) * block_size + 4 * lane, 0u);
+            if (lane == 0) gst<uint32_t>(error, 1u);
             return;
         }
     }
@@ -1184,10 +1190,7 @@ template <int KL> __device__ __forceinline__ Key<KL> key_lds(const uint64_t *key
 template <int KIND, int VW>
 __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
                                                     uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
-                                                    uint64_t *stage, uint64_t *probe, const uint32_t *cons) {
-    // probe (timing probe only): wall-clock ticks spent waiting for windows,
-    // searching, in the histogram, in the rest, and the step count.
-    uint64_t t_wait = 0, t_search = 0, t_hist = 0, t_rest = 0, steps = 0, t_mark = wall_clock64();
+                                                    uint64_t *stage, const uint32_t *cons) {
     constexpr int KL = KeyLimbs<KIND>::value;
     constexpr uint32_t W = 128;
     const uint32_t lane = threadIdx.x & 63;
@@ -1245,11 +1248,6 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
     uint32_t out = 0, published = 0;
     while (out < cnt) {
         const uint32_t E = cnt - out < W ? cnt - out : W;
-        if (probe) {
-            const uint64_t t = wall_clock64();
-            t_rest += t - t_mark;
-            t_mark = t;
-        }
         Key<KL> ka[2], kb[2];
         bool ta[2];
 #pragma unroll
@@ -1268,12 +1266,6 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(prog, (out * vs) & ~255u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             published = out;
-        }
-        if (probe) {
-            asm volatile("" ::"v"(ka[0].l[0]), "v"(kb[1].l[0]));
-            const uint64_t t = wall_clock64();
-            t_wait += t - t_mark;
-            t_mark = t;
         }
         // The B window's keys into this wave's LDS (limb-major, 128 per limb).
 #pragma unroll
@@ -1310,12 +1302,6 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
                 }
             }
         }
-        if (probe) {
-            asm volatile("" ::"v"(lo[0]), "v"(lo[1]));
-            const uint64_t t = wall_clock64();
-            t_search += t - t_mark;
-            t_mark = t;
-        }
         // Histogram of the A ranks, prefix: A values at or before each B position.
 #pragma unroll
         for (int q = 0; q < 2; q++)
@@ -1325,13 +1311,6 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint32_t c0 = wave_scan_incl(hist[lane]), c1 = wave_scan_incl(hist[lane + 64]);
         c1 += __builtin_amdgcn_readlane((int)c0, 63);
-        if (probe) {
-            asm volatile("" ::"v"(c0), "v"(c1));
-            const uint64_t t = wall_clock64();
-            t_hist += t - t_mark;
-            t_mark = t;
-            steps++;
-        }
         uint32_t pos_a[2], pos_b[2];
         bool ea[2], eb[2];
         pos_a[0] = lane + lo[0];
@@ -1398,26 +1377,14 @@ __device__ __forceinline__ void produce_unique_wide(const JobDesc &j, uint32_t k
         __hip_atomic_fetch_add(j.spec_any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) __hip_atomic_store(prog, len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (probe && lane == 0) {
-        t_rest += wall_clock64() - t_mark;
-        probe[0] = t_wait;
-        probe[1] = t_search;
-        probe[2] = t_hist;
-        probe[3] = t_rest;
-        probe[4] = steps;
-    }
 }
 
 template <int KIND>
 __device__ __forceinline__ void produce_unique_vs(const JobDesc &j, uint32_t k, uint32_t cnt, const SplitDesc &sp,
                                                   uint8_t *body, uint32_t *prog, uint32_t *err, uint32_t *spec,
-                                                  uint64_t *stage, uint32_t phase, const uint32_t *cons) {
-    // Timing probe (TBC_PROBE_PRODUCERS_ONLY, no chains): the block's header
-    // bytes receive the producer's time split.
-    uint64_t *probe = phase == kPhaseProducersOnly ? (uint64_t *)(body - kHeaderSize) : nullptr;
-    if (phase == kPhaseProducersOnly) cons = nullptr; // no chains to wait for
-    if (j.value_size == 32) produce_unique_wide<KIND, 2>(j, k, cnt, sp, body, prog, err, spec, stage, probe, cons);
-    else if (j.value_size == 16) produce_unique_wide<KIND, 1>(j, k, cnt, sp, body, prog, err, spec, stage, probe, cons);
+                                                  uint64_t *stage, const uint32_t *cons) {
+    if (j.value_size == 32) produce_unique_wide<KIND, 2>(j, k, cnt, sp, body, prog, err, spec, stage, cons);
+    else if (j.value_size == 16) produce_unique_wide<KIND, 1>(j, k, cnt, sp, body, prog, err, spec, stage, cons);
     else produce_unique<KIND, 0>(j, k, cnt, sp, body, prog, err, spec, stage, cons);
 }
 
@@ -1490,7 +1457,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
         if (!locate(mine, ji, k)) return;
         const JobDesc &j = jobs[ji];
-        if (j.unique && phase != 1 && phase != kPhaseChainsAlone) { // speculated: merges the block's values itself
+        if (j.unique && phase != 1) { // speculated: merges the block's values itself
             uint8_t *blk = block_ptr(j, data_block_slot(k, j.dbcm));
             const SplitDesc sp = bsplits[j.dblock_base + k];
             uint32_t *err = const_cast<uint32_t *>(&res[j.job_index].invariant);
@@ -1499,25 +1466,25 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
             const uint32_t cnt = block_count(j, k);
             switch (j.key_kind) {
             case kKeyTimestamp:
-                produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage,
                                                    &sCons[p]);
                 break;
             case kKeyIdU128:
-                produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage,
                                                    &sCons[p]);
                 break;
             case kKeyCompositeU64:
-                produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage,
                                                    &sCons[p]);
                 break;
             default:
-                produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage, phase,
+                produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, blk + kHeaderSize, &sProg[p], err, spec, stage,
                                                    &sCons[p]);
                 break;
             }
             return;
         }
-        if (sparse_job(j, res) || phase == kPhaseChainsAlone) { // body written by k_assemble (stream order)
+        if (sparse_job(j, res)) { // body written by k_assemble (stream order)
             if (lane == 0)
                 __hip_atomic_store(&sProg[p], block_count(j, k) * j.value_size, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1528,7 +1495,6 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
                      const_cast<uint32_t *>(&res[j.job_index].invariant), sStage[Fused ? p : 0]);
         return;
     }
-    if (phase == kPhaseProducersOnly) return; // timing probe: no chains
     // The chain is the critical path and mostly waits on LDS: let its
     // instructions win the SIMD's issue arbitration over the producers'.
     if constexpr (Fused) __builtin_amdgcn_s_setprio(2);
@@ -1623,16 +1589,16 @@ __global__ __launch_bounds__(64 * kProduceWaves) void k_produce_unique(const Job
     uint32_t *spec = const_cast<uint32_t *>(&res[j.job_index].spec);
     switch (j.key_kind) {
     case kKeyTimestamp:
-        produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
         break;
     case kKeyIdU128:
-        produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
         break;
     case kKeyCompositeU64:
-        produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
         break;
     default:
-        produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], 0u, nullptr);
+        produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
         break;
     }
 }
@@ -1912,14 +1878,14 @@ int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_
 
 int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *grid_base, uint32_t block_size,
                           uint64_t previous_address, const uint64_t *d_previous_checksum, uint8_t *d_verified,
-                          void *stream) {
+                          uint32_t *d_error, void *stream) {
     if (count == 0) return 0;
     const uint32_t wpb = waves_per_block((count + 1) / 2);
     hipLaunchKernelGGL(k_manifest_bodies, dim3(((count + 1) / 2 + wpb - 1) / wpb), dim3(64 * wpb), 0,
                        (hipStream_t)stream, d_addresses, count, grid_base, block_size);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(k_manifest_chain, dim3(1), dim3(64), 0, (hipStream_t)stream, d_addresses, count, grid_base,
-                       block_size, previous_address, d_previous_checksum, d_verified);
+                       block_size, previous_address, d_previous_checksum, d_verified, d_error);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1971,14 +1937,6 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         }
         uint32_t c = waves_per_block(waves);
         c = c > kMaxChainWaves ? kMaxChainWaves : c;
-        static const bool producers_only = getenv("TBC_PROBE_PRODUCERS_ONLY") != nullptr; // timing probe only
-        static const bool chains_alone = getenv("TBC_PROBE_CHAINS_ALONE") != nullptr;      // timing probe only
-        if (chains_alone && phase == 0) {
-            const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, 0u);
-            if (mark) mark(mark_ctx, "probe_assemble");
-        }
         if (phase == 1)
             hipLaunchKernelGGL(k_data_blocks_redo, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
                                total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
@@ -1986,8 +1944,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         else
             hipLaunchKernelGGL(k_data_blocks<true>, dim3((waves + c - 1) / c), dim3(3 * 64 * c), 0, s, d_jobs, njobs,
                                total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
-                               d_splits, c, (const uint32_t *)d_ready, d_bsplits,
-                               producers_only ? kPhaseProducersOnly : chains_alone ? kPhaseChainsAlone : 0u);
+                               d_splits, c, (const uint32_t *)d_ready, d_bsplits, 0u);
         if (hipGetLastError() != hipSuccess) return -1;
     } else if (total_dblocks) {
         // Throughput regime: assemble every body, then the chains, 4 per SIMD.

@@ -162,6 +162,10 @@ struct tbc_engine {
     };
     std::vector<TailOutputs> tail_out;
     int next_tail = 0;
+    // Deferred device-side errors of calls that return before the device
+    // ran them (a manifest close that refused to link): one word, read and
+    // cleared by tbc_synchronize.
+    uint32_t *d_error = nullptr;
     Arena dev, host;
     Staging staging;
     // Host ranges the caller registered (tbc_host_register: hipHostRegister):
@@ -238,10 +242,13 @@ static bool is_registered(const tbc_engine *e, const void *p, uint64_t bytes) {
 }
 
 // Host -> device through the pinned ring, enqueued on the engine stream
-// (registered memory: one direct DMA).
-static bool stage_h2d(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
-    if (is_registered(e, src, bytes))
+// (registered memory: one direct DMA, which still reads the caller's buffer
+// after the call returns: *direct tells the caller to wait for it).
+static bool stage_h2d(tbc_engine *e, void *dst, const void *src, uint64_t bytes, bool *direct = nullptr) {
+    if (is_registered(e, src, bytes)) {
+        if (direct) *direct = true;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) == hipSuccess;
+    }
     Staging &st = e->staging;
     const uint8_t *s = (const uint8_t *)src;
     uint8_t *d = (uint8_t *)dst;
@@ -460,6 +467,9 @@ static bool join_sorts(tbc_engine *e) {
     return !e->sort_recorded || hipStreamWaitEvent(e->stream, e->sort_last, 0) == hipSuccess;
 }
 
+// Every stream of the engine drained (internal: no deferred-error report).
+static bool sync_streams(tbc_engine *e);
+
 // Later work on the engine stream that touches grid blocks (staging blocks in
 // or out, synchronous checks) waits for every batch tail enqueued so far.
 static bool join_tails(tbc_engine *e) {
@@ -543,6 +553,8 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     // values (64 MiB of HBM), so submitting never waits on the device to grow
     // it; a larger batch still grows it (after a stream synchronize).
     ok = ok && ensure_masks(e, kInitialMaskWords);
+    ok = ok && hipMalloc((void **)&e->d_error, 256) == hipSuccess &&
+         hipMemsetAsync(e->d_error, 0, 256, e->stream) == hipSuccess;
     if (!ok) {
         tbc_engine_deinit(e);
         return TBC_ERR_OUT_OF_MEMORY;
@@ -577,6 +589,7 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (e->sort_status) hipFree(e->sort_status);
     if (e->kway_scratch) hipFree(e->kway_scratch);
     if (e->copy_desc) hipFree(e->copy_desc);
+    if (e->d_error) hipFree(e->d_error);
     for (int t = 0; t < e->ntails; t++) {
         if (e->tail_ev[t]) hipEventDestroy(e->tail_ev[t]);
         if (e->tail[t]) hipStreamDestroy(e->tail[t]);
@@ -619,7 +632,7 @@ tbc_status tbc_grid_init(tbc_engine *e, uint64_t block_count, tbc_grid **out) {
 void tbc_grid_deinit(tbc_grid *g) {
     if (!g) return;
     hipSetDevice(g->engine->device);
-    tbc_synchronize(g->engine);
+    sync_streams(g->engine);
     hipFree(g->verified);
     hipFree(g->base);
     delete g;
@@ -647,16 +660,34 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
     hipSetDevice(e->device);
     if (!join_tails(e)) return TBC_ERR_DEVICE; // no running batch reads a block being replaced
     if (!count) return TBC_OK;
+    // Validate before trusting: every staged block's verified byte is cleared
+    // BEFORE any image lands (stream order), so a call that fails halfway
+    // never leaves an untrusted image marked verified. One launch per address
+    // list that fits a staging slot.
+    constexpr uint32_t kChunk = (uint32_t)(Staging::kSlotBytes / 8);
+    for (uint32_t c0 = 0; c0 < count; c0 += kChunk) {
+        const uint32_t n = count - c0 < kChunk ? count - c0 : kChunk;
+        uint64_t region = 0;
+        const uint64_t *d_addr = stage_u64s(e, addresses + c0, n, &region);
+        if (!d_addr) return TBC_ERR_DEVICE;
+        const bool ok = launch_grid_set_verified(d_addr, n, g->verified, 0, e->stream) == 0;
+        e->dev.close(region);
+        if (!ok) return TBC_ERR_DEVICE;
+    }
+    bool direct = false;
     for (uint32_t i = 0; i < count; i++)
-        if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size))
+        if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size, &direct))
             return TBC_ERR_DEVICE;
-    // Validate before trusting: one launch clears every staged block's verified byte.
-    uint64_t region = 0;
-    const uint64_t *d_addr = stage_u64s(e, addresses, count, &region);
-    if (!d_addr) return TBC_ERR_DEVICE;
-    const bool ok = launch_grid_set_verified(d_addr, count, g->verified, 0, e->stream) == 0;
-    e->dev.close(region);
-    return ok ? TBC_OK : TBC_ERR_DEVICE;
+    // A registered source is read by DMA after the enqueue: the caller may
+    // reuse its buffer once this returns, so wait for those copies (pageable
+    // sources were already copied into the pinned ring).
+    if (direct) {
+        hipEvent_t ev = take_event(e);
+        const bool ok = ev && hipEventRecord(ev, e->stream) == hipSuccess && hipEventSynchronize(ev) == hipSuccess;
+        if (ev) e->event_pool.push_back(ev);
+        if (!ok) return TBC_ERR_DEVICE;
+    }
+    return TBC_OK;
 }
 
 tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *const *blocks, uint32_t count) {
@@ -706,11 +737,18 @@ tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, con
     Staging &st = e->staging;
     const uint64_t meta = 8ull * count + 16;
     if (meta > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
+    bool direct = false;
     for (uint32_t i = 0; i < count; i++) {
         uint32_t size;
         memcpy(&size, (const uint8_t *)host_images[i] + 96, 4);
-        if (!stage_h2d(e, g->base + (addresses[i] - 1) * bs, host_images[i], sector_ceil(size)))
+        if (!stage_h2d(e, g->base + (addresses[i] - 1) * bs, host_images[i], sector_ceil(size), &direct))
             return TBC_ERR_DEVICE;
+    }
+    if (direct) { // registered images are read by DMA after the enqueue: done before returning
+        hipEvent_t ev = take_event(e);
+        const bool ok = ev && hipEventRecord(ev, e->stream) == hipSuccess && hipEventSynchronize(ev) == hipSuccess;
+        if (ev) e->event_pool.push_back(ev);
+        if (!ok) return TBC_ERR_DEVICE;
     }
     const int slot = st.next;
     st.next = (st.next + 1) % Staging::kSlots;
@@ -730,7 +768,7 @@ tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, con
     bool ok = hipMemcpyAsync(d, host, meta, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
               launch_manifest_close((const uint64_t *)d, count, g->base, bs, previous_address,
                                     previous_checksum ? (const uint64_t *)(d + 8ull * count) : nullptr, g->verified,
-                                    e->stream) == 0 &&
+                                    e->d_error, e->stream) == 0 &&
               hipEventRecord(st.ev[slot], e->stream) == hipSuccess;
     st.used[slot] = true;
     e->dev.close(region);
@@ -826,7 +864,7 @@ tbc_status tbc_host_unregister(tbc_engine *e, void *ptr) {
     for (size_t i = 0; i < e->registered.size(); i++)
         if (e->registered[i].first == lo) {
             // Copies from or into it may still be enqueued.
-            if (tbc_synchronize(e) != TBC_OK) return TBC_ERR_DEVICE;
+            if (!sync_streams(e)) return TBC_ERR_DEVICE;
             e->registered.erase(e->registered.begin() + (long)i);
             return hipHostUnregister(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
         }
@@ -929,14 +967,26 @@ tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
-tbc_status tbc_synchronize(tbc_engine *e) {
-    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+static bool sync_streams(tbc_engine *e) {
     hipSetDevice(e->device);
     bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
     for (int t = 0; t < e->ntails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
     ok = ok && (!e->sort_stream || hipStreamSynchronize(e->sort_stream) == hipSuccess);
     retire_sorts(e);
-    return ok ? TBC_OK : TBC_ERR_DEVICE;
+    return ok;
+}
+
+tbc_status tbc_synchronize(tbc_engine *e) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    if (!sync_streams(e)) return TBC_ERR_DEVICE;
+    // Errors the device recorded for calls that had already returned.
+    uint32_t err = 0;
+    if (hipMemcpy(&err, e->d_error, 4, hipMemcpyDeviceToHost) != hipSuccess) return TBC_ERR_DEVICE;
+    if (err) {
+        if (hipMemset(e->d_error, 0, 4) != hipSuccess) return TBC_ERR_DEVICE;
+        return TBC_ERR_BLOCK_INVALID;
+    }
+    return TBC_OK;
 }
 
 tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const uint64_t *lengths, uint32_t count,
@@ -1498,7 +1548,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         d.out_offset = c.output_offset;
         d.out_blocks = grid ? nullptr : (uint8_t *)c.output_blocks;
         d.grid_base = grid ? c.grid->base : nullptr;
-        d.merge_tile = kMergeTile; // the staged merge's tile is set below, with the regime
+        d.merge_tile = kMergeTile;
         d.dblock_max = (uint32_t)db_max;
         d.table_max = (uint32_t)tables_max;
         d.job_index = i;
@@ -1506,23 +1556,11 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         addr_words += c.address_count;
         order[i] = i;
     }
-    // The staged merge (merge.hip k_merge_staged: values read once into
-    // registers, written straight to their output slots) can serve every
-    // batch whose bodies are not built beside their chains: grid batches,
-    // pipelined groups, VALUES_ONLY and the throughput regime. It moves R + W
-    // where the mask merge + k_assemble move R + 2 W, but measured slower
-    // (round 3, one box: config 5 19.9 vs 15.0 ms, its four fronts 16.7 vs
-    // 10.8 ms of kernel time; its tiles hold 64 KiB of registers each and
-    // serialise on the look-back beside the chain workgroups), so it is
-    // opt-in: TBC_STAGED=1 (A/B measurement and its parity tests).
-    uint64_t dblocks_all = 0;
-    for (uint32_t i = 0; i < count; i++) dblocks_all += hj[i].dblock_max;
-    const bool staged_on = staged_variant() != 0;
-    const bool staged = staged_on && (grid_mode || pipeline || (flags0 & TBC_COMPACTION_VALUES_ONLY) ||
-                                      (dblocks_all + 1) / 2 > fused_max_chain_waves());
+    // (Round 3's staged merge — values held in registers across a look-back,
+    // R + W — measured slower than the mask merge + k_assemble and was
+    // removed in round 5)
     for (uint32_t i = 0; i < count; i++) {
         JobDesc &d = hj[i];
-        if (staged) d.merge_tile = staged_tile(d.value_size);
         const uint64_t n = (uint64_t)d.a.n + d.b.n;
         d.tile_count = (uint32_t)((n + d.merge_tile - 1) / d.merge_tile);
     }
@@ -1531,7 +1569,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hj[x].key_kind < hj[y].key_kind; });
     uint64_t all_tiles = 0;
     for (uint32_t i = 0; i < count; i++) all_tiles += hj[i].tile_count;
-    if (!staged && !ensure_masks(e, all_tiles * (2 * kMergeTile / 64))) {
+    if (!ensure_masks(e, all_tiles * (2 * kMergeTile / 64))) {
         delete b;
         return TBC_ERR_OUT_OF_MEMORY;
     }
@@ -1584,7 +1622,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
-        d.unique = (spec_regime || (grid_mode && !staged && grid_spec)) && !no_spec &&
+        d.unique = (spec_regime || (grid_mode && grid_spec)) && !no_spec &&
                    (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) && d.dblock_max > 0;
         any_unique |= d.unique != 0;
     }
@@ -1643,8 +1681,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     uint32_t *d_ready = d_block_tile + dblocks;
     uint64_t *d_lookback = (uint64_t *)(uintptr_t)align_up((uint64_t)(uintptr_t)(d_ready + dblocks + 2), 8);
     uint32_t *d_ticket = (uint32_t *)(d_lookback + tiles);
-    const bool merge_bodies = staged;
-    uint64_t *m_lb = staged ? d_lookback : nullptr;
+    const bool merge_bodies = false;
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
     b->h_results = (JobResultDev *)(hbase + sz_in);
@@ -1766,10 +1803,10 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                      mark_cb, b) == 0;
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
         if (ok && any_unique)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b, 1) == 0;
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
@@ -1808,7 +1845,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // chains run beside the next group's merge and body assembly.
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
@@ -1840,7 +1877,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         b->count_only = true;
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b, nullptr, d_ticket, d_ready) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res, hipMemcpyDeviceToHost, s) == hipSuccess;
         ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     } else if (any_unique && spec_pipe) {
@@ -1858,7 +1895,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             mark_cb(b, "partition_blocks");
         }
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
+                                d_res, s, mark_cb, b, 0) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 0, s) == 0;
         mark_cb(b, "assemble");
         if (!unique_tiles) {
@@ -1866,7 +1903,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             mark_cb(b, "produce");
         }
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+                                d_res, s, mark_cb, b, 1) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 1, s) == 0;
         mark_cb(b, "recompute_assemble");
         const int ti = e->next_tail;
@@ -1901,12 +1938,12 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
         mark_cb(b, "partition_blocks");
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
+                                d_res, s, mark_cb, b, 0) == 0;
         ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
                                  d_block_tile, d_splits, false, maybe_sparse, s, mark_cb, b, false, d_bsplits, 0,
                                  false) == 0;
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+                                d_res, s, mark_cb, b, 1) == 0;
         ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
                                  d_block_tile, d_splits, false, true, s, mark_cb, b, false, d_bsplits, 1, false) == 0;
         // The index blocks and the results go to a tail stream, so the next
@@ -1939,12 +1976,12 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
         mark_cb(b, "partition_blocks");
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 0) == 0;
+                                d_res, s, mark_cb, b, 0) == 0;
         ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
                                  d_block_tile, d_splits, false, maybe_sparse, s, mark_cb, b, false, d_bsplits, 0,
                                  false) == 0;
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, nullptr, d_ticket, d_ready, 1) == 0;
+                                d_res, s, mark_cb, b, 1) == 0;
         ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
                                  d_block_tile, d_splits, false, true, s, mark_cb, b, false, d_bsplits, 1, true) == 0;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
@@ -1952,7 +1989,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     } else {
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b, m_lb, d_ticket, d_ready) == 0;
+                              d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
         if (ok && count)
             ok = launch_blocks((const JobDesc *)d_in, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos,
                                d_status, e->masks, d_block_tile, d_splits, (flags0 & TBC_COMPACTION_VALUES_ONLY) != 0,
@@ -1961,7 +1998,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     }
     if (!ok) {
-        tbc_synchronize(e);
+        sync_streams(e);
         tbc_batch_release(b);
         return TBC_ERR_DEVICE;
     }
@@ -2177,7 +2214,7 @@ tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **ou
               hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess &&
               hipEventRecord(b->done, s) == hipSuccess;
     if (!ok) {
-        tbc_synchronize(e);
+        sync_streams(e);
         tbc_batch_release(b);
         return TBC_ERR_DEVICE;
     }

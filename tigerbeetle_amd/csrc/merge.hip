@@ -29,16 +29,7 @@
 #include "tbc_internal.h"
 #include "keys.h"
 
-#ifndef TBC_ABLATE
-#define TBC_ABLATE 0 // timing experiments only: 4 = no key loads
-#endif
-
 namespace tbc {
-
-int staged_variant() {
-    static const int v = getenv("TBC_STAGED") ? 1 : 0;
-    return v;
-}
 
 __device__ __forceinline__ uint32_t load_tomb(const uint8_t *v, uint32_t ts_off) {
     return (uint32_t)(ld64(v + ts_off) >> 63);
@@ -477,9 +468,7 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
     (void)d_ticket;
-    // TBC_UNIQUE_PER_WG (A/B measurement): tiles per workgroup.
-    static const uint32_t per_wg = getenv("TBC_UNIQUE_PER_WG") ? (uint32_t)atoi(getenv("TBC_UNIQUE_PER_WG")) : 1u;
-    const uint32_t pw = per_wg < 1 ? 1 : per_wg;
+    const uint32_t pw = 1; // one tile per workgroup (2 and 4 measured slower)
     bool narrow = false, wide = false;
     for (int i = 0; i < njobs; i++)
         if (h_jobs[i].unique) (h_jobs[i].value_size > 32 ? wide : narrow) = true;
@@ -583,12 +572,8 @@ __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *o
         for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
         uint32_t tb = 0;
         if (ptrs[r]) {
-#if TBC_ABLATE & 4
-            k.l[0] = (uint64_t)(uintptr_t)ptrs[r];
-#else
             k = load_key<KIND>(ptrs[r], ts);
             if (e < ea) tb = load_tomb(ptrs[r], ts);
-#endif
         }
 #pragma unroll
         for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
@@ -705,295 +690,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_tile(const JobDesc *job
     merge_tile<KIND>(jobs, order, order_offset, splits, status, masks, res, phase, blockIdx.x);
 }
 
-// --------------------------------------------------------------------------
-// Staged merge (batches whose bodies are not built beside their chains:
-// grid batches, pipelined job groups, the throughput regime, VALUES_ONLY):
-// a tile's input values are read ONCE, into registers (up to 64 KiB per
-// workgroup, 16-byte chunks, lane groups per value: coalesced), their keys
-// go to LDS, the survivor rules decide each merged position, the tile takes
-// its output offset by decoupled look-back (tiles in ticket order, so every
-// tile looked back on is running or done), and the surviving values go from
-// registers straight to their output slots. R + W of HBM traffic, where
-// merge + k_assemble moved R + 2 W (the values re-read after the masks).
-// The last tile of a job writes its results (write_blocks' shape,
-// compaction.zig:806-850); every tile counts its survivors into the data
-// blocks they land in (checked by the chain kernel).
-// --------------------------------------------------------------------------
-constexpr uint32_t kStagedThreads = 256;
-constexpr uint32_t kStagedChunks = 16;   // 16-byte chunks per thread: 64 KiB of values per tile
-constexpr uint32_t kStagedMaxTile = 1024;
-static_assert(kStagedThreads * kStagedChunks * 16 == 65536, "64 KiB of staged values");
-
-
-template <int KIND>
-__global__ __launch_bounds__(kStagedThreads) void k_merge_staged(const JobDesc *jobs, const TileRef *order,
-                                                                 uint32_t order_offset, const SplitDesc *splits,
-                                                                 uint64_t *lookback, uint32_t *ticket,
-                                                                 uint32_t *ready, JobResultDev *res) {
-    constexpr int KL = KeyLimbs<KIND>::value;
-    __shared__ uint64_t s_key[KL][kStagedMaxTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
-    __shared__ uint8_t s_tomb[kStagedMaxTile + 4];
-    __shared__ uint32_t s_dst[kStagedMaxTile];         // per slot: tile-local output rank, or ~0
-    __shared__ uint32_t s_seg_pre[2][kSegWindow + 1];
-    __shared__ uint64_t s_seg_ptr[2][kSegWindow];
-    __shared__ uint32_t s_wsum[kStagedThreads / 64];
-    __shared__ uint32_t s_ticket, s_excl;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_ticket = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const TileRef ref = order[order_offset + s_ticket];
-    const JobDesc &j = jobs[ref.job];
-    const uint32_t t = ref.tile, T = j.merge_tile;
-    const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
-    const uint32_t d0 = t * T, d1 = (d0 + T) < n ? d0 + T : n;
-    const SplitDesc s0 = splits[j.split_base + t];
-    const uint32_t i0 = s0.i, i1 = splits[j.split_base + t + 1].i;
-    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
-    const uint32_t na = i1 - i0, nb = j1 - j0, slots = na + nb;
-    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
-    const uint32_t cpv_log = __builtin_ctz(vs >> 4);
-    const bool immutable = j.a_immutable != 0, secondary = j.usage == 1, drop = j.drop_tombstones != 0;
-    const uint32_t ea = na + 2;
-
-    if (tid < 2 * (kSegWindow + 1)) {
-        const uint32_t side = tid / (kSegWindow + 1), k = tid % (kSegWindow + 1);
-        const Stream &st = side == 0 ? j.a : j.b;
-        const uint32_t seg = (side == 0 ? s0.seg_a : s0.seg_b) + k;
-        s_seg_pre[side][k] = seg <= st.nseg && st.nseg ? gld<uint32_t>(st.seg_pre + seg) : 0xffffffffu;
-        if (k < kSegWindow) s_seg_ptr[side][k] = seg < st.nseg ? gld<uint64_t>(st.seg_ptr + seg) : 0;
-    }
-    __syncthreads();
-    // Element `idx` of stream `side` (inside the tile's segment window, or found globally).
-    auto elem = [&](uint32_t side, uint32_t idx) -> const uint8_t * {
-        uint32_t k = 0;
-        while (k + 1 < kSegWindow && s_seg_pre[side][k + 1] <= idx) k++;
-        if (k + 1 == kSegWindow && s_seg_pre[side][k + 1] <= idx) {
-            const Stream &st = side == 0 ? j.a : j.b;
-            return elem_ptr(st, seg_search(st, idx), idx, vs);
-        }
-        return (const uint8_t *)s_seg_ptr[side][k] + (size_t)(idx - s_seg_pre[side][k]) * vs;
-    };
-
-    // 1. Values into registers: chunk g = slot * cpv + c (16 bytes), thread
-    //    tid holds chunks tid + 256 r. A slot e < na is A[i0 + e], else B[j0 + e - na].
-    const uint32_t chunks = slots << cpv_log;
-    u32x4 v[kStagedChunks];
-#pragma unroll
-    for (uint32_t r = 0; r < kStagedChunks; r++) {
-        const uint32_t g = tid + kStagedThreads * r;
-        if (g < chunks) {
-            const uint32_t e = g >> cpv_log, c = g & ((1u << cpv_log) - 1);
-            const uint8_t *p = e < na ? elem(0, i0 + e) : elem(1, j0 + (e - na));
-            v[r] = gld<u32x4>(p + 16 * c);
-        }
-    }
-    // Boundary keys: A[i0 - 1], A[i1], B[j1] (max when absent).
-    if (tid < 3) {
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
-        uint32_t tb = 0, entry = 0;
-        if (tid == 0) {
-            entry = 0;
-            if (i0 >= 1) {
-                const uint8_t *p = elem_ptr(j.a, seg_search(j.a, i0 - 1), i0 - 1, vs);
-                k = load_key<KIND>(p, ts);
-                tb = load_tomb(p, ts);
-            }
-        } else if (tid == 1) {
-            entry = na + 1;
-            if (i1 < na_all) {
-                const uint8_t *p = elem_ptr(j.a, seg_search(j.a, i1), i1, vs);
-                k = load_key<KIND>(p, ts);
-                tb = load_tomb(p, ts);
-            }
-        } else {
-            entry = ea + nb;
-            if (j1 < nb_all) k = load_key<KIND>(elem_ptr(j.b, seg_search(j.b, j1), j1, vs), ts);
-        }
-#pragma unroll
-        for (int l = 0; l < KL; l++) s_key[l][entry] = k.l[l];
-        if (entry < ea) s_tomb[entry] = (uint8_t)tb;
-    }
-    // Keys (and A tombstones) of the staged slots, from the chunks that hold them.
-#pragma unroll
-    for (uint32_t r = 0; r < kStagedChunks; r++) {
-        const uint32_t g = tid + kStagedThreads * r;
-        if (g >= chunks) continue;
-        const uint32_t e = g >> cpv_log, c = g & ((1u << cpv_log) - 1);
-        const uint32_t entry = e < na ? e + 1 : ea + (e - na);
-#pragma unroll
-        for (int l = 0; l < KL; l++) {
-            const uint32_t o = key_limb_off<KIND>(l, ts);
-            if ((o >> 4) != c) continue;
-            uint64_t w = (o & 8) ? ((uint64_t)v[r].w << 32 | v[r].z) : ((uint64_t)v[r].y << 32 | v[r].x);
-            if (l == 0 && KIND != kKeyIdU128) w &= ~kTombstoneBit;
-            s_key[l][entry] = w;
-        }
-        if (e < na && (ts >> 4) == c) {
-            const uint32_t hi = (ts & 8) ? v[r].w : v[r].y;
-            s_tomb[entry] = (uint8_t)(hi >> 31);
-        }
-    }
-    __syncthreads();
-
-    auto entry_key = [&](uint32_t e) {
-        Key<KL> k;
-#pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = s_key[l][e];
-        return k;
-    };
-    auto run_len = [&](uint32_t ia) { // run of equal keys ending at A[ia] (secondary-index dedup)
-        const Key<KL> k = entry_key(ia - i0 + 1);
-        uint32_t len = 1;
-        int64_t idx = (int64_t)ia - 1;
-        while (idx >= 0) {
-            Key<KL> kk;
-            if (idx >= (int64_t)i0 - 1) kk = entry_key((uint32_t)(idx - ((int64_t)i0 - 1)));
-            else kk = load_key<KIND>(elem_ptr(j.a, seg_search(j.a, (uint32_t)idx), (uint32_t)idx, vs), ts);
-            if (!key_eq(kk, k)) break;
-            len++;
-            idx--;
-        }
-        return len;
-    };
-
-    // 2. Survivor rules (merge_tile's), kPer merged positions per thread.
-    const uint32_t kPer = T / kStagedThreads; // 1, 2 or 4
-    const uint32_t dd = kPer * tid < slots ? kPer * tid : slots;
-    uint32_t a, b;
-    {
-        uint32_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (key_le(entry_key(1 + mid), entry_key(ea + dd - 1 - mid))) lo = mid + 1;
-            else hi = mid;
-        }
-        a = lo;
-        b = dd - lo;
-    }
-    uint32_t slot_of[4], surv_bits = 0, mine = 0;
-    for (uint32_t k = 0; k < kPer; k++) {
-        slot_of[k] = ~0u;
-        if (dd + k >= slots) continue;
-        const bool take_a = a < na && (b >= nb || key_le(entry_key(1 + a), entry_key(ea + b)));
-        bool surv;
-        if (take_a) {
-            const uint32_t ia = i0 + a, e = a + 1;
-            const Key<KL> ka = entry_key(e);
-            bool dedup = true;
-            if (immutable) {
-                dedup = !((ia + 1 < na_all) && key_eq(entry_key(e + 1), ka));
-                if (dedup && secondary) dedup = (run_len(ia) & 1) != 0;
-            }
-            const bool eq_b = (b < nb || j1 < nb_all) && key_eq(entry_key(ea + b), ka);
-            surv = dedup && !(drop && s_tomb[e]) && !(secondary && eq_b);
-            slot_of[k] = a;
-            a++;
-        } else {
-            const Key<KL> kb = entry_key(ea + b);
-            bool a_exists = (i0 + a) >= 1 && key_eq(entry_key(a), kb);
-            if (a_exists && immutable && secondary) a_exists = (run_len(i0 + a - 1) & 1) != 0;
-            surv = !a_exists;
-            slot_of[k] = na + b;
-            b++;
-        }
-        surv_bits |= (surv ? 1u : 0u) << k;
-        mine += surv ? 1u : 0u;
-    }
-    // Tile-local ranks: exclusive scan of the per-thread survivor counts.
-    uint32_t incl = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    uint32_t woff = 0, cnt = 0;
-    for (uint32_t w = 0; w < kStagedThreads / 64; w++) {
-        woff += w < wave ? s_wsum[w] : 0u;
-        cnt += s_wsum[w];
-    }
-    uint32_t rank = woff + incl - mine;
-    for (uint32_t k = 0; k < kPer; k++) {
-        if (slot_of[k] == ~0u) continue;
-        const bool sv = (surv_bits >> k) & 1u;
-        s_dst[slot_of[k]] = sv ? rank : ~0u;
-        rank += sv ? 1u : 0u;
-    }
-
-    // 3. The job's survivors before this tile: decoupled look-back, wave 0
-    //    reading 64 predecessors per round trip (nearest first).
-    constexpr uint64_t kAgg = 1ull << 62, kPre = 2ull << 62, kCnt = (1ull << 62) - 1;
-    if (wave == 0) {
-        uint64_t *lb = lookback + j.tile_base;
-        if (lane == 0) __hip_atomic_store(&lb[t], kAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t excl = 0;
-        int64_t top = (int64_t)t - 1;
-        for (uint32_t spins = 0;;) {
-            const int64_t idx = top - (int64_t)lane;
-            const uint64_t w = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kPre;
-            const uint64_t fl = w >> 62;
-            const uint64_t pre = __ballot(fl == 2);
-            const uint32_t stop = pre ? __builtin_ctzll(pre) : 64u; // nearest inclusive prefix
-            const bool in = lane <= stop;
-            if (__ballot(in && fl == 0)) { // a tile up to the prefix has not published yet
-                if (++spins > (1u << 22)) { // bounded: report instead of hanging
-                    if (lane == 0) gst<uint32_t>(&res[j.job_index].invariant, 0xbeefu);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            uint64_t c = in ? (w & kCnt) : 0;
-            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-            excl += c;
-            if (stop < 64) break;
-            top -= 64;
-        }
-        if (lane == 0) {
-            __hip_atomic_store(&lb[t], kPre | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_excl = (uint32_t)excl;
-        }
-    }
-    __syncthreads();
-    const uint32_t out0 = s_excl, vcm = j.vcm;
-
-    // 4. Survivors from registers to their output slots.
-#pragma unroll
-    for (uint32_t r = 0; r < kStagedChunks; r++) {
-        const uint32_t g = tid + kStagedThreads * r;
-        if (g >= chunks) continue;
-        const uint32_t e = g >> cpv_log, c = g & ((1u << cpv_log) - 1);
-        const uint32_t dst = s_dst[e];
-        if (dst == ~0u) continue;
-        const uint32_t o = out0 + dst, k = o / vcm;
-        gst<u32x4>(block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(o - k * vcm) * vs + 16 * c, v[r]);
-    }
-    // Survivors landed per data block (the chain kernel checks them; the
-    // reader is a later kernel in stream order, so no release fence).
-    if (tid == 0) {
-        uint32_t o = out0;
-        const uint32_t end = out0 + cnt;
-        while (o < end) {
-            const uint32_t k = o / vcm;
-            const uint32_t e = (k + 1) * vcm < end ? (k + 1) * vcm : end;
-            __hip_atomic_fetch_add(ready + j.dblock_base + k, e - o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o = e;
-        }
-        if (t + 1 == j.tile_count) { // the job's shape (k_tile_scan's, from the inclusive prefix)
-            const uint64_t total = (uint64_t)out0 + cnt;
-            const uint32_t db = (uint32_t)((total + vcm - 1) / vcm);
-            const uint32_t tables = (db + j.dbcm - 1) / j.dbcm;
-            JobResultDev &rr = res[j.job_index];
-            rr.value_count = total;
-            rr.data_block_count = db;
-            rr.table_count = tables;
-            rr.block_count = db + tables;
-        }
-    }
-}
-
 // The recomputation phase of a speculating batch: a small grid strides over
 // the tiles (most leave at once, all of them while no speculation broke).
 template <int KIND>
@@ -1065,8 +761,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const JobDesc *jobs,
 template <int KIND>
 static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_jobs, int first, int count,
                        SplitDesc *d_splits, uint64_t *d_status, uint64_t *d_masks, const TileRef *d_order,
-                       uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready, const JobResultDev *d_res,
-                       hipStream_t s) {
+                       const JobResultDev *d_res, hipStream_t s) {
     const JobDesc &f = h_jobs[first];
     const JobDesc &l = h_jobs[first + count - 1];
     const uint32_t split_off = f.split_base;
@@ -1082,10 +777,6 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
     if (ntiles && phase)
         hipLaunchKernelGGL((k_merge_tile_redo<KIND>), dim3(std::min<uint32_t>(ntiles, 1024)), dim3(kMergeThreads), 0,
                            s, d_jobs, d_order, tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_res, ntiles);
-    else if (ntiles && d_lookback)
-        hipLaunchKernelGGL((k_merge_staged<KIND>), dim3(ntiles), dim3(kStagedThreads), 0, s, d_jobs, d_order, tile_off,
-                           (const SplitDesc *)d_splits, d_lookback, d_ticket + KIND, d_ready,
-                           const_cast<JobResultDev *>(d_res));
     else if (ntiles)
         hipLaunchKernelGGL((k_merge_tile<KIND>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,
                            (const SplitDesc *)d_splits, d_status, d_masks, d_res, phase);
@@ -1098,7 +789,7 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
                  uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
                  JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx,
-                 uint64_t *d_lookback, uint32_t *d_ticket, uint32_t *d_ready, uint32_t phase) {
+                 uint32_t phase) {
     hipStream_t s = (hipStream_t)stream;
     bool any = false;
     for (int k = 0; k < njobs; k++) any |= phase == 0 ? !h_jobs[k].unique : h_jobs[k].unique != 0;
@@ -1116,10 +807,10 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     auto run = [&](uint32_t ph) {
         return for_each_kind([&](uint32_t kind, int first, int count) {
             switch (kind) {
-            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
-            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
-            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
-            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_lookback, d_ticket, d_ready, d_results, s);
+            case kKeyTimestamp: return launch_kind<kKeyTimestamp>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_results, s);
+            case kKeyIdU128: return launch_kind<kKeyIdU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_results, s);
+            case kKeyCompositeU64: return launch_kind<kKeyCompositeU64>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_results, s);
+            default: return launch_kind<kKeyCompositeU128>(ph, d_jobs, h_jobs, first, count, d_splits, d_status, d_masks, d_order, d_results, s);
             }
         });
     };
@@ -1132,11 +823,9 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     }
     if (mark) mark(mark_ctx, phase ? "recompute_partition" : "merge_partition");
     if (run(phase)) return -1;
-    if (!d_lookback) { // the staged merge writes the offsets and results itself
-        hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
-                           d_results, phase);
-        if (hipGetLastError() != hipSuccess) return -1;
-    }
+    hipLaunchKernelGGL(k_tile_scan, dim3(njobs), dim3(kScanThreads), 0, s, d_jobs, d_status, d_block_tile,
+                       d_results, phase);
+    if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, phase ? "recompute_merge" : "merge");
     return 0;
 }

@@ -30,14 +30,6 @@ constexpr uint64_t kTombstoneBit = 1ull << 63;
 constexpr uint32_t kMergeTile = 2048;
 static_assert(2 * (kMergeTile / 64) == 64, "one mask word per lane");
 constexpr uint32_t kMergeThreads = kMergeTile / 4;
-// Tile of the staged merge (merge.hip k_merge_staged): its values are held
-// in registers, 64 KiB per workgroup at most.
-__host__ __device__ inline uint32_t staged_tile(uint32_t value_size) {
-    return value_size <= 64 ? 1024u : 65536u / value_size;
-}
-// TBC_STAGED=1 (A/B measurement): the staged merge (k_merge_staged) instead
-// of the mask merge + k_assemble.
-int staged_variant();
 
 enum KeyKind : uint32_t { kKeyTimestamp = 0, kKeyIdU128 = 1, kKeyCompositeU64 = 2, kKeyCompositeU128 = 3 };
 
@@ -68,7 +60,7 @@ struct JobDesc {
     Stream a, b;
     const uint64_t *addresses;
     uint32_t address_count;
-    uint32_t merge_tile; // merged positions per merge tile: kMergeTile, or staged_tile(value_size)
+    uint32_t merge_tile; // merged positions per merge tile (kMergeTile)
     uint8_t *out_blocks;
     // Batch bases (global grid indices).
     uint32_t tile_base, tile_count;      // merge tiles
@@ -147,8 +139,6 @@ struct JobResultDev {
 };
 
 constexpr uint32_t kSpecNone = 0, kSpecHeld = 1, kSpecBroken = 2;
-constexpr uint32_t kPhaseProducersOnly = 2; // timing probe (TBC_PROBE_PRODUCERS_ONLY): blocks without chains
-constexpr uint32_t kPhaseChainsAlone = 3;   // timing probe (TBC_PROBE_CHAINS_ALONE): bodies first, chains alone
 // Launch phases of a batch with speculated jobs: phase 0 runs every
 // non-speculated job (and the speculative block phase), phase 1 only the
 // speculated jobs whose speculation broke.
@@ -318,13 +308,11 @@ __device__ inline int find_job(const JobDesc *jobs, int njobs, uint32_t g, F bas
 // Kernel launchers (implemented in the .hip translation units).
 struct hipStream_t_;
 namespace tbc {
-// d_lookback (one u64 per tile, zeroed), d_ticket (4 u32, zeroed) and d_ready
-// given: the merge also writes every survivor into its output block (the
-// throughput regime's body assembly, fused; tiles take look-back offsets).
+// The mask merge of every job of a batch: merge-path splits, survivor and
+// side masks per tile, then the tile offsets and each job's output shape.
 int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_splits,
                  uint64_t *d_status, uint64_t *d_masks, uint32_t *d_block_tile, const TileRef *d_order,
                  JobResultDev *d_results, void *stream, void (*mark)(void *, const char *), void *mark_ctx,
-                 uint64_t *d_lookback = nullptr, uint32_t *d_ticket = nullptr, uint32_t *d_ready = nullptr,
                  uint32_t phase = 0);
 // Merge-path splits at the data-block boundaries of speculated jobs
 // (d_bsplits[dblock_base + k] for block k) and their results (every value
@@ -394,11 +382,11 @@ uint32_t fused_max_chain_waves();
 // d_addresses): body checksums, then the header chain in order.
 // previous_address (with no d_previous_checksum) must name a verified manifest
 // block of the grid; otherwise the new blocks' header checksums are left
-// zero (every later read fails validation) and they stay unverified. Closed
-// blocks are marked verified by the chain kernel itself.
+// zero (every later read fails validation), they are marked unverified and
+// *d_error is set. Closed blocks are marked verified by the chain kernel itself.
 int launch_manifest_close(const uint64_t *d_addresses, uint32_t count, uint8_t *grid_base, uint32_t block_size,
                           uint64_t previous_address, const uint64_t *d_previous_checksum, uint8_t *d_verified,
-                          void *stream);
+                          uint32_t *d_error, void *stream);
 // The grid's `verified` byte of every listed block set to `value` (one launch).
 int launch_grid_set_verified(const uint64_t *d_addresses, uint32_t count, uint8_t *d_verified, uint8_t value,
                              void *stream);

@@ -50,12 +50,6 @@ for v in ${VARIANTS:-d3 d1 d2 t8 t16}; do
     c5h) run c5h TBC_TAIL_TABLES=64 $B --depth 3 --config 5 --no-cpu-baseline ;;
     c1) run c1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c1h) run c1h TBC_TAIL_TABLES=64 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
-    c5s) run c5s TBC_STAGED=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
-    c1s) run c1s TBC_STAGED=1 $B --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
-    p1w2) run p1w2 TBC_UNIQUE_PER_WG=2 $B --depth 1 --pipeline on --no-cpu-baseline ;;
-    p1w4) run p1w4 TBC_UNIQUE_PER_WG=4 $B --depth 1 --pipeline on --no-cpu-baseline ;;
-    t8w2) run t8w2 TBC_UNIQUE_PER_WG=2 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
-    t8w4) run t8w4 TBC_UNIQUE_PER_WG=4 TBC_TAIL_CHAINS=8 $B --depth 3 --no-cpu-baseline ;;
     fp3) run fp3 TBC_FRONT_PRIORITY=1 $B --depth 3 --no-cpu-baseline ;;
     fp5) run fp5 TBC_FRONT_PRIORITY=1 $B --depth 3 --config 5 --no-cpu-baseline ;;
     d4p) run d4p $B --depth 4 --no-cpu-baseline ;;
