@@ -28,8 +28,26 @@ CASES = {
 }
 
 
+def _c4_split_inputs():
+    """The job bench.py splits over the ranks of config 4 at N = 2
+    (SplitPart): the largest job whose A needs no device sort — a 5-table
+    transfers.timestamp L1->L2 compaction, 168 MB — with bench's addresses."""
+    from tigerbeetle_amd import configs, workloads
+    bs = 1 << 20
+    ids = [j for j in range(2 * configs.DEFAULT_JOBS[4]) if configs.presorted(4, j)]
+    gid = max(ids, key=lambda j: configs.job_bytes(4, j))
+    js = configs.GENERATORS[4](gid)
+    assert not js.a_unsorted
+    ji = workloads.JobInputs(js.tree, js.a, js.a_immutable, list(js.b_tables), js.drop_tombstones)
+    dbcm = js.tree.layout(bs)["data_block_count_max"]
+    reservation = (len(js.b_tables) + 1) * dbcm + len(js.b_tables) + 1
+    return js.tree, bs, ji, np.arange(1, reservation + 1, dtype=np.uint64)
+
+
 def _inputs(name):
     from tigerbeetle_amd import trees, workloads
+    if name == "c4_split":
+        return _c4_split_inputs()
     tree, bs, tables, kw = CASES[name]
     spec = trees.BY_NAME[tree]
     if tables:
@@ -121,7 +139,8 @@ def _worker(name, rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("id_1mib", 2), ("debit_4k", 3), ("acct_last_level_4k", 4)])
+@pytest.mark.parametrize("name,world", [("id_1mib", 2), ("debit_4k", 3), ("acct_last_level_4k", 4),
+                                        ("c4_split", 2)])  # the job bench splits, full size
 def test_split_ranks_bit_exact(name, world):
     port = _free_port()
     ctx = mp.get_context("spawn")
@@ -129,7 +148,7 @@ def test_split_ranks_bit_exact(name, world):
     procs = [ctx.Process(target=_worker, args=(name, r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=150) for _ in range(world)]
+    out = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         if p.is_alive():

@@ -120,11 +120,11 @@ def test_gpu_manifest_refuses_to_link_an_untrusted_block():
             # an address reused after a checkpoint, verified from
             # its earlier block (6, closed above), refused again: its verified
             # byte is cleared, so a later close cannot link onto it.
-            images = manifest.pack_blocks(_infos(31, 3), [6], CLUSTER, bs, previous_address=7)
+            images = manifest.pack_blocks(_infos(20, 3), [6], CLUSTER, bs, previous_address=7)
             manifest.close_on_grid(grid, images, [6], previous_address=7, previous_checksum=None)
             with pytest.raises(abi.TbcError):
                 eng.synchronize()
-            images = manifest.pack_blocks(_infos(31, 4), [11], CLUSTER, bs, previous_address=6)
+            images = manifest.pack_blocks(_infos(20, 4), [11], CLUSTER, bs, previous_address=6)
             manifest.close_on_grid(grid, images, [11], previous_address=6, previous_checksum=None)
             with pytest.raises(abi.TbcError):  # 6 is no longer trusted: refused
                 eng.synchronize()
