@@ -382,8 +382,10 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
 
 
 # Engine marks that time a wait, not a kernel (a pipelined batch's tail
-# stream waiting for its front and for the tails before it).
-NOT_KERNELS = ("tail_wait",)
+# stream waiting for its front and for the tails before it; with the chain
+# server, the tail waiting for its batch's chains, which the server runs
+# beside other batches' — the batch's chain latency, not a launch).
+NOT_KERNELS = ("tail_wait", "chains")
 
 # bench kernel label -> rocprofv3 kernel symbol (tools/traffic.py short names)
 KERNEL_SYMBOL = {"merge_partition": "k_partition_all", "merge": "k_merge_tile", "data_blocks": "k_data_blocks",
@@ -416,13 +418,22 @@ def pmc_traffic(kernel: str, config: int = 2):
     return (k["traffic_bytes"], src) if k else (None, None)
 
 
-def pmc_step_traffic(config: int, per_step_kernel: str):
-    """PMC HBM bytes of one steady pipelined step from the committed profile
-    of this very libtbc.so and config: `per_step_kernel` is launched once per
-    such step, every other instantiation counts with its launches per step
-    (rounded). Short-name aliases of an instantiation (tools/traffic.py) are
-    skipped so nothing counts twice, and kernels launched in fewer steps than
-    `per_step_kernel` (the fused first steps of the warmup, which run no
+# The kernel each config launches a known number of times per steady step
+# (pmc_step_traffic's clock): configs 2-4 merge their speculated bodies once
+# per pipelined step, config 5's step is four pipelined job groups (one
+# k_tile_scan each), config 1's replay closes its manifest log's full block
+# once per step.
+STEP_KERNEL = {1: ("k_manifest_chain", 1), 2: ("k_merge_unique", 1), 3: ("k_merge_unique", 1),
+               4: ("k_merge_unique", 1), 5: ("k_tile_scan", 4)}
+
+
+def pmc_step_traffic(config: int, per_step_kernel: str, per_step: int = 1):
+    """PMC HBM bytes of one steady step from the committed profile of this
+    very libtbc.so and config: `per_step_kernel` is launched `per_step` times
+    per such step, every other instantiation counts with its launches per
+    step (rounded). Short-name aliases of an instantiation (tools/traffic.py)
+    are skipped so nothing counts twice, and kernels launched in fewer steps
+    than `per_step_kernel` (the fused first steps of the warmup, which run no
     k_merge_unique) are left out."""
     import glob
     import hashlib
@@ -436,7 +447,7 @@ def pmc_step_traffic(config: int, per_step_kernel: str):
         ks = d.get("kernels", {})
         if d.get("lib_md5") != md5 or d.get("baseline_config", 2) != config or per_step_kernel not in ks:
             continue
-        steps = ks[per_step_kernel].get("calls")
+        steps = ks[per_step_kernel].get("calls", 0) // max(1, per_step)
         if not steps or any("calls" not in k for k in ks.values()):
             continue
         insts = {n for n in ks if "<" in n}
@@ -729,7 +740,7 @@ def main() -> None:
         # algorithmic bytes (R + W_data) per step time, with the dominant
         # kernel's per-launch figures kept beside it.
         step_alg = R + W_data
-        st_traffic, st_src = pmc_step_traffic(args.config, "k_merge_unique")
+        st_traffic, st_src = pmc_step_traffic(args.config, *STEP_KERNEL[args.config])
         roofline = {"bound": "hbm", "basis": f"whole step ({depth} steps in flight, kernels overlap)",
                     "achieved": round(step_alg / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(step_alg / step_s / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_step": step_alg,
@@ -761,6 +772,11 @@ def main() -> None:
     if "data_blocks" in per_step:
         line["compute_roofline"] = aes_roofline(out_values, data_blocks, kt_us if dominant == "data_blocks" else
                                                 per_step["data_blocks"], "data_blocks", args.config)
+    elif "chains" in per_step:
+        # Chain server: the AES work of a step against the step's time (the
+        # chains of consecutive steps overlap, so no launch bounds them).
+        line["compute_roofline"] = dict(aes_roofline(out_values, data_blocks, step_s * 1e6, "k_chain_server",
+                                                     args.config), basis="whole step")
     if pcie:
         pcie["pcie_inclusive_MBps"] = round(wl.input_bytes / (step_s + (pcie["h2d"]["ms"] + pcie["d2h"]["ms"]) * 1e-3)
                                             / 1e6, 1)
@@ -865,11 +881,20 @@ def main_config1(args, eng, rank, world, local, dist, backend, bs) -> None:
         traffic, traffic_src = pmc_traffic(dominant, 1)
         if "data_blocks" in per_step:
             line["compute_roofline"] = aes_roofline(out_values, data_blocks, per_step["data_blocks"], "data_blocks", 1)
-        line["roofline"] = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                            "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_step": a_bytes,
-                            "note": "the kernel's time summed over the replay's batches (hipEvents on the "
-                                    "engine stream); its AEGIS chains bound it, not HBM (DESIGN.md §4)"}
+        elif "chains" in per_step:
+            line["compute_roofline"] = dict(aes_roofline(out_values, data_blocks, step_s * 1e6, "k_chain_server", 1),
+                                            basis="whole step")
+        dominant_line = {"bound": "hbm", "kernel": dominant, "basis": "summed over the replay's batches (hipEvents "
+                         "on the engine stream)", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "alg_bytes_per_step": a_bytes}
+        # Whole step (the replay's batches overlap): R + W of every compaction
+        # (+ the bar-end sorts' S) per step time, with the PMC bytes of a step.
+        st_traffic, st_src = pmc_step_traffic(1, *STEP_KERNEL[1])
+        line["roofline"] = {"bound": "hbm", "basis": "whole step (every sort and batch of the replay)",
+                            "achieved": round(job_bytes / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(job_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_step": job_bytes,
+                            "traffic": st_traffic, "traffic_source": st_src, "dominant_kernel": dominant_line}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_config1()
     if rank == 0:

@@ -1,9 +1,21 @@
-"""The engine's opt-in paths, measured slower and off by default (DESIGN.md
-§3), stay bit-exact: the bar-end sort on its own stream (TBC_SORT_STREAM=1:
-pending-sort waits) and tails at the highest stream priority
-(TBC_TAIL_PRIORITY=1). The library reads these once per process, so one
-child process runs the tests that exercise those paths with both set; each
-of those tests compares with the oracle."""
+"""Every environment knob libtbc.so still reads leaves
+the output bytes oracle-exact. The library reads them once per process, so
+each setting runs, in a child process, GPU tests that exercise the paths it
+changes; each of those tests compares with the oracle.
+
+  TBC_SORT_STREAM=1, TBC_TAIL_PRIORITY=1   bar-end sorts on their own stream
+                                           (pending-sort waits), tails at the
+                                           highest stream priority
+  TBC_GRID_SPECULATION=1                   grid batches merge UNIQUE_KEYS jobs
+                                           tile by tile, recompute in front
+  TBC_CHAIN_SERVER=0, TBC_TAILS=2,         one chain kernel per batch tail (the
+  TBC_DEBUG_SYNC=1                         round-4 path); stage-by-stage waits
+  TBC_SERVER_WGS=64, TBC_SERVER_WAVES=4,   a small chain server whose idle
+  TBC_CHAIN_LINGER_US=0, TBC_GROUPS=2      waves leave at once; two job groups
+                                           in the throughput regime
+
+GPU_MAX_HW_QUEUES is HIP's own (the engine sizes its tails from it).
+"""
 import os
 import subprocess
 import sys
@@ -12,26 +24,35 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-SELECT = " or ".join([
-    "test_compaction_parity_throughput_regime",      # throughput regime: 4 pipelined groups
-    "test_immutable_compaction_after_device_sort",   # sort stream, then a batch that waits on it
+# Pipelined, grid and throughput-regime batches, sorts, overlapping tails.
+PIPELINED = " or ".join([
+    "test_compaction_parity_throughput_regime",      # throughput regime: pipelined job groups
+    "test_immutable_compaction_after_device_sort",   # a batch after a device sort
     "test_sort_values_batch_of_memtables",
     "test_two_half_bars_chained_through_the_grid",   # grid batches
     "test_pipelined_grid_batches_in_flight",
     "test_values_only_bodies_equal_full_compaction",  # VALUES_ONLY bodies
+    "test_speculated_batches_pipelined_three_in_flight",
+    "test_back_to_back_batches_share_outputs",
 ])
+FILES = ("test_gpu_parity.py", "test_gpu_grid.py", "test_gpu_engine.py", "test_gpu_split.py", "test_gpu_overlap.py")
 
 
-@pytest.mark.gpu
-def test_opt_in_paths_bit_exact():
-    env = dict(os.environ, TBC_SORT_STREAM="1", TBC_TAIL_PRIORITY="1")
-    files = [os.path.join(HERE, f) for f in ("test_gpu_parity.py", "test_gpu_grid.py", "test_gpu_engine.py",
-                                              "test_gpu_split.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", "-k", SELECT,
-                        *files], env=env, capture_output=True, text=True, timeout=200)
+def _child(env_extra: dict, files, select=None, timeout=240):
+    env = dict(os.environ, **env_extra)
+    args = [sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider"]
+    if select:
+        args += ["-k", select]
+    r = subprocess.run(args + [os.path.join(HERE, f) for f in files], env=env, capture_output=True, text=True,
+                       timeout=timeout)
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout, tail
+
+
+@pytest.mark.gpu
+def test_sort_stream_and_tail_priority_bit_exact():
+    _child({"TBC_SORT_STREAM": "1", "TBC_TAIL_PRIORITY": "1"}, FILES, PIPELINED)
 
 
 @pytest.mark.gpu
@@ -39,10 +60,15 @@ def test_grid_speculation_bit_exact():
     """TBC_GRID_SPECULATION=1: grid batches merge their UNIQUE_KEYS jobs tile
     by tile (k_merge_unique), broken speculations recomputed in the front —
     the grid tests and the 11-bar config-1 lockstep against the oracle."""
-    env = dict(os.environ, TBC_GRID_SPECULATION="1")
-    files = [os.path.join(HERE, f) for f in ("test_gpu_grid.py", "test_gpu_config1.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", *files],
-                       env=env, capture_output=True, text=True, timeout=230)
-    tail = (r.stdout + r.stderr)[-3000:]
-    assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " failed" not in r.stdout, tail
+    _child({"TBC_GRID_SPECULATION": "1"}, ("test_gpu_grid.py", "test_gpu_config1.py"), timeout=300)
+
+
+@pytest.mark.gpu
+def test_per_batch_tails_bit_exact():
+    _child({"TBC_CHAIN_SERVER": "0", "TBC_TAILS": "2", "TBC_DEBUG_SYNC": "1"}, FILES, PIPELINED)
+
+
+@pytest.mark.gpu
+def test_small_chain_server_bit_exact():
+    _child({"TBC_SERVER_WGS": "64", "TBC_SERVER_WAVES": "4", "TBC_CHAIN_LINGER_US": "0", "TBC_GROUPS": "2"}, FILES,
+           PIPELINED)

@@ -327,6 +327,44 @@ struct StepValuKey {
     }
 };
 
+// Compact T-tables (the chain server, round 5): T0 and T2 only, each
+// replicated once per bank as the full layout is, in 64 KiB — entry T0[b]
+// for lane bank k at b * 256 + k * 4, T2[b] at b * 256 + 128 + k * 4 — and
+// T1 = rotl(T0, 8), T3 = rotl(T2, 8) (AES: T_r[x] = rotl(T0[x], 8r)). Two
+// v_alignbit_b32 per column step buy back 64 KiB of each chain CU's LDS, so
+// a front's workgroups (16-52 KiB: merges, sorts) fit beside the server's.
+constexpr uint32_t kCompactTableBytes = 65536;
+constexpr uint32_t kCompactTableDwords = kCompactTableBytes / 4;
+
+__device__ __forceinline__ void load_tables_compact(uint32_t *sT) {
+    for (uint32_t i = threadIdx.x; i < kCompactTableDwords; i += blockDim.x) {
+        const uint32_t b = i >> 6, half = (i >> 5) & 1;
+        sT[i] = c_aes.t[half ? 2 : 0][b];
+    }
+}
+
+__device__ __forceinline__ uint32_t rotl8(uint32_t v) { return __builtin_amdgcn_alignbit(v, v, 24); }
+
+struct StepCompact {
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &tb, uint32_t key_src,
+                                                    uint32_t x, uint32_t m) {
+        const uint32_t key = bpermute(key_src, x);
+        const uint32_t a0 = __builtin_amdgcn_perm(x, tb.lo, 0x03020400u);
+        const uint32_t a1 = __builtin_amdgcn_perm(x, tb.lo, 0x03020500u);
+        const uint32_t a2 = __builtin_amdgcn_perm(x, tb.lo, 0x03020600u);
+        const uint32_t a3 = __builtin_amdgcn_perm(x, tb.lo, 0x03020700u);
+        const uint32_t t0 = lds_u32(sT, a0);
+        const uint32_t t1 = rotl8(lds_u32(sT, a1));
+        const uint32_t t2 = lds_u32(sT, a2 + 128);
+        const uint32_t t3 = rotl8(lds_u32(sT, a3 + 128));
+        uint32_t r = (key ^ m) ^ t0;
+        r ^= quad_perm<1, 2, 3, 0>(t1);
+        r ^= quad_perm<2, 3, 0, 1>(t2);
+        r ^= quad_perm<3, 0, 1, 2>(t3);
+        return r;
+    }
+};
+
 // A step with `kMaskedMsg` takes the message word and its lane masks (the
 // lanes whose block absorbs it this step) instead of the selected word
 // (tools/aegis_lab.hip: hand-scheduled variants, measured no faster alone).
@@ -722,6 +760,7 @@ __device__ __forceinline__ uint32_t header_dword(const HeaderFields &h, uint32_t
 
 // Fill a 256-byte header in LDS (hdr: 64 dwords), checksum [16, 256), and
 // return the header checksum column in every lane.
+template <class Step = StepValuKey>
 __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *hdr, const HeaderFields &h,
                                                   uint32_t body_tag) {
     const uint32_t lane = threadIdx.x & 63, g = lane & 31;
@@ -731,7 +770,7 @@ __device__ __forceinline__ uint32_t finish_header(const uint32_t *sT, uint32_t *
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     LdsMsg m(hdr + 4, kHeaderSize - 16);
-    uint32_t tag = aegis_mac32(sT, m);
+    uint32_t tag = aegis_mac32<LdsMsg, Step>(sT, m);
     return tag;
 }
 
@@ -882,9 +921,19 @@ __device__ __forceinline__ void produce_body(const JobDesc &j, uint32_t k, uint3
     }
 }
 
+// A 4-byte store; write-through (sc1: the line leaves this XCD's L2 at once)
+// when WT, so another CU that acquires after a later signal of this wave
+// sees it without a release fence (MI355X_MICROARCH.md, inter-workgroup
+// visibility). The chain server's outputs are stored this way.
+template <bool WT> __device__ __forceinline__ void st32(void *p, uint32_t v) {
+    if constexpr (WT) __hip_atomic_store((uint32_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else gst<uint32_t>(p, v);
+}
+
 // Data block k of job j, body checksummed (`body_tag`: column lane & 3 of
 // the tag, per 32-lane group): header fields, header checksum, the header
 // and the zeroed sector tail stored by the `writer` group.
+template <bool WT = false, class Step = StepValuKey>
 __device__ __forceinline__ void finish_data_block(const uint32_t *sT, uint32_t *hdr, const JobDesc &j, uint32_t k,
                                                   uint32_t cnt, uint32_t body_tag, bool writer) {
     const uint32_t slot = data_block_slot(k, j.dbcm);
@@ -901,17 +950,17 @@ __device__ __forceinline__ void finish_data_block(const uint32_t *sT, uint32_t *
     h.meta2 = j.value_size; // .value_size
     h.meta3 = j.tree_id;    // .tree_id (u16), reserved = 0
     h.block_type = 5;       // BlockType.data (schema.zig:65)
-    const uint32_t hdr_tag = finish_header(sT, hdr, h, body_tag);
+    const uint32_t hdr_tag = finish_header<Step>(sT, hdr, h, body_tag);
     const uint32_t g = threadIdx.x & 31;
     if (g < 4) hdr[g] = hdr_tag;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (writer) {
-        gst<uint32_t>(blk + 4 * g, hdr[g]);
-        gst<uint32_t>(blk + 4 * (g + 32), hdr[g + 32]);
+        st32<WT>(blk + 4 * g, hdr[g]);
+        st32<WT>(blk + 4 * (g + 32), hdr[g + 32]);
         // Zero [size, sector_ceil(size)) (grid.zig:686).
         const uint32_t end = (uint32_t)sector_ceil(size);
-        for (uint32_t o = size + 4 * g; o < end; o += 128) gst<uint32_t>(blk + o, 0u);
+        for (uint32_t o = size + 4 * g; o < end; o += 128) st32<WT>(blk + o, 0u);
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -1527,7 +1576,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         // k_assemble ran before this kernel (stream order): every survivor of
         // the block must have landed.
         // (A speculated job whose speculation held was merged by
-        // k_produce_unique, before this kernel in stream order: no counts.)
+        // k_merge_unique, before this kernel in stream order: no counts.)
         // (Seal jobs: the caller placed the bodies, tbc_compaction_seal.)
         const bool produced = (j.unique && res[j.job_index].spec != kSpecBroken) || j.seal;
         if (!produced &&
@@ -1557,50 +1606,6 @@ __global__ __launch_bounds__(3 * 64 * kMaxChainWaves) void k_data_blocks_redo(
     const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
     const uint32_t *ready) {
     data_blocks<true>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready, nullptr, 1u);
-}
-
-// Pipelined speculated batches (engine.hip submit_impl, round 4): the bodies
-// of every speculated job's data blocks, one producer wave per block
-// (produce_unique: the block merges its own positions, speculation checks
-// included), on the engine stream with no chain beside it and no throttle;
-// the chains run later on a tail stream (k_data_blocks<false>), so chains of
-// consecutive batches share the chip while the next batch's bodies are
-// merged. A workgroup is kProduceWaves producers with their LDS staging
-// only (no T-tables), so it fits beside the chain workgroups of running tails.
-constexpr uint32_t kProduceWaves = 4;
-
-__global__ __launch_bounds__(64 * kProduceWaves) void k_produce_unique(const JobDesc *jobs, int njobs, uint32_t total,
-                                                                       const JobResultDev *res,
-                                                                       const SplitDesc *bsplits) {
-    __shared__ uint64_t sStage[kProduceWaves][kStageWords];
-    __shared__ uint32_t sProg[kProduceWaves];
-    const uint32_t w = threadIdx.x >> 6;
-    const uint32_t m = blockIdx.x * kProduceWaves + w;
-    if (m >= total) return; // wave-uniform (producers use wave-level barriers only)
-    const int ji = find_job(jobs, njobs, m, [](const JobDesc &d) { return d.dblock_base; });
-    const JobDesc &j = jobs[ji];
-    const uint32_t k = m - j.dblock_base;
-    if (!j.unique || k >= res[j.job_index].data_block_count) return;
-    const uint64_t n_out = res[j.job_index].value_count, first = (uint64_t)k * j.vcm;
-    const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
-    uint8_t *body = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize;
-    const SplitDesc sp = bsplits[j.dblock_base + k];
-    uint32_t *err = const_cast<uint32_t *>(&res[j.job_index].invariant);
-    uint32_t *spec = const_cast<uint32_t *>(&res[j.job_index].spec);
-    switch (j.key_kind) {
-    case kKeyTimestamp:
-        produce_unique_vs<kKeyTimestamp>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
-        break;
-    case kKeyIdU128:
-        produce_unique_vs<kKeyIdU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
-        break;
-    case kKeyCompositeU64:
-        produce_unique_vs<kKeyCompositeU64>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
-        break;
-    default:
-        produce_unique_vs<kKeyCompositeU128>(j, k, cnt, sp, body, &sProg[w], err, spec, sStage[w], nullptr);
-        break;
-    }
 }
 
 // Throughput regime, pass 1: assemble every data block body from the merge's
@@ -1851,6 +1856,344 @@ __global__ __launch_bounds__(256) void k_index_layout(const JobDesc *jobs, int n
     gst<uint64_t>(idx + j.idx_addresses_off + 8 * (k - t * j.dbcm), gld<uint64_t>(j.addresses + data_block_slot(k, j.dbcm)));
 }
 
+// --------------------------------------------------------------------------
+// Chain server (round 5).
+//
+// A batch's AEGIS chains used to be one kernel launch on one of three tail
+// streams: at most three batches' chains ran at once (one per hardware queue
+// beside the engine stream), and a small batch held a few dozen CUs for a
+// whole chain time (~2 ms per 1 MiB block) while the rest of the chip idled
+// (config 1: 58 such launches per step). Here every batch's data blocks are
+// tasks in ONE device ring (tbc_internal.h ChainRing): the batch's front
+// publishes them (k_chain_publish, engine stream, after its bodies are in
+// place) and the server's chain waves take them two at a time (one per
+// 32-lane group) whatever batch they belong to, so the number of chains in
+// flight is set by the server's workgroups, not by the hardware queues.
+//
+// A server instance is an ordinary launch on the chain stream: its waves
+// take tasks while there are any and leave after the ring has stayed empty
+// for `linger`; the front of every batch also queues an instance behind it
+// (stream order after the publish), so a task published after the last
+// wave of a running instance has left is always taken by a later one. The
+// instance never waits on anything but the ring, so it always ends.
+//
+// Per task (data block k of job j): the body's AEGIS-128L chain and the
+// header (data_block_finish, table.zig:306-384), then the block's index
+// entry — header checksum, key_min, key_max, address (TableIndex,
+// schema.zig:80-260) — straight into its table's index block image; the
+// table's counter counts the block, and the wave that counts its table's
+// last block seals the index block (index_block_finish, table.zig:403-457:
+// unused entries zeroed, body and header checksums, header) and writes the
+// TableInfo (schema.zig:489-509). No T-table workgroup of its own waits for
+// a free CU (k_index_blocks held 148 KiB of LDS for ~2 MB of work per
+// batch). Every output is stored write-through (sc1), and a task counts in
+// its batch's `done` only after its stores have completed (s_waitcnt), so a
+// kernel that runs after k_chain_wait sees them, as does the sealer after an
+// agent-scope acquire (MI355X_MICROARCH.md: sc1 payload -> vmcnt(0) ->
+// agent atomic; consumer acquire -> plain loads).
+// --------------------------------------------------------------------------
+constexpr uint32_t kServerWavesMax = 16;
+
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Claim word fields (tbc_internal.h ChainRing.claim).
+__device__ __forceinline__ uint32_t claim_seq(unsigned long long w) { return (uint32_t)(w >> 40); }
+__device__ __forceinline__ uint32_t claim_tasks(unsigned long long w) { return (uint32_t)(w >> 20) & 0xFFFFFu; }
+__device__ __forceinline__ uint32_t claim_taken(unsigned long long w) { return (uint32_t)w & 0xFFFFFu; }
+
+// Batch `seq`: its descriptor, then (released) its claim word, then the
+// count of published batches.
+__global__ __launch_bounds__(64) void k_chain_publish(ChainRing r, ChainBatch cb, unsigned long long seq) {
+    if (threadIdx.x != 0) return;
+    const uint32_t slot = (uint32_t)(seq % kChainSlots);
+    r.batches[slot] = cb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(r.claim + slot, (seq & 0xFFFFFFull) << 40 | (unsigned long long)cb.ntasks << 20,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(r.pub, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A chain task (batch slot, block m of the batch) resolved to its job.
+struct ChainTask {
+    const ChainBatch *cb;
+    const JobDesc *j;
+    uint32_t m; // block of the batch (dblock_base numbering)
+    uint32_t k; // the job's data block
+    __device__ __forceinline__ void resolve(const ChainRing &r, uint32_t slot, uint32_t m_) {
+        cb = r.batches + slot;
+        m = m_;
+        const JobDesc *jobs = cb->jobs;
+        const int ji = find_job(jobs, cb->njobs, m, [](const JobDesc &d) { return d.dblock_base; });
+        j = jobs + ji;
+        k = m - j->dblock_base + j->block_lo;
+    }
+};
+
+// Seal table t of job j (its blocks' entries are in the image): zero the
+// unused entries, checksum the index body and the header, store the header,
+// the sector tail and the TableInfo. Both 32-lane groups run it (a group
+// with nothing to seal mirrors its partner's table with writer = false).
+template <class Step>
+__device__ __forceinline__ void seal_table(const uint32_t *sT, uint32_t *hdr, const JobDesc &j, const JobResultDev &res,
+                                           uint8_t *infos, uint32_t t, bool writer) {
+    const uint32_t g = threadIdx.x & 31;
+    const uint32_t db = res.data_block_count, dbcm = j.dbcm, ks = j.key_size;
+    const uint32_t k0 = t * dbcm, nblk = (db - k0) < dbcm ? (db - k0) : dbcm, k_last = k0 + nblk - 1;
+    const uint32_t index_slot = index_block_slot(t, k_last);
+    uint8_t *idx = block_ptr(j, index_slot);
+    if (writer && nblk < dbcm) { // the last table of the job: unused entries are zero
+        const uint32_t spans[4][2] = {{j.idx_checksums_off, 32}, {j.idx_keys_min_off, ks}, {j.idx_keys_max_off, ks},
+                                      {j.idx_addresses_off, 8}};
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+            for (uint32_t o = spans[a][0] + nblk * spans[a][1] + 4 * g; o < spans[a][0] + dbcm * spans[a][1]; o += 128)
+                st32<true>(idx + o, 0u);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // our own write-through zeros, read back below
+    GlobalMsg body(idx + kHeaderSize, j.index_size - kHeaderSize);
+    const uint32_t body_tag = aegis_mac32<GlobalMsg, Step>(sT, body);
+    HeaderFields h;
+    h.cluster_lo = j.cluster_lo;
+    h.cluster_hi = j.cluster_hi;
+    h.address = gld<uint64_t>(j.addresses + index_slot);
+    h.snapshot = j.snapshot_min;
+    h.size = j.index_size;
+    h.meta0 = nblk;      // TableIndex.Metadata.data_block_count
+    h.meta1 = dbcm;      // .data_block_count_max
+    h.meta2 = ks;        // .key_size
+    h.meta3 = j.tree_id; // .tree_id
+    h.block_type = 4;    // BlockType.index (schema.zig:64)
+    const uint32_t hdr_tag = finish_header<Step>(sT, hdr, h, body_tag);
+    if (g < 4) hdr[g] = hdr_tag;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (!writer) return;
+    st32<true>(idx + 4 * g, hdr[g]);
+    st32<true>(idx + 4 * (g + 32), hdr[g + 32]);
+    const uint32_t end = (uint32_t)sector_ceil(j.index_size);
+    for (uint32_t o = j.index_size + 4 * g; o < end; o += 128) st32<true>(idx + o, 0u);
+    // ManifestNode.TableInfo (schema.zig:489-509): key_min of the first entry,
+    // key_max of the last, the index block's checksum and address.
+    const uint64_t n_out = res.value_count;
+    const uint64_t vcount = (n_out - (uint64_t)k0 * j.vcm) < (uint64_t)nblk * j.vcm ? (n_out - (uint64_t)k0 * j.vcm)
+                                                                                   : (uint64_t)nblk * j.vcm;
+    uint32_t v = 0;
+    if (g < 8) v = 4 * g < ks ? gld<uint32_t>(idx + j.idx_keys_min_off + 4 * g) : 0u;
+    else if (g < 16) v = 4 * (g - 8) < ks ? gld<uint32_t>(idx + j.idx_keys_max_off + ks * (nblk - 1) + 4 * (g - 8)) : 0u;
+    else if (g < 20) v = hdr[g - 16];
+    else if (g == 24) v = (uint32_t)h.address;
+    else if (g == 25) v = (uint32_t)(h.address >> 32);
+    else if (g == 26) v = (uint32_t)j.snapshot_min;
+    else if (g == 27) v = (uint32_t)(j.snapshot_min >> 32);
+    else if (g == 28 || g == 29) v = 0xffffffffu; // snapshot_max = maxInt(u64)
+    else if (g == 30) v = (uint32_t)vcount;
+    else if (g == 31) v = (uint32_t)j.tree_id | ((uint32_t)((j.level_b & 0x3f) | (1u << 6)) << 16);
+    st32<true>(infos + (size_t)(j.info_base + t - j.table_lo) * kTableInfoSize + 4 * g, v);
+}
+
+// Whether batch q (< pub) still has unclaimed tasks; *stale: its slot has
+// been reused (q is long claimed).
+__device__ __forceinline__ bool claimable(const ChainRing &r, unsigned long long q, bool *stale) {
+    const unsigned long long w = ld_sc1(r.claim + q % kChainSlots);
+    *stale = claim_seq(w) != (uint32_t)(q & 0xFFFFFFu);
+    return !*stale && claim_taken(w) < claim_tasks(w);
+}
+
+template <class Step>
+__global__ __launch_bounds__(64 * kServerWavesMax) void k_chain_server(ChainRing r, unsigned long long first_seq) {
+    __shared__ uint32_t sT[kCompactTableDwords];
+    __shared__ uint32_t sHdr[kServerWavesMax][2][64];
+    __shared__ uint32_t s_go;
+    const uint32_t lane = threadIdx.x & 63, g = lane & 31;
+    const bool upper = lane >= 32;
+    // Every batch before first_seq was claimed before this instance started
+    // (the instance before it left only when nothing was claimable): one
+    // queued behind an instance that took everything leaves at once.
+    if (threadIdx.x == 0) {
+        bool any = false, stale;
+        const unsigned long long p = ld_sc1(r.pub);
+        for (unsigned long long q = first_seq; q < p && !any; q++) any = claimable(r, q, &stale);
+        s_go = any ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_go) return;
+    load_tables_compact(sT);
+    __syncthreads(); // the last workgroup barrier: from here on every wave runs on its own
+    uint32_t *hdr = sHdr[threadIdx.x >> 6][upper ? 1 : 0];
+    unsigned long long cur = first_seq; // (lane 0) every batch before it is claimed
+    for (;;) {
+        // Claim up to two tasks (lane 0): one fetch_add of 2 on the claim
+        // word of the oldest batch with unclaimed tasks; leave once nothing
+        // has been claimable for the linger time (idle polls back off to
+        // ~27 us).
+        uint32_t slot = 0, t0 = 0, got = 0;
+        if (lane == 0) {
+            const uint64_t since = wall_clock64();
+            uint32_t backoff = 1;
+            for (;;) {
+                // The instance leaves as a whole: once one wave has decided to,
+                // no wave claims again (what is published from then on is the
+                // next instance's, with every wave).
+                if (ld_sc1(r.closing) == first_seq + 1) break;
+                const unsigned long long p = ld_sc1(r.pub);
+                for (unsigned long long q = cur; q < p && !got; q++) {
+                    bool stale;
+                    if (!claimable(r, q, &stale)) {
+                        if (q == cur) cur++;
+                        continue;
+                    }
+                    const unsigned long long w = __hip_atomic_fetch_add(r.claim + q % kChainSlots, 2ull,
+                                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // (If the slot has just been reused, these are the new batch's tasks.)
+                    const uint32_t n = claim_tasks(w), c = claim_taken(w);
+                    if (c < n) {
+                        slot = (uint32_t)(q % kChainSlots);
+                        t0 = c;
+                        got = n - c < 2 ? n - c : 2;
+                    }
+                }
+                if (got) {
+                    __hip_atomic_fetch_add(r.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                // An idle wave stays while any wave of the instance holds a
+                // task, and the instance leaves as a whole once none has
+                // held one for the linger time: a task published meanwhile
+                // finds every wave of this instance, or of the next one (a
+                // later instance waits behind this one on the chain stream).
+                if (wall_clock64() - since > r.linger &&
+                    __hip_atomic_load(r.active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                    __hip_atomic_store(r.closing, first_seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                for (uint32_t i = 0; i < backoff; i++) __builtin_amdgcn_s_sleep(63);
+                backoff = backoff < 16 ? 2 * backoff : 16;
+            }
+        }
+        got = __builtin_amdgcn_readfirstlane(got);
+        if (!got) return;
+        slot = __builtin_amdgcn_readfirstlane(slot);
+        t0 = __builtin_amdgcn_readfirstlane(t0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // the batch's descriptor, results, bodies
+        // This group's task (a group beyond `got` shares task 0 and owns nothing).
+        const bool own = !upper || got == 2;
+        const uint32_t my_slot = slot, my_m = t0 + (upper && got == 2 ? 1u : 0u);
+        // The other group's task.
+        const uint32_t slot_p = slot, m_p = t0 + (!upper && got == 2 ? 1u : 0u);
+        ChainTask task;
+        task.resolve(r, my_slot, my_m);
+        unsigned long long *own_done = task.cb->done;
+        const bool live = own && task.k < task.cb->res[task.j->job_index].data_block_count;
+        const bool live_lo = __builtin_amdgcn_readlane((int)live, 0) != 0;
+        const bool live_hi = __builtin_amdgcn_readlane((int)live, 32) != 0;
+        if (live_lo || live_hi) {
+            // A group with no live block mirrors its partner's, writing nothing.
+            if (!live) task.resolve(r, slot_p, m_p);
+            const bool writer = live;
+            const JobDesc &j = *task.j;
+            JobResultDev &res = task.cb->res[j.job_index];
+            const uint32_t k = task.k;
+            const uint64_t n_out = res.value_count, first = (uint64_t)k * j.vcm;
+            const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
+            uint8_t *blk = block_ptr(j, data_block_slot(k, j.dbcm));
+            const uint32_t *ready = task.cb->ready;
+            const bool produced = (j.unique && res.spec != kSpecBroken) || j.seal || !ready;
+            if (writer && g == 0 && !produced &&
+                __hip_atomic_load(ready + task.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
+                st32<true>(&res.invariant, 0xdeafu);
+            GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
+            const uint32_t body_tag = aegis_mac32<GlobalMsg, Step>(sT, body);
+            finish_data_block<true, Step>(sT, hdr, j, k, cnt, body_tag, writer);
+            // Its index entry, into the table's index block image.
+            const uint32_t db = res.data_block_count, tb = k / j.dbcm, s = k - tb * j.dbcm;
+            const uint32_t k_last = ((tb + 1) * j.dbcm < db ? (tb + 1) * j.dbcm : db) - 1;
+            const uint32_t ks = j.key_size;
+            if (writer) {
+                uint8_t *image = block_ptr(j, index_block_slot(tb, k_last));
+                uint64_t kmin[4], kmax[4];
+                value_key(j, blk + kHeaderSize, kmin);
+                value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
+                if (g < 8) st32<true>(image + j.idx_checksums_off + 32 * s + 4 * g, g < 4 ? hdr[g] : 0u);
+                if (4 * g < ks) {
+                    st32<true>(image + j.idx_keys_min_off + ks * s + 4 * g, (uint32_t)(kmin[g >> 1] >> (32 * (g & 1))));
+                    st32<true>(image + j.idx_keys_max_off + ks * s + 4 * g, (uint32_t)(kmax[g >> 1] >> (32 * (g & 1))));
+                }
+                if (g < 2) {
+                    const uint64_t a = gld<uint64_t>(j.addresses + data_block_slot(k, j.dbcm));
+                    st32<true>(image + j.idx_addresses_off + 8 * s + 4 * g, (uint32_t)(a >> (32 * g)));
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // Count the block in its table; the group that counts the last one seals it.
+            uint32_t seal = 0;
+            if (writer && g == 0) {
+                const uint32_t nblk = k_last - tb * j.dbcm + 1;
+                const uint32_t old = __hip_atomic_fetch_add(task.cb->table_cnt + j.table_base + tb - j.table_lo, 1u,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                seal = old + 1 == nblk ? 1u : 0u;
+            }
+            const bool seal_lo = __builtin_amdgcn_readlane((int)seal, 0) != 0;
+            const bool seal_hi = __builtin_amdgcn_readlane((int)seal, 32) != 0;
+            if (seal_lo || seal_hi) {
+                // A sealing group's task is its own; the other group mirrors it.
+                const bool mine = upper ? seal_hi : seal_lo;
+                ChainTask st;
+                if (mine) st.resolve(r, my_slot, my_m);
+                else st.resolve(r, slot_p, m_p);
+                const JobDesc &sj = *st.j;
+                seal_table<Step>(sT, hdr, sj, st.cb->res[sj.job_index], st.cb->infos, st.k / sj.dbcm, mine);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (own && g == 0)
+            __hip_atomic_fetch_add(own_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_fetch_add(r.active, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// A batch's tail waits here (one lane) until every task of the batch has
+// counted; bounded (~15 s): then every job of the batch carries an
+// invariant error instead of the tail hanging.
+__global__ __launch_bounds__(64) void k_chain_wait(const unsigned long long *done, uint32_t target,
+                                                   JobResultDev *res, uint32_t njobs) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t spins = 0;; spins++) {
+        if (ld_sc1(done) >= target) return;
+        if (spins > (1u << 22)) break;
+        __builtin_amdgcn_s_sleep(127);
+    }
+    for (uint32_t i = 0; i < njobs; i++) st32<true>(&res[i].invariant, 0x7a17u);
+}
+
+int launch_chain_publish(const ChainRing &r, const ChainBatch &cb, unsigned long long seq, void *stream) {
+    hipLaunchKernelGGL(k_chain_publish, dim3(1), dim3(64), 0, (hipStream_t)stream, r, cb, seq);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Chain waves per workgroup: one workgroup per CU (the tables take 128 KiB
+// of LDS); two or more chain waves per SIMD take the round key by
+// ds_bpermute, one alone by VALU lane moves.
+int launch_chain_server(const ChainRing &r, unsigned long long first_seq, uint32_t wgs, uint32_t waves,
+                        void *stream) {
+    waves = waves < 1 ? 1 : (waves > kServerWavesMax ? kServerWavesMax : waves);
+    hipLaunchKernelGGL(k_chain_server<StepCompact>, dim3(wgs), dim3(64 * waves), 0, (hipStream_t)stream, r,
+                       first_seq);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_chain_wait(const unsigned long long *done, uint32_t target, JobResultDev *d_results, uint32_t njobs,
+                      void *stream) {
+    if (!target) return 0;
+    hipLaunchKernelGGL(k_chain_wait, dim3(1), dim3(64), 0, (hipStream_t)stream, done, target, d_results, njobs);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // One workgroup per CU (the tables take 128 KiB of LDS): spread the waves
 // over all 256 CUs, at most 16 waves per workgroup.
 static uint32_t waves_per_block(uint32_t waves) {
@@ -1898,11 +2241,7 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-uint32_t fused_max_chain_waves() {
-    static const uint32_t v = getenv("TBC_FUSED_MAX_WAVES") ? (uint32_t)atoi(getenv("TBC_FUSED_MAX_WAVES"))
-                                                            : kFusedMaxChainWaves; // A/B measurement only
-    return v;
-}
+uint32_t fused_max_chain_waves() { return kFusedMaxChainWaves; }
 
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
@@ -1982,15 +2321,6 @@ int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables,
     if (!total_tables) return 0;
     hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, (hipStream_t)stream, d_jobs, njobs,
                        d_results, d_infos);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_produce_unique(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, const JobResultDev *d_results,
-                          const SplitDesc *d_bsplits, void *stream) {
-    if (!total_dblocks) return 0;
-    hipLaunchKernelGGL(k_produce_unique, dim3((total_dblocks + kProduceWaves - 1) / kProduceWaves),
-                       dim3(64 * kProduceWaves), 0, (hipStream_t)stream, d_jobs, njobs, total_dblocks, d_results,
-                       d_bsplits);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2103,16 +2433,12 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
             // so that two consecutive batches' tails fill the chip (config 2:
             // 8 vs 12 waves, 1.98–2.02 vs 2.01–2.05 ms per step over three
             // calls, gpurun_out/r04).
-            // TBC_TAIL_CHAINS (A/B measurement): chain waves per workgroup.
-            static const uint32_t forced = getenv("TBC_TAIL_CHAINS") ? (uint32_t)atoi(getenv("TBC_TAIL_CHAINS")) : 0u;
             uint32_t c = waves > 512 ? 8u : 4u;
-            if (forced) c = forced < 1 ? 1 : (forced > 16 ? 16 : forced);
             if (c > waves) c = waves;
             // Two or more chains per SIMD share its VALU issue: the round key by
             // one ds_bpermute (LDS pipe) instead of six VALU lane moves, as the
-            // throughput regime does. TBC_TAIL_STEP=valu|bperm (A/B only).
-            static const char *step_env = getenv("TBC_TAIL_STEP");
-            const bool bperm = step_env ? step_env[0] == 'b' : c >= 8;
+            // throughput regime does.
+            const bool bperm = c >= 8;
             if (bperm)
                 hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
                                    d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,

@@ -166,6 +166,27 @@ struct tbc_engine {
     // ran them (a manifest close that refused to link): one word, read and
     // cleared by tbc_synchronize.
     uint32_t *d_error = nullptr;
+    // Chain server (aegis.hip k_chain_server, round 5): pipelined and grid
+    // batches publish their data blocks (ChainRing: a descriptor and a claim
+    // word per batch) and a server instance on the chain stream (a hardware
+    // queue of its own) takes them, whatever batch they belong to; a batch's
+    // tail waits for its count. TBC_CHAIN_SERVER=0 (A/B measurement) restores
+    // one chain kernel per batch tail. Host side: the batches published so
+    // far and the descriptor slots of those in flight (oldest first).
+    bool server = false;
+    hipStream_t chain_stream = nullptr;
+    ChainRing ring{};
+    uint8_t *ring_mem = nullptr;
+    unsigned long long published = 0; // batches published (the next batch's sequence number)
+    hipEvent_t slot_ev[kChainSlots] = {};
+    std::vector<uint32_t> slot_fifo; // descriptor slots of batches in flight, oldest first
+    // Server geometry per batch: a batch whose front fits beside a chain
+    // workgroup on every CU (k_merge_unique: 16.4 KiB of LDS; the
+    // timestamp-key mask merge: 18.9 KiB) gets one workgroup of 8 chain
+    // waves per CU; others (grid batches, composite-key mask merges, the
+    // bar-end sorts: 35-52 KiB of LDS) leave half the CUs whole: 128
+    // workgroups of 16. TBC_SERVER_WGS / TBC_SERVER_WAVES (A/B) set both.
+    uint32_t wide_wgs = 256, wide_waves = 8, narrow_wgs = 128, narrow_waves = 16;
     Arena dev, host;
     Staging staging;
     // Host ranges the caller registered (tbc_host_register: hipHostRegister):
@@ -392,6 +413,8 @@ struct tbc_batch {
     bool seal = false;
     tbc_compaction_result seal_result{};
     bool count_only = false; // TBC_COMPACTION_COUNT_ONLY: value_count only
+    uint32_t chain_slot = 0;       // chain server: the batch's descriptor slot
+    unsigned long long chain_seq = 0; // and sequence number
 };
 
 struct tbc_kway {
@@ -498,12 +521,9 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     e->flags = config->flags;
     e->dev.size = config->arena_bytes ? config->arena_bytes : kDefaultArena;
     e->host.size = kPinnedArena;
-    // TBC_FRONT_PRIORITY=1 (A/B measurement only): the engine stream (fronts,
-    // sorts) at the highest stream priority, the tails' chains filling in.
-    int lo_prio = 0, hi_prio = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) hi_prio = 0;
-    if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, getenv("TBC_FRONT_PRIORITY") ? hi_prio : 0) !=
-        hipSuccess) {
+    // (The engine stream at the highest priority measured no different for
+    // config 1, 52.3 vs 52.0 ms: DESIGN 4.3.)
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return TBC_ERR_DEVICE;
     }
@@ -528,10 +548,16 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
     static const bool high = getenv("TBC_TAIL_PRIORITY") != nullptr; // A/B measurement only
     {
-        const char *q = getenv("GPU_MAX_HW_QUEUES"), *t = getenv("TBC_TAILS");
+        const char *q = getenv("GPU_MAX_HW_QUEUES"), *t = getenv("TBC_TAILS"), *cs = getenv("TBC_CHAIN_SERVER");
         const int queues = q && atoi(q) > 0 ? atoi(q) : 4;
-        const int want = t && atoi(t) > 0 ? atoi(t) : queues - 1;
+        e->server = !(cs && cs[0] == '0');
+        // Streams, one per hardware queue: the engine stream, the chain
+        // stream (server) and the tails.
+        const int want = t && atoi(t) > 0 ? atoi(t) : queues - (e->server ? 2 : 1);
         e->ntails = want < 1 ? 1 : (want > tbc_engine::kMaxTails ? tbc_engine::kMaxTails : want);
+        const char *w = getenv("TBC_SERVER_WGS"), *v = getenv("TBC_SERVER_WAVES"); // A/B measurement
+        if (w && atoi(w) > 0) e->wide_wgs = e->narrow_wgs = (uint32_t)atoi(w);
+        if (v && atoi(v) > 0) e->wide_waves = e->narrow_waves = (uint32_t)atoi(v);
     }
     for (int t = 0; ok && t < e->ntails; t++)
         ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, high ? prio_greatest : 0) == hipSuccess &&
@@ -555,6 +581,29 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     ok = ok && ensure_masks(e, kInitialMaskWords);
     ok = ok && hipMalloc((void **)&e->d_error, 256) == hipSuccess &&
          hipMemsetAsync(e->d_error, 0, 256, e->stream) == hipSuccess;
+    if (ok && e->server) {
+        // kChainSlots claim words, the published count on a line of its own,
+        // kChainSlots batch descriptors; all zero.
+        const uint64_t ring_bytes = 8ull * kChainSlots + 256 + sizeof(ChainBatch) * kChainSlots;
+        ok = hipStreamCreateWithFlags(&e->chain_stream, hipStreamNonBlocking) == hipSuccess &&
+             hipMalloc((void **)&e->ring_mem, ring_bytes) == hipSuccess &&
+             hipMemsetAsync(e->ring_mem, 0, ring_bytes, e->stream) == hipSuccess;
+        for (uint32_t i = 0; ok && i < kChainSlots; i++)
+            ok = hipEventCreateWithFlags(&e->slot_ev[i], hipEventDisableTiming) == hipSuccess;
+        if (ok) {
+            ChainRing &r = e->ring;
+            r.claim = (unsigned long long *)e->ring_mem;
+            r.pub = (unsigned long long *)(e->ring_mem + 8ull * kChainSlots);
+            r.batches = (ChainBatch *)(e->ring_mem + 8ull * kChainSlots + 256);
+            r.active = (uint32_t *)(e->ring_mem + 8ull * kChainSlots + 128);
+            r.closing = (unsigned long long *)(e->ring_mem + 8ull * kChainSlots + 192);
+            // An idle server wave polls 200 us (100 MHz clock) before leaving,
+            // so a running instance takes a batch published meanwhile at once
+            // (a later instance is queued behind it on the chain stream).
+            const char *l = getenv("TBC_CHAIN_LINGER_US");
+            r.linger = 100u * (uint32_t)(l && atoi(l) >= 0 ? atoi(l) : 200);
+        }
+    }
     if (!ok) {
         tbc_engine_deinit(e);
         return TBC_ERR_OUT_OF_MEMORY;
@@ -569,6 +618,12 @@ void tbc_engine_deinit(tbc_engine *e) {
     hipStreamSynchronize(e->stream);
     for (int t = 0; t < e->ntails; t++)
         if (e->tail[t]) hipStreamSynchronize(e->tail[t]);
+    // The last server instance leaves once the ring has stayed empty.
+    if (e->chain_stream) hipStreamSynchronize(e->chain_stream);
+    for (uint32_t i = 0; i < kChainSlots; i++)
+        if (e->slot_ev[i]) hipEventDestroy(e->slot_ev[i]);
+    if (e->chain_stream) hipStreamDestroy(e->chain_stream);
+    if (e->ring_mem) hipFree(e->ring_mem);
     if (e->sort_stream) hipStreamSynchronize(e->sort_stream);
     for (auto &p : e->pending_sorts) e->event_pool.push_back(p.done);
     for (auto &t : e->tail_out) e->event_pool.push_back(t.done);
@@ -980,11 +1035,16 @@ tbc_status tbc_synchronize(tbc_engine *e) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!sync_streams(e)) return TBC_ERR_DEVICE;
     // Errors the device recorded for calls that had already returned.
-    uint32_t err = 0;
-    if (hipMemcpy(&err, e->d_error, 4, hipMemcpyDeviceToHost) != hipSuccess) return TBC_ERR_DEVICE;
-    if (err) {
-        if (hipMemset(e->d_error, 0, 4) != hipSuccess) return TBC_ERR_DEVICE;
-        return TBC_ERR_BLOCK_INVALID;
+    // (Engine stream, not the null stream: nothing here waits behind a
+    // running chain server.)
+    uint32_t err[2] = {0, 0};
+    if (hipMemcpyAsync(err, e->d_error, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        return TBC_ERR_DEVICE;
+    if (err[0] || err[1]) {
+        if (hipMemsetAsync(e->d_error, 0, 8, e->stream) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess)
+            return TBC_ERR_DEVICE;
+        return err[1] ? TBC_ERR_DEVICE : TBC_ERR_BLOCK_INVALID; // [1]: the chain ring lost a task
     }
     return TBC_OK;
 }
@@ -1408,6 +1468,59 @@ tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment
     return st;
 }
 
+// Chain server, front side (engine stream, after the batch's bodies are in
+// place): the batch published under the next sequence number. Its descriptor
+// slot (sequence % kChainSlots) is free once the batch that held it has
+// completed (its tail's slot event): a caller with kChainSlots batches in
+// flight waits for the oldest here.
+static bool publish_chains(tbc_engine *e, tbc_batch *b, const JobDesc *d_jobs, int njobs, uint32_t dblocks,
+                           JobResultDev *d_res, uint8_t *d_infos, const uint32_t *d_ready, uint32_t *d_table_cnt,
+                           unsigned long long *d_done) {
+    if (!e->server || !dblocks) return true;
+    if (dblocks > kChainMaxTasks) return false;
+    auto &f = e->slot_fifo;
+    while (!f.empty() && hipEventQuery(e->slot_ev[f.front()]) == hipSuccess) f.erase(f.begin());
+    while (f.size() >= kChainSlots) {
+        if (hipEventSynchronize(e->slot_ev[f.front()]) != hipSuccess) return false;
+        f.erase(f.begin());
+    }
+    const unsigned long long seq = e->published++;
+    b->chain_slot = (uint32_t)(seq % kChainSlots);
+    b->chain_seq = seq;
+    f.push_back(b->chain_slot);
+    ChainBatch cb;
+    cb.jobs = d_jobs;
+    cb.res = d_res;
+    cb.infos = d_infos;
+    cb.ready = d_ready;
+    cb.table_cnt = d_table_cnt;
+    cb.done = d_done;
+    cb.njobs = njobs;
+    cb.ntasks = dblocks;
+    return launch_chain_publish(e->ring, cb, seq, e->stream) == 0;
+}
+
+// Chain server, tail side (after the batch's fork): a server instance queued
+// on the chain stream (it runs at once unless one is still running, whose
+// waves take these tasks too), and the batch's tail waits for its count.
+// Without the server: the batch's own chain and index-block kernels.
+static bool tail_chains(tbc_engine *e, tbc_batch *b, hipStream_t T, const JobDesc *d_jobs, int njobs, uint32_t dblocks,
+                        uint32_t tables, JobResultDev *d_res, uint8_t *d_infos, const uint64_t *d_status,
+                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
+                        unsigned long long *d_done, bool wide) {
+    if (!e->server)
+        return launch_blocks_tail(d_jobs, njobs, dblocks, tables, d_res, d_infos, d_status, e->masks, d_block_tile,
+                                  d_splits, d_ready, T, mark_cb, b) == 0;
+    if (!dblocks) return true;
+    bool ok = hipStreamWaitEvent(e->chain_stream, b->fork, 0) == hipSuccess &&
+              launch_chain_server(e->ring, b->chain_seq, wide ? e->wide_wgs : e->narrow_wgs,
+                                  wide ? e->wide_waves : e->narrow_waves, e->chain_stream) == 0 &&
+              launch_chain_wait(d_done, dblocks, d_res, (uint32_t)njobs, T) == 0 &&
+              hipEventRecord(e->slot_ev[b->chain_slot], T) == hipSuccess;
+    mark_cb(b, "chains");
+    return ok;
+}
+
 static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, bool pipeline,
                               tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
@@ -1597,11 +1710,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     const bool spec_regime = !grid_mode && !pipeline &&
                              !(flags0 & (TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_COUNT_ONLY)) &&
                              (uint64_t)(dblocks + 1) / 2 <= fused_max_chain_waves();
-    static const bool no_spec = getenv("TBC_NO_SPECULATION") != nullptr; // A/B measurement only
-    // The speculated batch's index blocks and results on a tail stream
-    // (round 3, one box: config 2 2.276/2.251 -> 2.235/2.222 ms, configs 3
-    // and 4 within noise); TBC_NO_TAIL_FORK=1 keeps them on the engine stream.
-    static const bool no_tail_fork = getenv("TBC_NO_TAIL_FORK") != nullptr; // A/B measurement only
+    // (The speculated batch's index blocks and results go to a tail stream:
+    // round 3, one box: config 2 2.276/2.251 -> 2.235/2.222 ms.)
     // Pipelined speculated batch (round 4): the speculated bodies are merged
     // on the engine stream (k_merge_unique) and the chains run on a tail
     // stream, packed on a share of the CUs, so chains of batches in flight
@@ -1622,15 +1732,14 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
-        d.unique = (spec_regime || (grid_mode && grid_spec)) && !no_spec &&
+        d.unique = (spec_regime || (grid_mode && grid_spec)) &&
                    (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) && d.dblock_max > 0;
         any_unique |= d.unique != 0;
     }
     // Pipelined: the speculated jobs' tiles of kUniqueTile positions and
-    // their merge-path splits (merge.hip k_merge_unique). TBC_PIPE_PRODUCERS=1
-    // (A/B measurement only) merges them by one producer wave per block instead.
-    static const bool pipe_producers = getenv("TBC_PIPE_PRODUCERS") != nullptr;
-    const bool unique_tiles = any_unique && ((spec_pipe && !pipe_producers) || grid_mode);
+    // their merge-path splits (merge.hip k_merge_unique; round 4 measured it
+    // faster than one producer wave per block).
+    const bool unique_tiles = any_unique && (spec_pipe || grid_mode);
     uint32_t utiles = 0, usplits = 0;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
@@ -1645,6 +1754,11 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         }
     }
 
+    // Chain server geometry (tail_chains): the front fits beside a chain
+    // workgroup when every job merges by k_merge_unique or by the
+    // timestamp-key mask merge.
+    bool wide_front = !grid_mode;
+    for (uint32_t k = 0; k < count; k++) wide_front &= sj[k].unique || sj[k].key_kind == kKeyTimestamp;
     // Device layout of the batch.
     const uint64_t sz_jobs = align_up(sizeof(JobDesc) * (uint64_t)count, 256);
     const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
@@ -1662,7 +1776,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     // tile status, block tiles, per-block landed counts, the assembling
     // merge's look-back words (one per tile) and its ticket counters
-    const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8 + 8ull * tiles + 16 + 32, 256);
+    // (+ the chain server's done count and per-table block counts)
+    const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8 + 8ull * tiles + 16 + 32 + 8 + 4ull * tables, 256);
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
     uint8_t *dbase = e->dev.open(sz_in + sz_splits + sz_tiles + sz_res + sz_infos, &b->dev_region);
@@ -1681,6 +1796,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     uint32_t *d_ready = d_block_tile + dblocks;
     uint64_t *d_lookback = (uint64_t *)(uintptr_t)align_up((uint64_t)(uintptr_t)(d_ready + dblocks + 2), 8);
     uint32_t *d_ticket = (uint32_t *)(d_lookback + tiles);
+    unsigned long long *d_done = (unsigned long long *)(d_ticket + 8); // chain server: tasks finished
+    uint32_t *d_table_cnt = d_ticket + 10;                             // chain server: blocks per table
     const bool merge_bodies = false;
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
@@ -1815,6 +1932,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                  d_splits, 1, s) == 0;
             mark_cb(b, "recompute_assemble");
         }
+        ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
+                                  d_table_cnt, d_done);
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
@@ -1823,8 +1942,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         b->mark_stream = T;
         mark_cb(b, "tail_wait");
         if (ok && count)
-            ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
-                                    e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
+            ok = tail_chains(e, b, T, (const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
+                             d_block_tile, d_splits, d_ready, d_done, wide_front);
         for (int o = 0; ok && o < e->ntails; o++)
             if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
         if (ok && n_checks)
@@ -1849,6 +1968,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
+        ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
+                                  d_table_cnt, d_done);
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
@@ -1857,8 +1978,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         b->mark_stream = T;
         mark_cb(b, "tail_wait");
         if (ok && count)
-            ok = launch_blocks_tail((const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
-                                    e->masks, d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
+            ok = tail_chains(e, b, T, (const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
+                             d_block_tile, d_splits, d_ready, d_done, wide_front);
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {
@@ -1887,25 +2008,17 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // bodies; each kernel leaves at once when none broke). Tail: the
         // chains of every data block, the index blocks, the results.
         const JobDesc *dj = (const JobDesc *)d_in;
-        if (unique_tiles) {
-            ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s, mark_cb,
-                                           b) == 0;
-        } else {
-            ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
-            mark_cb(b, "partition_blocks");
-        }
+        ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s, mark_cb, b) == 0;
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, 0) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 0, s) == 0;
         mark_cb(b, "assemble");
-        if (!unique_tiles) {
-            ok = ok && launch_produce_unique(dj, (int)count, dblocks, d_res, d_bsplits, s) == 0;
-            mark_cb(b, "produce");
-        }
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, 1) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 1, s) == 0;
         mark_cb(b, "recompute_assemble");
+        ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
+                                  d_table_cnt, d_done);
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
@@ -1913,8 +2026,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
         b->mark_stream = T;
         mark_cb(b, "tail_wait");
-        ok = ok && launch_blocks_tail(dj, (int)count, dblocks, tables, d_res, d_infos, d_status, e->masks,
-                                      d_block_tile, d_splits, d_ready, T, mark_cb, b) == 0;
+        ok = ok && tail_chains(e, b, T, dj, (int)count, dblocks, tables, d_res, d_infos, d_status, d_block_tile,
+                               d_splits, d_ready, d_done, wide_front);
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {
@@ -1928,7 +2041,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             if (ok) e->tail_out.push_back(std::move(to));
             else if (to.done) e->event_pool.push_back(to.done);
         }
-    } else if (any_unique && !no_tail_fork) {
+    } else if (any_unique) {
         // Speculated jobs: their block splits and results first, then the
         // merge of the others, then ONE block pass for all (speculated
         // producers merge their blocks themselves), then the recomputation of
@@ -1971,21 +2084,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             if (ok) e->tail_out.push_back(std::move(to));
             else if (to.done) e->event_pool.push_back(to.done);
         }
-    } else if (any_unique) { // the speculated path with everything on the engine stream (A/B only)
-        const JobDesc *dj = (const JobDesc *)d_in;
-        ok = ok && launch_partition_blocks(dj, (int)count, dblocks, d_bsplits, d_res, s) == 0;
-        mark_cb(b, "partition_blocks");
-        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, 0) == 0;
-        ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
-                                 d_block_tile, d_splits, false, maybe_sparse, s, mark_cb, b, false, d_bsplits, 0,
-                                 false) == 0;
-        ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
-                                d_res, s, mark_cb, b, 1) == 0;
-        ok = ok && launch_blocks(dj, (int)count, tiles, dblocks, tables, d_ready, d_res, d_infos, d_status, e->masks,
-                                 d_block_tile, d_splits, false, true, s, mark_cb, b, false, d_bsplits, 1, true) == 0;
-        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess;
-        ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     } else {
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
@@ -2067,10 +2165,9 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
             k++;
         }
     }
-    static const bool no_groups = getenv("TBC_NO_GROUPS") != nullptr; // A/B measurement only
     uint32_t groups = 1;
     std::vector<uint64_t> n(count, 0);
-    if (!no_groups && count >= 2 &&
+    if (count >= 2 &&
         !(jobs_in[0].flags & (TBC_COMPACTION_GRID | TBC_COMPACTION_VALUES_ONLY | TBC_COMPACTION_COUNT_ONLY))) {
         uint64_t waves = 0;
         for (uint32_t i = 0; i < count; i++) {

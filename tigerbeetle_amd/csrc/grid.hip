@@ -215,9 +215,8 @@ __global__ __launch_bounds__(256) void k_upload(uint64_t *dst, const uint64_t *s
 
 int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    static const bool copy = getenv("TBC_UPLOAD_COPY") != nullptr;
     if (!bytes) return 0;
-    if (copy || (((uintptr_t)dst | (uintptr_t)host_src) & 7))
+    if (((uintptr_t)dst | (uintptr_t)host_src) & 7)
         return hipMemcpyAsync(dst, host_src, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
     const uint64_t n8 = bytes / 8;
     const uint32_t tail = (uint32_t)(bytes - 8 * n8);
