@@ -8,11 +8,14 @@ changes; each of those tests compares with the oracle.
                                            highest stream priority
   TBC_GRID_SPECULATION=1                   grid batches merge UNIQUE_KEYS jobs
                                            tile by tile, recompute in front
-  TBC_CHAIN_SERVER=0, TBC_TAILS=2,         one chain kernel per batch tail (the
-  TBC_DEBUG_SYNC=1                         round-4 path); stage-by-stage waits
-  TBC_SERVER_WGS=64, TBC_SERVER_WAVES=4,   a small chain server whose idle
-  TBC_CHAIN_LINGER_US=0, TBC_GROUPS=2      waves leave at once; two job groups
-                                           in the throughput regime
+  TBC_TAILS=2, TBC_DEBUG_SYNC=1            two tails; stage-by-stage waits
+  TBC_CHAIN_SERVER=1                       the chain server (round 5, opt-in):
+                                           every batch's chains claimed by one
+                                           server on its own stream
+  TBC_CHAIN_SERVER=1, TBC_SERVER_WGS=64,   a small server whose idle waves
+  TBC_SERVER_WAVES=4,                      leave at once and poll slowly; two
+  TBC_CHAIN_LINGER_US=0,                   job groups in the throughput regime
+  TBC_CHAIN_BACKOFF=128, TBC_GROUPS=2
 
 GPU_MAX_HW_QUEUES is HIP's own (the engine sizes its tails from it).
 """
@@ -64,11 +67,20 @@ def test_grid_speculation_bit_exact():
 
 
 @pytest.mark.gpu
-def test_per_batch_tails_bit_exact():
-    _child({"TBC_CHAIN_SERVER": "0", "TBC_TAILS": "2", "TBC_DEBUG_SYNC": "1"}, FILES, PIPELINED)
+def test_two_tails_debug_sync_bit_exact():
+    _child({"TBC_TAILS": "2", "TBC_DEBUG_SYNC": "1"}, FILES, PIPELINED)
+
+
+@pytest.mark.gpu
+def test_chain_server_bit_exact():
+    """The chain server with its default geometry: the pipelined, grid and
+    throughput-regime tests, and the 11-bar config-1 lockstep with a
+    checkpoint and restart."""
+    _child({"TBC_CHAIN_SERVER": "1"}, FILES, PIPELINED)
+    _child({"TBC_CHAIN_SERVER": "1"}, ("test_gpu_config1.py",), "checkpoint", timeout=300)
 
 
 @pytest.mark.gpu
 def test_small_chain_server_bit_exact():
-    _child({"TBC_SERVER_WGS": "64", "TBC_SERVER_WAVES": "4", "TBC_CHAIN_LINGER_US": "0", "TBC_GROUPS": "2"}, FILES,
-           PIPELINED)
+    _child({"TBC_CHAIN_SERVER": "1", "TBC_SERVER_WGS": "64", "TBC_SERVER_WAVES": "4", "TBC_CHAIN_LINGER_US": "0",
+            "TBC_CHAIN_BACKOFF": "128", "TBC_GROUPS": "2"}, FILES, PIPELINED)

@@ -365,6 +365,20 @@ struct StepCompact {
     }
 };
 
+// The T-table layout a step reads, its loader, and the step the same
+// kernel's header checksums use (full tables: VALU round keys; compact: its
+// own step).
+template <class Step> struct TableLayout {
+    static constexpr uint32_t kDwords = kTableDwords;
+    using HeaderStep = StepValuKey;
+    __device__ static __forceinline__ void load(uint32_t *sT) { load_tables(sT); }
+};
+template <> struct TableLayout<StepCompact> {
+    static constexpr uint32_t kDwords = kCompactTableDwords;
+    using HeaderStep = StepCompact;
+    __device__ static __forceinline__ void load(uint32_t *sT) { load_tables_compact(sT); }
+};
+
 // A step with `kMaskedMsg` takes the message word and its lane masks (the
 // lanes whose block absorbs it this step) instead of the selected word
 // (tools/aegis_lab.hip: hand-scheduled variants, measured no faster alone).
@@ -387,7 +401,7 @@ template <class S> struct StepMasked<S, decltype((void)S::kMaskedMsg)> {
 // continues in the lean loop (the finished group's lanes compute junk, its
 // tag is already captured) and ends the same way. Every load stays inside
 // its own group's message (addresses are clamped to it).
-template <class Msg, class Step = StepValuKey>
+template <class Msg, class Step = StepValuKey, uint32_t kGroup = 8>
 __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &msg) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t g = lane & 31, half = lane & 32;
@@ -433,7 +447,8 @@ __device__ __forceinline__ uint32_t aegis_mac32(const uint32_t *sT, const Msg &m
     // the top of each group the words of the next group are loaded (a full
     // group ahead of use, so the compiler's loop back-edge vmcnt(0) finds
     // them landed) and the addresses of the group after resolved.
-    constexpr uint32_t kGroup = 8; // windows per group: 64 updates (~3.8 us) hide two dependent gathers
+    // kGroup: windows per group (8: 64 updates, ~3.8 us, hide two dependent
+    // gathers; the chain server's direct loads take 4, half the registers).
     auto fast = [&](uint32_t w0, uint32_t w1) {
         if (w0 >= w1) return;
         const uint32_t groups = (w1 - w0 + kGroup - 1) / kGroup;
@@ -1468,7 +1483,8 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
                                             uint32_t chain_waves, const uint32_t *ready, const SplitDesc *bsplits,
                                             uint32_t phase) {
     constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
-    __shared__ uint32_t sT[kTableDwords];
+    using Layout = TableLayout<ChainStep>;
+    __shared__ uint32_t sT[Layout::kDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
     __shared__ uint32_t sProg[2 * kMaxChainWaves];
     __shared__ uint32_t sCons[2 * kMaxChainWaves]; // the chains' positions (body bytes needed so far)
@@ -1489,7 +1505,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
         const bool mine = threadIdx.x < 2 * C && locate(2 * blockIdx.x * C + threadIdx.x, ji_, k_);
         if (!__syncthreads_or(mine)) return;
     }
-    load_tables(sT);
+    Layout::load(sT);
     if (threadIdx.x < 2 * kMaxChainWaves) sProg[threadIdx.x] = sCons[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t wave_in_block = threadIdx.x >> 6;
@@ -1587,7 +1603,8 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     }
 
     (void)size;
-    finish_data_block(sT, sHdr[wave_in_block][upper ? 1 : 0], j, k, cnt, body_tag, writer);
+    finish_data_block<false, typename Layout::HeaderStep>(sT, sHdr[wave_in_block][upper ? 1 : 0], j, k, cnt, body_tag,
+                                                          writer);
 }
 
 template <bool Fused, class ChainStep = StepBpermute>
@@ -1726,14 +1743,16 @@ __device__ __forceinline__ void wave_sync() {
 // wave (both groups compute it; the lower group writes).
 constexpr uint32_t kIndexLdsBytes = 16384;
 
+template <class Step = StepValuKey>
 __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
                                                      uint8_t *infos) {
-    __shared__ uint32_t sT[kTableDwords];
+    using Layout = TableLayout<Step>;
+    __shared__ uint32_t sT[Layout::kDwords];
     __shared__ uint32_t sIdx[kIndexLdsBytes / 4];
     __shared__ uint64_t sKeys[2][4];
     // Sixteen waves load the 128 KiB of replicated tables (one wave alone spent
     // ~50 us on it); wave 0 then builds the table's index block.
-    load_tables(sT);
+    Layout::load(sT);
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const uint32_t wave = blockIdx.x;
@@ -1786,7 +1805,7 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
     }
     wave_sync();
     LdsMsg body(sIdx + kHeaderSize / 4, j.index_size - kHeaderSize);
-    const uint32_t body_tag = aegis_mac32(sT, body);
+    const uint32_t body_tag = aegis_mac32<LdsMsg, Step>(sT, body);
     const uint32_t index_slot = index_block_slot(t, k_last);
     HeaderFields h;
     h.cluster_lo = j.cluster_lo;
@@ -1800,7 +1819,7 @@ __global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int 
     h.meta3 = j.tree_id;  // .tree_id
     h.block_type = 4;     // BlockType.index (schema.zig:64)
     wave_sync();
-    const uint32_t hdr_tag = finish_header(sT, sIdx, h, body_tag);
+    const uint32_t hdr_tag = finish_header<Step>(sT, sIdx, h, body_tag);
     wave_sync();
     if (lane < 4) sIdx[lane] = hdr_tag;
     wave_sync();
@@ -1893,6 +1912,12 @@ __global__ __launch_bounds__(256) void k_index_layout(const JobDesc *jobs, int n
 // agent atomic; consumer acquire -> plain loads).
 // --------------------------------------------------------------------------
 constexpr uint32_t kServerWavesMax = 16;
+// The server's message prefetch: 4 windows (32 updates, ~2-3 us at two or
+// more chain waves per SIMD) ahead; its loads are direct (no indirection).
+#ifndef TBC_SERVER_GROUP
+#define TBC_SERVER_GROUP 4
+#endif
+constexpr uint32_t kServerGroup = TBC_SERVER_GROUP;
 
 __device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1957,7 +1982,7 @@ __device__ __forceinline__ void seal_table(const uint32_t *sT, uint32_t *hdr, co
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // our own write-through zeros, read back below
     GlobalMsg body(idx + kHeaderSize, j.index_size - kHeaderSize);
-    const uint32_t body_tag = aegis_mac32<GlobalMsg, Step>(sT, body);
+    const uint32_t body_tag = aegis_mac32<GlobalMsg, Step, kServerGroup>(sT, body);
     HeaderFields h;
     h.cluster_lo = j.cluster_lo;
     h.cluster_hi = j.cluster_hi;
@@ -2031,7 +2056,8 @@ __global__ __launch_bounds__(64 * kServerWavesMax) void k_chain_server(ChainRing
         // Claim up to two tasks (lane 0): one fetch_add of 2 on the claim
         // word of the oldest batch with unclaimed tasks; leave once nothing
         // has been claimable for the linger time (idle polls back off to
-        // ~27 us).
+        // backoff_max pauses: every poll is a few cross-XCD loads of the
+        // same lines).
         uint32_t slot = 0, t0 = 0, got = 0;
         if (lane == 0) {
             const uint64_t since = wall_clock64();
@@ -2073,7 +2099,7 @@ __global__ __launch_bounds__(64 * kServerWavesMax) void k_chain_server(ChainRing
                     break;
                 }
                 for (uint32_t i = 0; i < backoff; i++) __builtin_amdgcn_s_sleep(63);
-                backoff = backoff < 16 ? 2 * backoff : 16;
+                backoff = 2 * backoff < r.backoff_max ? 2 * backoff : r.backoff_max;
             }
         }
         got = __builtin_amdgcn_readfirstlane(got);
@@ -2108,7 +2134,7 @@ __global__ __launch_bounds__(64 * kServerWavesMax) void k_chain_server(ChainRing
                 __hip_atomic_load(ready + task.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
                 st32<true>(&res.invariant, 0xdeafu);
             GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
-            const uint32_t body_tag = aegis_mac32<GlobalMsg, Step>(sT, body);
+            const uint32_t body_tag = aegis_mac32<GlobalMsg, Step, kServerGroup>(sT, body);
             finish_data_block<true, Step>(sT, hdr, j, k, cnt, body_tag, writer);
             // Its index entry, into the table's index block image.
             const uint32_t db = res.data_block_count, tb = k / j.dbcm, s = k - tb * j.dbcm;
@@ -2309,7 +2335,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
     if (mark) mark(mark_ctx, phase ? "recompute_blocks" : "data_blocks");
     if (!index_blocks) return 0;
     if (total_tables) {
-        hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
+        hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "index_blocks");
@@ -2319,7 +2345,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
 int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
                         uint8_t *d_infos, void *stream) {
     if (!total_tables) return 0;
-    hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, (hipStream_t)stream, d_jobs, njobs,
+    hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(total_tables), dim3(1024), 0, (hipStream_t)stream, d_jobs, njobs,
                        d_results, d_infos);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2387,7 +2413,7 @@ int launch_seal(const JobDesc *d_job, uint32_t blocks, uint32_t tables, JobResul
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (tables) {
-        hipLaunchKernelGGL(k_index_blocks, dim3(tables), dim3(1024), 0, s, d_job, 1, d_results, d_infos);
+        hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(tables), dim3(1024), 0, s, d_job, 1, d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;
@@ -2450,15 +2476,21 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
         } else {
             const uint32_t rounds = (waves + 256 * kMaxChainOnlyWaves - 1) / (256 * kMaxChainOnlyWaves);
             const uint32_t c = (waves + 256 * rounds - 1) / (256 * rounds);
-            hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
-                               d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
+            hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0,
+                               s, d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
                                d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         }
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "data_blocks");
     if (total_tables) {
-        hipLaunchKernelGGL(k_index_blocks, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
+        // Index blocks read the compact T-tables (80 KiB of LDS with the
+        // index image, not 144), so their 1,024-thread workgroups find a CU
+        // beside chain workgroups: config 2's index blocks 1,050 -> 634 us of
+        // summed time per step (gpurun_out/r05h). The chains keep the full
+        // tables: compact ones cost them 2,462 -> 3,142 us.
+        hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs,
+                           d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "index_blocks");

@@ -170,9 +170,10 @@ struct tbc_engine {
     // batches publish their data blocks (ChainRing: a descriptor and a claim
     // word per batch) and a server instance on the chain stream (a hardware
     // queue of its own) takes them, whatever batch they belong to; a batch's
-    // tail waits for its count. TBC_CHAIN_SERVER=0 (A/B measurement) restores
-    // one chain kernel per batch tail. Host side: the batches published so
-    // far and the descriptor slots of those in flight (oldest first).
+    // tail waits for its count. Opt-in (TBC_CHAIN_SERVER=1): it measured
+    // slower than one chain kernel per batch tail on every config (DESIGN
+    // 4.8). Host side: the batches published so far and the descriptor
+    // slots of those in flight (oldest first).
     bool server = false;
     hipStream_t chain_stream = nullptr;
     ChainRing ring{};
@@ -550,7 +551,7 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     {
         const char *q = getenv("GPU_MAX_HW_QUEUES"), *t = getenv("TBC_TAILS"), *cs = getenv("TBC_CHAIN_SERVER");
         const int queues = q && atoi(q) > 0 ? atoi(q) : 4;
-        e->server = !(cs && cs[0] == '0');
+        e->server = cs && cs[0] == '1';
         // Streams, one per hardware queue: the engine stream, the chain
         // stream (server) and the tails.
         const int want = t && atoi(t) > 0 ? atoi(t) : queues - (e->server ? 2 : 1);
@@ -602,6 +603,8 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
             // (a later instance is queued behind it on the chain stream).
             const char *l = getenv("TBC_CHAIN_LINGER_US");
             r.linger = 100u * (uint32_t)(l && atoi(l) >= 0 ? atoi(l) : 200);
+            const char *bo = getenv("TBC_CHAIN_BACKOFF"); // A/B measurement
+            r.backoff_max = bo && atoi(bo) > 0 ? (uint32_t)atoi(bo) : 16u;
         }
     }
     if (!ok) {

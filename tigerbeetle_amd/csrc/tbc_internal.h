@@ -206,7 +206,7 @@ struct ChainRing {
     unsigned long long *closing; // the instance (its first_seq + 1) that has decided to leave
     ChainBatch *batches;       // kChainSlots descriptors (batch sequence % kChainSlots)
     uint32_t linger;           // 100 MHz ticks an idle wave polls before it leaves
-    uint32_t pad;
+    uint32_t backoff_max;      // an idle wave's longest pause between polls (units of s_sleep 63, ~1.7 us)
 };
 constexpr uint32_t kChainMaxTasks = (1u << 19) - 1; // a batch's data blocks (20-bit count fields)
 
