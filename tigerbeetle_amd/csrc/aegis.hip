@@ -365,9 +365,34 @@ struct StepCompact {
     }
 };
 
+// Shared T-tables (index blocks, round 5): the four tables once, T_r[b] at
+// dword r * 256 + b — 4 KiB instead of 128. Lanes whose bytes fall in one
+// bank serialise, which costs nothing that matters for an index block's
+// short message, and the index-block workgroup (4 KiB of tables + its 16 KiB
+// image) starts on a CU beside a chain workgroup's 136 KiB instead of
+// waiting for one to leave (config 2: k_index_blocks ~1.1 ms of which ~1 ms
+// waiting).
+constexpr uint32_t kSharedTableDwords = 1024;
+
+struct StepShared {
+    __device__ static __forceinline__ uint32_t step(const uint32_t *sT, const TableBase &, uint32_t key_src,
+                                                    uint32_t x, uint32_t m) {
+        const uint32_t key = bpermute(key_src, x);
+        const uint32_t t0 = sT[x & 0xffu];
+        const uint32_t t1 = sT[256 + ((x >> 8) & 0xffu)];
+        const uint32_t t2 = sT[512 + ((x >> 16) & 0xffu)];
+        const uint32_t t3 = sT[768 + (x >> 24)];
+        uint32_t r = (key ^ m) ^ t0;
+        r ^= quad_perm<1, 2, 3, 0>(t1);
+        r ^= quad_perm<2, 3, 0, 1>(t2);
+        r ^= quad_perm<3, 0, 1, 2>(t3);
+        return r;
+    }
+};
+
 // The T-table layout a step reads, its loader, and the step the same
-// kernel's header checksums use (full tables: VALU round keys; compact: its
-// own step).
+// kernel's header checksums use (full tables: VALU round keys; compact and
+// shared: their own step).
 template <class Step> struct TableLayout {
     static constexpr uint32_t kDwords = kTableDwords;
     using HeaderStep = StepValuKey;
@@ -377,6 +402,13 @@ template <> struct TableLayout<StepCompact> {
     static constexpr uint32_t kDwords = kCompactTableDwords;
     using HeaderStep = StepCompact;
     __device__ static __forceinline__ void load(uint32_t *sT) { load_tables_compact(sT); }
+};
+template <> struct TableLayout<StepShared> {
+    static constexpr uint32_t kDwords = kSharedTableDwords;
+    using HeaderStep = StepShared;
+    __device__ static __forceinline__ void load(uint32_t *sT) {
+        for (uint32_t i = threadIdx.x; i < kSharedTableDwords; i += blockDim.x) sT[i] = c_aes.t[i >> 8][i & 255];
+    }
 };
 
 // A step with `kMaskedMsg` takes the message word and its lane masks (the
@@ -1743,15 +1775,16 @@ __device__ __forceinline__ void wave_sync() {
 // wave (both groups compute it; the lower group writes).
 constexpr uint32_t kIndexLdsBytes = 16384;
 
-template <class Step = StepValuKey>
-__global__ __launch_bounds__(1024) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
-                                                     uint8_t *infos) {
+template <class Step = StepShared, uint32_t kThreads = 64>
+__global__ __launch_bounds__(kThreads) void k_index_blocks(const JobDesc *jobs, int njobs, JobResultDev *res,
+                                                         uint8_t *infos) {
     using Layout = TableLayout<Step>;
     __shared__ uint32_t sT[Layout::kDwords];
     __shared__ uint32_t sIdx[kIndexLdsBytes / 4];
     __shared__ uint64_t sKeys[2][4];
-    // Sixteen waves load the 128 KiB of replicated tables (one wave alone spent
-    // ~50 us on it); wave 0 then builds the table's index block.
+    // The workgroup's waves load the tables (replicated 128 KiB tables took
+    // sixteen: one wave alone spent ~50 us on them); wave 0 then builds the
+    // table's index block.
     Layout::load(sT);
     __syncthreads();
     if (threadIdx.x >= 64) return;
@@ -2335,7 +2368,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
     if (mark) mark(mark_ctx, phase ? "recompute_blocks" : "data_blocks");
     if (!index_blocks) return 0;
     if (total_tables) {
-        hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs, d_results, d_infos);
+        hipLaunchKernelGGL((k_index_blocks<StepShared, 64>), dim3(total_tables), dim3(64), 0, s, d_jobs, njobs, d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "index_blocks");
@@ -2345,7 +2378,7 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
 int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
                         uint8_t *d_infos, void *stream) {
     if (!total_tables) return 0;
-    hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(total_tables), dim3(1024), 0, (hipStream_t)stream, d_jobs, njobs,
+    hipLaunchKernelGGL((k_index_blocks<StepShared, 64>), dim3(total_tables), dim3(64), 0, (hipStream_t)stream, d_jobs, njobs,
                        d_results, d_infos);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2413,7 +2446,7 @@ int launch_seal(const JobDesc *d_job, uint32_t blocks, uint32_t tables, JobResul
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (tables) {
-        hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(tables), dim3(1024), 0, s, d_job, 1, d_results, d_infos);
+        hipLaunchKernelGGL((k_index_blocks<StepShared, 64>), dim3(tables), dim3(64), 0, s, d_job, 1, d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;
@@ -2484,12 +2517,12 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
     }
     if (mark) mark(mark_ctx, "data_blocks");
     if (total_tables) {
-        // Index blocks read the compact T-tables (80 KiB of LDS with the
-        // index image, not 144), so their 1,024-thread workgroups find a CU
-        // beside chain workgroups: config 2's index blocks 1,050 -> 634 us of
-        // summed time per step (gpurun_out/r05h). The chains keep the full
-        // tables: compact ones cost them 2,462 -> 3,142 us.
-        hipLaunchKernelGGL(k_index_blocks<StepCompact>, dim3(total_tables), dim3(1024), 0, s, d_jobs, njobs,
+        // Index blocks read shared T-tables (StepShared: 20 KiB of LDS with
+        // the index image, not 144), so their one-wave workgroups start
+        // beside chain workgroups instead of waiting for a CU to empty. The
+        // chains keep the full tables: compact ones cost them 2,462 -> 3,142
+        // us per step in config 2 (gpurun_out/r05h).
+        hipLaunchKernelGGL((k_index_blocks<StepShared, 64>), dim3(total_tables), dim3(64), 0, s, d_jobs, njobs,
                            d_results, d_infos);
         if (hipGetLastError() != hipSuccess) return -1;
     }
