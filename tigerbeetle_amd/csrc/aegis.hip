@@ -1661,18 +1661,32 @@ __global__ __launch_bounds__(3 * 64 * kMaxChainWaves) void k_data_blocks_redo(
 // masks, parallel over merge positions (not sequential per block like the
 // fused path's producers): one workgroup per merge tile; the tile's output
 // offset (k_tile_scan) and A/B cursors (merge-path split) plus per-mask-word
-// prefix counts give every survivor its source value and output slot; each
-// wave then copies its word's survivors cooperatively, 16 bytes per lane, so
-// consecutive lanes read and write consecutive bytes. HBM-bound: every
-// survivor is read once and written once.
+// prefix counts give every survivor its source value and output slot.
+// HBM-bound: every survivor is read once and written once.
+//
+// Per half tile (1,024 merged positions) every survivor's source pointer is
+// staged in LDS first (each wave stages 4 mask words), then the workgroup
+// copies them in output order, 16 bytes per lane and 8 loads in flight per
+// lane, each destination found from the output position (a per-half table
+// of the data blocks' addresses). Round 4 copied one mask word's survivors
+// per wave at a time — for 16-32 byte values 1-2 KiB per wave per memory
+// round trip, here 8 KiB: config 1's assembly 12.3 -> 9.1 ms per step,
+// config 3's 804 -> 635 us, config 4's 262 -> 212 us; config 5's 128-byte
+// values unchanged (gpurun_out/r05k). A job with vcm < 15 or values over 256 bytes (none of
+// TigerBeetle's trees at 4 KiB blocks or more) finds each destination by a
+// division instead of the table.
+constexpr uint32_t kHalfTile = kMergeTile / 2;
+constexpr uint32_t kHalfBlocks = kHalfTile / 15 + 3;
+
 template <bool SparseOnly>
 __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs, uint32_t total_tiles,
-                                                  const uint64_t *status, const uint64_t *masks,
-                                                  const SplitDesc *splits, uint32_t *ready,
-                                                  const JobResultDev *res, uint32_t phase) {
-    constexpr uint32_t W = kMergeTile / 64; // mask words per kind per tile
-    __shared__ uint32_t s_pre[3][W + 1];    // survivors, A taken, B taken before word w
-    __shared__ uint64_t s_src[4][64], s_dst[4][64];
+                                                       const uint64_t *status, const uint64_t *masks,
+                                                       const SplitDesc *splits, uint32_t *ready,
+                                                       const JobResultDev *res, uint32_t phase) {
+    constexpr uint32_t W = kMergeTile / 64;       // mask words per kind per tile
+    __shared__ uint32_t s_pre[3][W + 1];          // survivors, A taken, B taken before word w
+    __shared__ uint64_t s_src[kHalfTile];         // source of each survivor of the half
+    __shared__ uint64_t s_blk[kHalfBlocks];       // data block k_first + i of the half's survivors
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1;
     if (phase == 1 && *(volatile const uint32_t *)jobs[0].spec_any == 0) return; // no speculation broke
@@ -1691,7 +1705,7 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
             const uint32_t pos0 = t * kMergeTile + 64 * w;
             return pos0 >= n ? 0ull : (n - pos0 >= 64 ? ~0ull : ((1ull << (n - pos0)) - 1));
         };
-        __syncthreads(); // the previous tile's readers of s_pre are done
+        __syncthreads(); // the previous tile's readers of s_pre / s_src are done
         if (tid < W) {
             const uint64_t sm = gld<uint64_t>(m + tid), am = gld<uint64_t>(m + W + tid);
             s_pre[0][tid + 1] = __builtin_popcountll(sm);
@@ -1711,46 +1725,74 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
         SegCursor ca, cb;
         ca.init(j.a, sp.seg_a);
         cb.init(j.b, sp.seg_b);
-        const uint32_t cpv_log = __builtin_ctz(vs >> 4);
-        // The next word's masks are loaded while this word is copied.
-        uint64_t sm_n = wv < W ? gld<uint64_t>(m + wv) : 0, am_n = wv < W ? gld<uint64_t>(m + W + wv) : 0;
-        for (uint32_t w = wv; w < W; w += 4) {
-            if (t * kMergeTile + 64 * w >= n) break;
-            const uint64_t sm = sm_n, am = am_n;
-            if (w + 4 < W) {
-                sm_n = gld<uint64_t>(m + w + 4);
-                am_n = gld<uint64_t>(m + W + w + 4);
+        const uint32_t cpv_log = __builtin_ctz(vs >> 4), qmask = (1u << cpv_log) - 1;
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t w0 = h * (W / 2);
+            if (t * kMergeTile + 64 * w0 >= n) break; // uniform
+            const uint32_t s0 = s_pre[0][w0], S = s_pre[0][w0 + W / 2] - s0;
+            if (S == 0) continue; // uniform
+            const uint32_t obase = (uint32_t)j.out_offset + out0 + s0; // the half's first output position
+            const bool fast = vcm >= 15 && vs <= 256; // uniform
+            const uint32_t kfirst = obase / vcm;
+            const uint32_t nblk = (obase + S - 1) / vcm - kfirst + 1;
+            if (fast && tid < nblk)
+                s_blk[tid] = (uint64_t)(uintptr_t)(block_ptr(j, data_block_slot(kfirst + tid, j.dbcm)) + kHeaderSize);
+            // Stage: wave wv takes words w0 + wv + 4i.
+            for (uint32_t w = w0 + wv; w < w0 + W / 2; w += 4) {
+                if (t * kMergeTile + 64 * w >= n) break;
+                const uint64_t sm = gld<uint64_t>(m + w), am = gld<uint64_t>(m + W + w);
+                if (sm == 0) continue;
+                const uint64_t valid = valid_of(w);
+                const uint32_t ab = a0 + s_pre[1][w], bb = b0 + s_pre[2][w];
+                ca.advance(ab);
+                cb.advance(bb);
+                if ((sm >> lane) & 1) {
+                    const uint32_t r = __builtin_popcountll(sm & lt);
+                    const uint8_t *src = ((am >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(am & lt), vs)
+                                                            : cb.elem(bb + __builtin_popcountll(valid & ~am & lt), vs);
+                    s_src[s_pre[0][w] - s0 + r] = (uint64_t)(uintptr_t)src;
+                }
             }
-            const uint32_t ns = __builtin_popcountll(sm);
-            if (ns == 0) continue;
-            const uint64_t valid = valid_of(w);
-            const uint32_t ab = a0 + s_pre[1][w], bb = b0 + s_pre[2][w];
-            ca.advance(ab);
-            cb.advance(bb);
-            if ((sm >> lane) & 1) {
-                const uint32_t r = __builtin_popcountll(sm & lt);
-                const uint64_t o = j.out_offset + out0 + s_pre[0][w] + r; // the job's merged output position
-                const uint8_t *src = ((am >> lane) & 1) ? ca.elem(ab + __builtin_popcountll(am & lt), vs)
-                                                        : cb.elem(bb + __builtin_popcountll(valid & ~am & lt), vs);
-                const uint32_t k = (uint32_t)(o / vcm);
-                uint8_t *dst = block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize +
-                               (size_t)(o - (uint64_t)k * vcm) * vs;
-                s_src[wv][r] = (uint64_t)(uintptr_t)src;
-                s_dst[wv][r] = (uint64_t)(uintptr_t)dst;
+            __syncthreads();
+            // Copy in output order: chunk c = survivor c >> cpv_log, 16-byte
+            // piece c & qmask; a lane's chunks are 256 apart.
+            const uint32_t total = S << cpv_log;
+            const uint32_t ds = 256u >> cpv_log; // survivors between a lane's chunks (vs <= 256)
+            for (uint32_t c = tid; !fast && c < total; c += 256) { // one chunk at a time (rare layouts)
+                const uint32_t o = obase + (c >> cpv_log);
+                const uint32_t k = o / vcm;
+                const u32x4 v = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[c >> cpv_log] + 16 * (c & qmask));
+                gst<u32x4>(block_ptr(j, data_block_slot(k, j.dbcm)) + kHeaderSize + (size_t)(o - k * vcm) * vs +
+                               16 * (c & qmask), v);
             }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            copy_staged(s_src[wv], s_dst[wv], ns, cpv_log);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (uint32_t c0 = 0; fast && c0 < total; c0 += 256 * 8) {
+                const uint32_t sl = (c0 + tid) >> cpv_log;
+                uint32_t k = (obase + sl) / vcm - kfirst;
+                uint32_t rem = obase + sl - (kfirst + k) * vcm;
+                u32x4 v[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t c = c0 + tid + 256 * u;
+                    if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[c >> cpv_log] + 16 * (c & qmask));
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t c = c0 + tid + 256 * u;
+                    if (c < total) {
+                        uint8_t *dst = (uint8_t *)(uintptr_t)s_blk[k] + (size_t)rem * vs + 16 * (c & qmask);
+                        gst<u32x4>(dst, v[u]);
+                    }
+                    rem += ds;
+                    while (rem >= vcm) {
+                        rem -= vcm;
+                        k++;
+                    }
+                }
+            }
+            __syncthreads(); // s_src and s_blk are rewritten by the next half
         }
-        // Count the survivors landed in every data block (checked by the
-        // chain kernel before it checksums the block).
-        // (No release fence: the reader is the next kernel in stream order, and
-        // an agent-scope release writes back the XCD's L2 — per tile, that
-        // quadrupled this kernel's time.)
-        __syncthreads();
-        if (tid == 0 && j.out_offset == 0) { // (an offset job is VALUES_ONLY: no chains count them)
+        // Count the survivors landed in every data block (as k_assemble).
+        if (tid == 0 && j.out_offset == 0) {
             const uint32_t cnt = s_pre[0][W];
             uint32_t o = out0;
             while (o < out0 + cnt) {
@@ -2302,6 +2344,14 @@ int launch_checksum_batch(const uint64_t *d_ptrs, const uint64_t *d_lens, uint32
 
 uint32_t fused_max_chain_waves() { return kFusedMaxChainWaves; }
 
+template <bool SparseOnly>
+static void run_assemble(uint32_t grid, hipStream_t s, const JobDesc *d_jobs, int njobs, uint32_t total_tiles,
+                         const uint64_t *d_status, const uint64_t *d_masks, const SplitDesc *d_splits,
+                         uint32_t *d_ready, const JobResultDev *d_results, uint32_t phase) {
+    hipLaunchKernelGGL(k_assemble<SparseOnly>, dim3(grid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
+                       d_masks, d_splits, d_ready, d_results, phase);
+}
+
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
@@ -2316,8 +2366,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         // and no index blocks.
         if (total_dblocks && !bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, phase);
+            run_assemble<false>(agrid, s, d_jobs, njobs, total_tiles, d_status, d_masks, d_splits, d_ready,
+                               (const JobResultDev *)d_results, phase);
             if (hipGetLastError() != hipSuccess) return -1;
         }
         if (mark) mark(mark_ctx, "assemble");
@@ -2328,8 +2378,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         // the bodies while the chains absorb them.
         if (maybe_sparse) { // heavy-dedup jobs: bodies first, parallel (sparse_job decides on device)
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-            hipLaunchKernelGGL(k_assemble<true>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, phase);
+            run_assemble<true>(agrid, s, d_jobs, njobs, total_tiles, d_status, d_masks, d_splits, d_ready,
+                               (const JobResultDev *)d_results, phase);
             if (hipGetLastError() != hipSuccess) return -1;
             if (mark) mark(mark_ctx, phase ? "recompute_assemble" : "assemble");
         }
@@ -2353,8 +2403,8 @@ int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32
         // reports an invariant error instead of checksumming a partial body.
         if (!bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, (const JobResultDev *)d_results, phase);
+            run_assemble<false>(agrid, s, d_jobs, njobs, total_tiles, d_status, d_masks, d_splits, d_ready,
+                               (const JobResultDev *)d_results, phase);
             if (hipGetLastError() != hipSuccess) return -1;
             if (mark) mark(mark_ctx, "assemble");
         }
@@ -2391,8 +2441,8 @@ int launch_assemble(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint
                     const SplitDesc *d_splits, uint32_t phase, void *stream) {
     if (!total_tiles) return 0;
     const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-    hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, (hipStream_t)stream, d_jobs, njobs, total_tiles,
-                       d_status, d_masks, d_splits, d_ready, d_results, phase);
+    run_assemble<false>(agrid, (hipStream_t)stream, d_jobs, njobs, total_tiles, d_status, d_masks, d_splits, d_ready,
+                               d_results, phase);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2462,8 +2512,8 @@ int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, 
     if (total_dblocks) {
         if (!bodies_done) {
             const uint32_t agrid = total_tiles < 8192 ? total_tiles : 8192;
-            hipLaunchKernelGGL(k_assemble<false>, dim3(agrid), dim3(256), 0, s, d_jobs, njobs, total_tiles, d_status,
-                               d_masks, d_splits, d_ready, d_results, 0u);
+            run_assemble<false>(agrid, s, d_jobs, njobs, total_tiles, d_status, d_masks, d_splits, d_ready, d_results,
+                                0u);
             if (hipGetLastError() != hipSuccess) return -1;
         }
         hipLaunchKernelGGL(k_index_layout, dim3((total_dblocks + 255) / 256), dim3(256), 0, s, d_jobs, njobs,

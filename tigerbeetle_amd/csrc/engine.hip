@@ -2011,11 +2011,15 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         // bodies; each kernel leaves at once when none broke). Tail: the
         // chains of every data block, the index blocks, the results.
         const JobDesc *dj = (const JobDesc *)d_in;
+        bool any_plain = false; // jobs not speculated: mask merge and assembly
+        for (uint32_t k = 0; k < count; k++) any_plain |= !sj[k].unique;
         ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s, mark_cb, b) == 0;
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, 0) == 0;
-        ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 0, s) == 0;
-        mark_cb(b, "assemble");
+        if (any_plain) {
+            ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 0, s) == 0;
+            mark_cb(b, "assemble");
+        }
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, 1) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 1, s) == 0;
