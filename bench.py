@@ -385,7 +385,7 @@ def cpu_baseline(config: int, njobs: int, budget_s: float = 12.0, bs: int = 1 <<
 # stream waiting for its front and for the tails before it; with the chain
 # server, the tail waiting for its batch's chains, which the server runs
 # beside other batches' — the batch's chain latency, not a launch).
-NOT_KERNELS = ("tail_wait", "chains")
+NOT_KERNELS = ("tail_wait", "tail_wait_paired", "chains")
 
 # bench kernel label -> rocprofv3 kernel symbol (tools/traffic.py short names)
 KERNEL_SYMBOL = {"merge_partition": "k_partition_all", "merge": "k_merge_tile", "data_blocks": "k_data_blocks",

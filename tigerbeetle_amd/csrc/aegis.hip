@@ -1513,7 +1513,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
                                             const uint64_t *status, const uint64_t *masks,
                                             const uint32_t *block_tile, const SplitDesc *splits,
                                             uint32_t chain_waves, const uint32_t *ready, const SplitDesc *bsplits,
-                                            uint32_t phase) {
+                                            uint32_t phase, uint32_t bid) {
     constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
     using Layout = TableLayout<ChainStep>;
     __shared__ uint32_t sT[Layout::kDwords];
@@ -1534,7 +1534,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     if (phase == 1) { // recomputation of broken speculations: leave at once if none of ours
         int ji_;
         uint32_t k_;
-        const bool mine = threadIdx.x < 2 * C && locate(2 * blockIdx.x * C + threadIdx.x, ji_, k_);
+        const bool mine = threadIdx.x < 2 * C && locate(2 * bid * C + threadIdx.x, ji_, k_);
         if (!__syncthreads_or(mine)) return;
     }
     Layout::load(sT);
@@ -1551,7 +1551,7 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     uint32_t k;
     if (Fused && wave_in_block >= C) { // producer
         const uint32_t p = wave_in_block - C;
-        const uint32_t mine = 2 * (blockIdx.x * C + (p >> 1)) + (p & 1);
+        const uint32_t mine = 2 * (bid * C + (p >> 1)) + (p & 1);
         if (!locate(mine, ji, k)) return;
         const JobDesc &j = jobs[ji];
         if (j.unique && phase != 1) { // speculated: merges the block's values itself
@@ -1595,7 +1595,8 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
     // The chain is the critical path and mostly waits on LDS: let its
     // instructions win the SIMD's issue arbitration over the producers'.
     if constexpr (Fused) __builtin_amdgcn_s_setprio(2);
-    const uint32_t wave = blockIdx.x * C + wave_in_block;
+    if (!Fused && wave_in_block >= C) return; // a paired launch's narrower half (k_data_blocks_pair)
+    const uint32_t wave = bid * C + wave_in_block;
     const bool upper = lane >= 32;
     const uint32_t mine = 2 * wave + (upper ? 1u : 0u);
     const bool live = locate(mine, ji, k);
@@ -1645,7 +1646,18 @@ __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data
     const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
     const uint32_t *ready, const SplitDesc *bsplits, uint32_t phase) {
     data_blocks<Fused, ChainStep>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready,
-                                  bsplits, phase);
+                                  bsplits, phase, blockIdx.x);
+}
+
+// Two grid batches' chains in one launch (tail pairing, engine.hip
+// grid_tail_pair): workgroups [0, a.wgs) take batch a's blocks, the rest
+// batch b's, each half with its own chain waves per workgroup.
+template <class ChainStep>
+__global__ __launch_bounds__(1024) void k_data_blocks_pair(ChainHalf a, ChainHalf b) {
+    const bool second = blockIdx.x >= a.wgs;
+    const ChainHalf &x = second ? b : a;
+    data_blocks<false, ChainStep>(x.jobs, x.njobs, x.total, x.res, nullptr, nullptr, nullptr, nullptr, x.c, x.ready,
+                                  nullptr, 0u, second ? blockIdx.x - a.wgs : blockIdx.x);
 }
 
 // The recomputation of broken speculations (phase 1) in its own symbol, so
@@ -1654,7 +1666,8 @@ __global__ __launch_bounds__(3 * 64 * kMaxChainWaves) void k_data_blocks_redo(
     const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res, const uint64_t *status,
     const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
     const uint32_t *ready) {
-    data_blocks<true>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready, nullptr, 1u);
+    data_blocks<true>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready, nullptr, 1u,
+                      blockIdx.x);
 }
 
 // Throughput regime, pass 1: assemble every data block body from the merge's
@@ -2577,6 +2590,47 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mark) mark(mark_ctx, "index_blocks");
+    return 0;
+}
+
+// Tail pairing: two grid batches' chains in one launch, then each batch's
+// index blocks. Each half packs its chains as launch_blocks_tail would (4
+// chain waves per workgroup, 8 above 512 waves); the round key comes by
+// VALU lane moves unless a half runs two chains per SIMD.
+int launch_blocks_tail_pair(const TailHalf &a, const TailHalf &b, void *stream, void (*mark)(void *, const char *),
+                            void *ctx_a, void *ctx_b) {
+    hipStream_t s = (hipStream_t)stream;
+    auto half = [](const TailHalf &t) {
+        ChainHalf h{t.jobs, t.njobs, t.dblocks, t.res, t.ready, 0u, 0u};
+        const uint32_t waves = (t.dblocks + 1) / 2;
+        if (!waves) return h;
+        h.c = waves > 512 ? 8u : 4u;
+        if (h.c > waves) h.c = waves;
+        h.wgs = (waves + h.c - 1) / h.c;
+        return h;
+    };
+    const ChainHalf ha = half(a), hb = half(b);
+    const uint32_t c = ha.c > hb.c ? ha.c : hb.c;
+    if (ha.wgs + hb.wgs) {
+        if (c >= 8)
+            hipLaunchKernelGGL((k_data_blocks_pair<StepBpermute>), dim3(ha.wgs + hb.wgs), dim3(64 * c), 0, s, ha, hb);
+        else
+            hipLaunchKernelGGL((k_data_blocks_pair<StepValuKey>), dim3(ha.wgs + hb.wgs), dim3(64 * c), 0, s, ha, hb);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (mark) {
+        mark(ctx_a, "data_blocks");
+        mark(ctx_b, "data_blocks");
+    }
+    for (int i = 0; i < 2; i++) {
+        const TailHalf &t = i ? b : a;
+        if (t.tables) {
+            hipLaunchKernelGGL((k_index_blocks<StepShared, 64>), dim3(t.tables), dim3(64), 0, s, t.jobs, t.njobs, t.res,
+                               t.infos);
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
+        if (mark) mark(i ? ctx_b : ctx_a, "index_blocks");
+    }
     return 0;
 }
 

@@ -174,6 +174,11 @@ struct tbc_engine {
     // slower than one chain kernel per batch tail on every config (DESIGN
     // 4.8). Host side: the batches published so far and the descriptor
     // slots of those in flight (oldest first).
+    // Tail pairing: a grid batch whose tail waits for the next grid batch,
+    // so that both batches' chains run as one launch on one tail stream
+    // (grid_tail_pair); launched alone by any other call (flush_tail).
+    tbc_batch *deferred = nullptr;
+    bool pair_tails = true;
     bool server = false;
     hipStream_t chain_stream = nullptr;
     ChainRing ring{};
@@ -416,6 +421,21 @@ struct tbc_batch {
     bool count_only = false; // TBC_COMPACTION_COUNT_ONLY: value_count only
     uint32_t chain_slot = 0;       // chain server: the batch's descriptor slot
     unsigned long long chain_seq = 0; // and sequence number
+    // A grid batch's tail (chains, index blocks, input checks, results), as
+    // enqueued when the batch is submitted or, deferred for pairing, later.
+    struct GridTail {
+        TailHalf half{};
+        const uint64_t *status = nullptr;
+        const uint32_t *block_tile = nullptr;
+        const SplitDesc *splits = nullptr;
+        unsigned long long *done_ctr = nullptr;
+        bool wide = false;
+        const ResolveItem *resolve = nullptr;
+        uint32_t n_resolve = 0, n_checks = 0;
+        InputCheck *checks = nullptr;
+        tbc_grid *grid = nullptr;
+        uint64_t copy_bytes = 0;
+    } gt;
 };
 
 struct tbc_kway {
@@ -493,10 +513,12 @@ static bool join_sorts(tbc_engine *e) {
 
 // Every stream of the engine drained (internal: no deferred-error report).
 static bool sync_streams(tbc_engine *e);
+static void flush_tail(tbc_engine *e);
 
 // Later work on the engine stream that touches grid blocks (staging blocks in
 // or out, synchronous checks) waits for every batch tail enqueued so far.
 static bool join_tails(tbc_engine *e) {
+    flush_tail(e);
     for (int t = 0; t < e->ntails; t++)
         if (hipStreamWaitEvent(e->stream, e->tail_ev[t], 0) != hipSuccess) return false;
     return join_sorts(e);
@@ -552,6 +574,8 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
         const char *q = getenv("GPU_MAX_HW_QUEUES"), *t = getenv("TBC_TAILS"), *cs = getenv("TBC_CHAIN_SERVER");
         const int queues = q && atoi(q) > 0 ? atoi(q) : 4;
         e->server = cs && cs[0] == '1';
+        const char *pt = getenv("TBC_PAIR_TAILS"); // A/B: 0 = every grid tail alone
+        e->pair_tails = !(pt && pt[0] == '0');
         // Streams, one per hardware queue: the engine stream, the chain
         // stream (server) and the tails.
         const int want = t && atoi(t) > 0 ? atoi(t) : queues - (e->server ? 2 : 1);
@@ -616,6 +640,7 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
 }
 
 void tbc_engine_deinit(tbc_engine *e) {
+    flush_tail(e);
     if (!e) return;
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
@@ -697,6 +722,7 @@ void tbc_grid_deinit(tbc_grid *g) {
 }
 
 tbc_status tbc_grid_invalidate(tbc_grid *g) {
+    flush_tail(g ? g->engine : nullptr);
     if (!g) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
@@ -711,6 +737,7 @@ tbc_status tbc_grid_block_pointer(const tbc_grid *g, uint64_t address, void **ou
 }
 
 tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *blocks, uint32_t count) {
+    flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
         if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
@@ -749,6 +776,7 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
 }
 
 tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *const *blocks, uint32_t count) {
+    flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
         if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
@@ -763,6 +791,7 @@ tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *con
 
 tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *host_images,
                                      uint32_t count, uint64_t previous_address, const uint64_t *previous_checksum) {
+    flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !host_images))) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     const uint32_t bs = e->block_size;
@@ -905,6 +934,7 @@ tbc_status tbc_tree_layout_get(const tbc_engine *e, const tbc_tree *tree, tbc_tr
 }
 
 tbc_status tbc_host_register(tbc_engine *e, void *ptr, uint64_t bytes) {
+    flush_tail(e);
     if (!e || !ptr || !bytes) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     const uint64_t lo = (uint64_t)(uintptr_t)ptr;
@@ -916,6 +946,7 @@ tbc_status tbc_host_register(tbc_engine *e, void *ptr, uint64_t bytes) {
 }
 
 tbc_status tbc_host_unregister(tbc_engine *e, void *ptr) {
+    flush_tail(e);
     if (!e || !ptr) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     const uint64_t lo = (uint64_t)(uintptr_t)ptr;
@@ -936,12 +967,14 @@ tbc_status tbc_device_alloc(tbc_engine *e, uint64_t bytes, void **out_ptr) {
 }
 
 tbc_status tbc_device_free(tbc_engine *e, void *ptr) {
+    flush_tail(e);
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     return hipFree(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
 
 tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    flush_tail(e);
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
@@ -951,6 +984,7 @@ tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_
 }
 
 tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
+    flush_tail(e);
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
@@ -1027,6 +1061,7 @@ tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes
 
 static bool sync_streams(tbc_engine *e) {
     hipSetDevice(e->device);
+    flush_tail(e);
     bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
     for (int t = 0; t < e->ntails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
     ok = ok && (!e->sort_stream || hipStreamSynchronize(e->sort_stream) == hipSuccess);
@@ -1054,6 +1089,7 @@ tbc_status tbc_synchronize(tbc_engine *e) {
 
 tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const uint64_t *lengths, uint32_t count,
                               uint8_t *checksums_out) {
+    flush_tail(e);
     if (!e || (count && (!messages || !lengths || !checksums_out))) return TBC_ERR_INVALID_ARGUMENT;
     if (!count) return TBC_OK;
     for (uint32_t i = 0; i < count; i++)
@@ -1090,6 +1126,7 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
 
 tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const uint64_t *expect_checksums,
                                const uint64_t *expect_addresses, uint32_t count, uint8_t *results_out) {
+    flush_tail(e);
     if (!e || (count && (!blocks || !expect_checksums || !expect_addresses || !results_out)))
         return TBC_ERR_INVALID_ARGUMENT;
     if (!count) return TBC_OK;
@@ -1226,6 +1263,7 @@ tbc_status tbc_sort_values_async(tbc_engine *e, const tbc_tree *tree, void *valu
 }
 
 tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, uint32_t count) {
+    flush_tail(e);
     tbc_status st = tbc_sort_values_async(e, tree, values, count);
     if (st != TBC_OK) return st;
     return tbc_synchronize(e);
@@ -1239,6 +1277,7 @@ struct KPairHost {
 
 tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams,
                                  uint32_t stream_count, uint32_t descending, void *out_values, tbc_kway **out) {
+    flush_tail(e);
     Layout L;
     if (!e || !tree || !out || (stream_count && !streams) || stream_count > TBC_KWAY_STREAMS_MAX ||
         !compute_layout(tree, e->block_size, &L) || ((uintptr_t)out_values & 15) ||
@@ -1522,6 +1561,80 @@ static bool tail_chains(tbc_engine *e, tbc_batch *b, hipStream_t T, const JobDes
               hipEventRecord(e->slot_ev[b->chain_slot], T) == hipSuccess;
     mark_cb(b, "chains");
     return ok;
+}
+
+// Grid batch, tail after its chains and index blocks: the input checks
+// (after every earlier tail: they read blocks earlier batches sealed), the
+// outputs marked trusted, the results, the done events.
+static bool grid_tail_rest(tbc_engine *e, tbc_batch *b, int ti) {
+    const auto &g = b->gt;
+    hipStream_t T = e->tail[ti];
+    bool ok = true;
+    for (int o = 0; ok && o < e->ntails; o++)
+        if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
+    if (ok && g.n_checks)
+        ok = launch_grid_expect(g.resolve, g.n_resolve, g.checks, T) == 0 &&
+             launch_grid_validate(g.checks, g.n_checks, g.grid->verified, g.half.jobs, g.half.njobs, g.half.res,
+                                  e->block_size, T) == 0 &&
+             launch_grid_checks(g.checks, g.n_checks, g.grid->verified, g.half.jobs, g.half.njobs, g.half.res,
+                                e->block_size, T) == 0;
+    // Outputs written by the engine are trusted like the reference's grid
+    // cache entries (grid.zig:802-841), once the job's inputs checked out.
+    if (ok) ok = launch_grid_mark(g.half.jobs, g.half.njobs, g.grid->verified, g.half.res, T) == 0;
+    mark_cb(b, "grid_check");
+    ok = ok && hipMemcpyAsync(b->h_results, g.half.res, g.copy_bytes, hipMemcpyDeviceToHost, T) == hipSuccess;
+    return ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+}
+
+static int take_tail(tbc_engine *e) {
+    const int ti = e->next_tail;
+    e->next_tail = (ti + 1) % e->ntails;
+    return ti;
+}
+
+// A grid batch's whole tail on the next tail stream, after its front.
+static bool grid_tail_alone(tbc_engine *e, tbc_batch *b) {
+    const auto &g = b->gt;
+    const int ti = take_tail(e);
+    hipStream_t T = e->tail[ti];
+    bool ok = hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
+    b->mark_stream = T;
+    mark_cb(b, "tail_wait");
+    if (ok && g.half.njobs)
+        ok = tail_chains(e, b, T, g.half.jobs, g.half.njobs, g.half.dblocks, g.half.tables, g.half.res, g.half.infos,
+                         g.status, g.block_tile, g.splits, g.half.ready, g.done_ctr, g.wide);
+    return ok && grid_tail_rest(e, b, ti);
+}
+
+// Tail pairing (round 5). A grid batch's chains take one AEGIS chain time
+// (~2 ms per 1 MiB block) however few blocks it has, and only the tail
+// streams (one per hardware queue beside the engine stream: three) run them
+// concurrently; config 1's batches have a few hundred blocks each, so three
+// tails held ~40 % of the CUs while the batches queued for a tail
+// (tail_wait 28 ms per step). A grid batch's tail therefore waits for the
+// next grid batch's front and both batches' chains run as ONE launch
+// (k_data_blocks_pair) on one tail: twice the chains in flight per tail.
+// Any other call launches a waiting tail alone first (flush_tail), so a
+// caller that waits for a batch before submitting the next never pairs.
+static bool grid_tail_pair(tbc_engine *e, tbc_batch *p, tbc_batch *b) {
+    const int ti = take_tail(e);
+    hipStream_t T = e->tail[ti];
+    bool ok = hipStreamWaitEvent(T, b->fork, 0) == hipSuccess; // after both fronts (engine stream order)
+    p->mark_stream = b->mark_stream = T;
+    mark_cb(p, "tail_wait");
+    mark_cb(b, "tail_wait_paired");
+    ok = ok && launch_blocks_tail_pair(p->gt.half, b->gt.half, T, mark_cb, p, b) == 0;
+    return ok && grid_tail_rest(e, p, ti) && grid_tail_rest(e, b, ti);
+}
+
+static void flush_tail(tbc_engine *e) {
+    tbc_batch *p = e ? e->deferred : nullptr;
+    if (!p) return;
+    e->deferred = nullptr;
+    if (!grid_tail_alone(e, p)) {
+        p->complete = true;
+        p->result = TBC_ERR_DEVICE;
+    }
 }
 
 static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, bool pipeline,
@@ -1937,30 +2050,36 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         }
         ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
                                   d_table_cnt, d_done);
-        const int ti = e->next_tail;
-        e->next_tail = (e->next_tail + 1) % e->ntails;
-        hipStream_t T = e->tail[ti];
         b->fork = take_event(e);
-        ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
-        b->mark_stream = T;
-        mark_cb(b, "tail_wait");
-        if (ok && count)
-            ok = tail_chains(e, b, T, (const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
-                             d_block_tile, d_splits, d_ready, d_done, wide_front);
-        for (int o = 0; ok && o < e->ntails; o++)
-            if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
-        if (ok && n_checks)
-            ok = launch_grid_expect(d_resolve, (uint32_t)resolve.size(), d_checks, T) == 0 &&
-                 launch_grid_validate(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in,
-                                      (int)count, d_res, e->block_size, T) == 0 &&
-                 launch_grid_checks(d_checks, (uint32_t)n_checks, grid0->verified, (const JobDesc *)d_in, (int)count,
-                                    d_res, e->block_size, T) == 0;
-        // Outputs written by the engine are trusted like the reference's grid
-        // cache entries (grid.zig:802-841), once the job's inputs checked out.
-        if (ok) ok = launch_grid_mark((const JobDesc *)d_in, (int)count, grid0->verified, d_res, T) == 0;
-        mark_cb(b, "grid_check");
-        ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
-        ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
+        ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess;
+        auto &g = b->gt;
+        g.half = TailHalf{(const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_ready};
+        g.status = d_status;
+        g.block_tile = d_block_tile;
+        g.splits = d_splits;
+        g.done_ctr = d_done;
+        g.wide = wide_front;
+        g.resolve = d_resolve;
+        g.n_resolve = (uint32_t)resolve.size();
+        g.n_checks = (uint32_t)n_checks;
+        g.checks = d_checks;
+        g.grid = grid0;
+        g.copy_bytes = sz_res + sz_infos;
+        const bool pairable = e->pair_tails && !e->server && count && dblocks;
+        if (ok && pairable && e->deferred) {
+            tbc_batch *p = e->deferred;
+            e->deferred = nullptr;
+            if (!grid_tail_pair(e, p, b)) {
+                p->complete = true;
+                p->result = TBC_ERR_DEVICE;
+                ok = false;
+            }
+        } else if (ok && pairable) {
+            e->deferred = b;
+        } else if (ok) {
+            flush_tail(e);
+            ok = grid_tail_alone(e, b);
+        }
     } else if (pipeline) {
         // A group of a split batch: front (merge + bodies) on the engine
         // stream, chains and index blocks on a tail stream, so the group's
@@ -2144,6 +2263,9 @@ static tbc_status check_plain_job(const tbc_engine *e, const tbc_compaction &c, 
 
 tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, tbc_batch **out) {
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
+    // A grid batch may pair with a deferred grid tail; anything else
+    // launches it first.
+    if (!count || !(jobs_in[0].flags & TBC_COMPACTION_GRID)) flush_tail(e);
     // A batch with caller-provided output blocks may write blocks an earlier
     // batch's tail (its chains) still reads, when the caller reuses them
     // while that batch is in flight: its fronts then start after that tail.
@@ -2229,6 +2351,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
 }
 
 tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **out) {
+    flush_tail(e);
     if (!e || !sl || !out) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     Layout L;
@@ -2351,6 +2474,7 @@ static tbc_status parent_finish(tbc_batch *b, bool wait) {
 }
 
 tbc_status tbc_batch_poll(tbc_batch *b) {
+    flush_tail(b ? b->engine : nullptr);
     if (!b) return TBC_ERR_INVALID_ARGUMENT;
     if (b->complete) return b->result;
     if (!b->children.empty()) return parent_finish(b, false);
@@ -2367,6 +2491,7 @@ tbc_status tbc_batch_poll(tbc_batch *b) {
 }
 
 tbc_status tbc_batch_wait(tbc_batch *b) {
+    flush_tail(b ? b->engine : nullptr);
     if (!b) return TBC_ERR_INVALID_ARGUMENT;
     if (b->complete) return b->result;
     if (!b->children.empty()) return parent_finish(b, true);
@@ -2476,6 +2601,7 @@ tbc_status tbc_batch_kernel_times(tbc_batch *b, const char **names, double *us, 
 }
 
 void tbc_batch_release(tbc_batch *b) {
+    flush_tail(b ? b->engine : nullptr);
     if (!b) return;
     if (!b->children.empty()) { // reverse order: the groups' arena regions are a stack
         for (auto it = b->children.rbegin(); it != b->children.rend(); ++it) tbc_batch_release(*it);

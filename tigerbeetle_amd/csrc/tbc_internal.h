@@ -386,6 +386,26 @@ int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, 
                         uint32_t *d_ready, const JobResultDev *d_results, const uint64_t *d_status,
                         const uint64_t *d_masks, const SplitDesc *d_splits, void *stream,
                         void (*mark)(void *, const char *), void *mark_ctx, bool bodies_done);
+// Tail pairing (engine.hip grid_tail_pair): one batch's half of a paired
+// tail launch.
+struct TailHalf {
+    const JobDesc *jobs;
+    int njobs;
+    uint32_t dblocks, tables;
+    JobResultDev *res;
+    uint8_t *infos;
+    const uint32_t *ready;
+};
+struct ChainHalf { // k_data_blocks_pair's kernel argument
+    const JobDesc *jobs;
+    int njobs;
+    uint32_t total;
+    const JobResultDev *res;
+    const uint32_t *ready;
+    uint32_t c, wgs; // chain waves per workgroup, workgroups
+};
+int launch_blocks_tail_pair(const TailHalf &a, const TailHalf &b, void *stream, void (*mark)(void *, const char *),
+                            void *ctx_a, void *ctx_b);
 int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
                        JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,

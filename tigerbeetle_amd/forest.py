@@ -607,6 +607,7 @@ class GridExecutor:
         # re-executed with its inputs resident in HBM (bench.py --config 1).
         self.recording = record
         self.record: list = []
+        self.frozen: dict = {}  # recording: name -> (device copy, count) of an unsorted immutable table
         self.archive: list = []
         self.puts_bytes = 0
 
@@ -630,6 +631,22 @@ class GridExecutor:
         for name in list(self.mutable):
             self.mutable[name], self.immutable[name] = self.immutable[name], self.mutable[name]
             self.mutable[name].reset()
+        # Recording: an immutable table that needs no sort (its puts arrived
+        # in key order) is compacted from a copy of its own, so that a replay
+        # of the record reads this bar's values rather than whatever the
+        # memtable buffer holds by then (a sorted table is re-landed before
+        # its sort instead, below).
+        self.frozen = {}
+        if self.recording:
+            for name, mt in self.immutable.items():
+                ptr, n = mt.values()
+                if name in names or n == 0:
+                    continue
+                nbytes = n * trees.BY_NAME[name].value_size
+                copy = self.engine.alloc(nbytes)
+                self.engine.copy_device_async(copy.ptr, ptr, nbytes)
+                self.archive.append(copy)
+                self.frozen[name] = (copy.ptr, n)
         jobs = []
         for name in names:
             ptr, n = self.immutable[name].values()
@@ -659,6 +676,7 @@ class GridExecutor:
         for name in list(self.mutable):
             self.mutable[name].reset()
             self.immutable[name].reset()
+        self.frozen = {}
         self.grid.invalidate()
         if self.recording:
             self.record.append(("restart",))
@@ -669,7 +687,7 @@ class GridExecutor:
         js = []
         for name, c in jobs:
             if c.table_a is None:
-                ptr, n = self.immutable[name].values()
+                ptr, n = self.frozen.get(name) or self.immutable[name].values()
                 segs_a, tables_a = [(ptr, n)], []
             else:
                 segs_a, tables_a = [], [c.table_a.ref()]
