@@ -8,8 +8,9 @@ and cut into 8 full level-B tables. IdTreeValue{id, timestamp, padding = 0},
 no tombstones, drop_tombstones = false, usage general. 66,044,160 values x
 32 B = 2.11 GB of input per GPU, resident in HBM (as 1 MiB grid blocks)
 before timing. `--config 3|4|5` run BASELINE configs[2] / [3] / [4]
-(tigerbeetle_amd/configs.py); config 3's step includes landing each unsorted
-memtable (a D2D copy) and sorting all of them (tbc_sort_values_batch).
+(tigerbeetle_amd/configs.py); configs 3 and 4 include sorting each unsorted
+memtable from the table as put into its memtable array (tbc_sort_values_batch,
+out of place, as tbc_memtable_make_immutable does at a bar end).
 
 A step = one batch of all the GPU's compactions (merge, data blocks with
 AEGIS-128L checksums, index blocks, TableInfos) through the C ABI. Multi-GPU:
@@ -44,14 +45,14 @@ def blocks_of(table: np.ndarray, vcm: int) -> list:
 
 class Workload:
     """All jobs of one GPU staged in HBM: disk tables as 1 MiB grid blocks,
-    memtables as one contiguous array (plus the unsorted copy they are
-    re-landed from each step when the config sorts them)."""
+    memtables as one contiguous array (plus, when the config sorts them, the
+    table as put, sorted out of place into the memtable array each step)."""
 
     def __init__(self, eng: Engine, config: int, job_ids: list, bs: int, keep_host: bool = True):
         self.config = config
         self.bs = bs
         self.jobs, self.bufs, self.specs = [], [], []
-        self.sorts, self.landings = [], []
+        self.sorts = []
         self.input_values = 0
         self.input_bytes = 0
         self.sort_bytes = 0
@@ -71,11 +72,10 @@ class Workload:
                 segs_a = [(abuf.ptr, len(js.a))] if abuf else []
                 if abuf:
                     self.bufs.append(abuf)
-                if js.a_unsorted:
+                if js.a_unsorted:  # sorted each step from the table as put into the immutable buffer
                     pristine = eng.upload(js.a)
                     self.bufs.append(pristine)
-                    self.landings.append((abuf.ptr, pristine.ptr, js.a.nbytes))
-                    self.sorts.append((spec, abuf.ptr, len(js.a)))
+                    self.sorts.append((spec, pristine.ptr, len(js.a), abuf.ptr))
                     self.sort_bytes += 2 * js.a.nbytes
                 tables = []
             else:
@@ -138,11 +138,9 @@ class Workload:
         return 1 + len(self.job_sets)
 
     def submit(self, eng: Engine):
-        """Land + sort the bar's memtables (config 3), then submit the
+        """Sort the bar's memtables (configs 3 and 4), then submit the
         compaction batch (no wait). With rotate(), steps take the output
         sets in turn."""
-        if self.landings:
-            eng.copy_device_batch(self.landings)
         if self.sorts:
             eng.sort_values_batch(self.sorts)
         sets = [self.jobs] + self.job_sets
@@ -261,10 +259,8 @@ class ReplayWorkload:
         host = self.host_s
         for kind, *rest in self.executor.record:
             t = time.perf_counter()
-            if kind == "sort":
-                jobs, landings = rest
-                eng.copy_device_batch(landings)
-                eng.sort_values_batch(jobs)
+            if kind == "sort":  # from the put-order copy straight into the immutable buffer
+                eng.sort_values_batch(rest[0])
             elif kind == "checkpoint":  # the replica checkpoints with no grid IO in flight
                 eng.synchronize()
             elif kind == "restart":

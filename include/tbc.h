@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TBC_ABI_VERSION 4u
+#define TBC_ABI_VERSION 5u
 
 typedef enum tbc_status {
     TBC_OK = 0,
@@ -311,6 +311,19 @@ tbc_status tbc_memtable_put(tbc_memtable *memtable, const void *values, uint32_t
 tbc_status tbc_memtable_values(const tbc_memtable *memtable, void **out_values, uint32_t *out_count);
 /* make_mutable: empty the table (after its immutable compaction flushed it). */
 tbc_status tbc_memtable_reset(tbc_memtable *memtable);
+/* Bar end of a forest (Tree.swap_mutable_and_immutable + TableMemory.make_immutable,
+ * tree.zig:979-999, table_memory.zig:110-154), for every pair at once: the
+ * values put into mutables[i] become immutables[i]'s, in key order, and
+ * mutables[i] is emptied. immutables[i] must be empty (flushed, then
+ * tbc_memtable_reset) and of the same tree and capacity. A table whose puts
+ * arrived in key order (in_order[i] != 0, the reference's sorted flag,
+ * table_memory.zig:83-87; in_order may be NULL) trades buffers with its
+ * immutable table; the others are sorted by ONE segmented out-of-place sort
+ * (tbc_sort_job.values_out) from the mutable buffers into the immutable
+ * ones. Enqueued on the engine stream; later puts into the mutable tables
+ * are ordered after the sort's reads. */
+tbc_status tbc_memtable_make_immutable(tbc_engine *engine, tbc_memtable *const *mutables,
+                                       tbc_memtable *const *immutables, const uint8_t *in_order, uint32_t count);
 
 /* ---- registered host memory ------------------------------------------------
  * hipHostRegister of a caller range (TigerBeetle's I/O buffers are allocated
@@ -389,6 +402,12 @@ typedef struct tbc_sort_job {
     void *values;   /* device pointer, 16-byte aligned */
     uint32_t count;
     uint32_t reserved;
+    /* NULL: sorted in place. Otherwise the sorted values are written here
+     * (device, 16-byte aligned, count * value_size bytes, not overlapping
+     * `values`) and `values` is only read: the put-order values are read
+     * once and written once, with no copy of the table (a table already in
+     * order is copied as is). */
+    void *values_out;
 } tbc_sort_job;
 tbc_status tbc_sort_values_batch(tbc_engine *engine, const tbc_sort_job *jobs, uint32_t count);
 

@@ -24,7 +24,7 @@ def test_abi_version_and_struct_layout_match_c():
         "tbc_tree": (abi.Tree, ["tree_id", "key_kind", "usage", "value_size", "timestamp_offset",
                                 "table_value_count_max"]),
         "tbc_segment": (abi.Segment, ["values", "count"]),
-        "tbc_sort_job": (abi.SortJob, ["tree", "values", "count"]),
+        "tbc_sort_job": (abi.SortJob, ["tree", "values", "count", "values_out"]),
         "tbc_config": (abi.Config, ["device", "block_size", "arena_bytes", "flags"]),
         "tbc_compaction": (abi.Compaction, [f for f, _ in abi.Compaction._fields_ if not f.startswith("reserved")]),
         "tbc_compaction_result": (abi.CompactionResult, [f for f, _ in abi.CompactionResult._fields_]),

@@ -8,7 +8,9 @@ changes; each of those tests compares with the oracle.
                                            highest stream priority
   TBC_GRID_SPECULATION=1                   grid batches merge UNIQUE_KEYS jobs
                                            tile by tile, recompute in front
-  TBC_TAILS=2, TBC_DEBUG_SYNC=1            two tails; stage-by-stage waits
+  TBC_TAILS=2                              two tail streams
+  TBC_DEBUG_SYNC=1                         stage-by-stage waits (nothing pipelines)
+  TBC_PAIR_TAILS=0                         grid tails never paired (test_gpu_pairing.py)
   TBC_CHAIN_SERVER=1                       the chain server (round 5, opt-in):
                                            every batch's chains claimed by one
                                            server on its own stream
@@ -67,8 +69,17 @@ def test_grid_speculation_bit_exact():
 
 
 @pytest.mark.gpu
-def test_two_tails_debug_sync_bit_exact():
-    _child({"TBC_TAILS": "2", "TBC_DEBUG_SYNC": "1"}, FILES, PIPELINED)
+def test_two_tails_bit_exact():
+    _child({"TBC_TAILS": "2"}, FILES, PIPELINED)
+
+
+@pytest.mark.gpu
+def test_debug_sync_bit_exact():
+    """TBC_DEBUG_SYNC=1 waits for every stage, so nothing pipelines: the
+    parity tests that do not require it."""
+    _child({"TBC_DEBUG_SYNC": "1"}, FILES, " or ".join([
+        "test_compaction_parity_throughput_regime", "test_immutable_compaction_after_device_sort",
+        "test_two_half_bars_chained_through_the_grid", "test_values_only_bodies_equal_full_compaction"]))
 
 
 @pytest.mark.gpu

@@ -11,7 +11,7 @@ import pytest
 
 import zig_prng
 from helpers import disk_image, gpu_run, run_oracle
-from tigerbeetle_amd import trees, workloads
+from tigerbeetle_amd import abi, trees, workloads
 
 pytestmark = pytest.mark.gpu
 
@@ -350,6 +350,90 @@ def test_sort_values_batch_of_memtables(engine, oracle_lib):
     for (spec, buf, n), want in zip(tables, wants):
         got = buf.download(n * spec.value_size).reshape(n, spec.value_size)
         assert np.array_equal(got, want), spec.name
+
+
+def _bar_end_tables(oracle_lib, rng):
+    """Tables of many trees (unsorted, in order, tiny, empty) and the oracle's
+    stable sort of each."""
+    names = ["transfers.debit_account_id", "transfers.timestamp", "accounts.ledger", "transfers.id",
+             "posted.timestamp", "account_history.timestamp", "transfers.credit_account_id", "accounts.user_data_64"]
+    sizes = [40_000, 9_000, 2049, 2048, 1, 3000, 0, 70_001]
+    out = []
+    for name, n in zip(names, sizes):
+        spec = trees.BY_NAME[name]
+        limbs = workloads.random_keys(spec, max(n, 1), rng, field_max=50)
+        limbs[0] = rng.integers(1, 3000, size=max(n, 1), dtype=np.uint64)
+        vals = workloads.values_from_keys(spec, limbs, rng.random(max(n, 1)) < 0.1, rng)[:n]
+        if name == "transfers.timestamp":  # in key order
+            vals = vals[np.argsort(workloads.keys_of(vals, spec)[0], kind="stable")]
+        t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                            spec.value_count_max, 1 << 20)
+        out.append((spec, vals, oracle_lib.sort_values(t, vals) if n else vals))
+    return out
+
+
+def test_sort_values_batch_out_of_place(engine, oracle_lib):
+    """tbc_sort_job.values_out: every table sorted into its own output,
+    bit-exact vs the oracle's stable sort (a table in order copied as is, a
+    one-value table copied), the input left as put; an output overlapping its
+    input is refused."""
+    cases = _bar_end_tables(oracle_lib, np.random.default_rng(15))
+    jobs, keep = [], []
+    for spec, vals, want in cases:
+        src = engine.upload(vals, pad=16)
+        dst = engine.upload(np.full((max(len(vals), 1), spec.value_size), 0xEE, dtype=np.uint8), pad=16)
+        keep.append((spec, vals, want, src, dst))
+        jobs.append((spec, src, len(vals), dst.ptr))
+    engine.sort_values_batch(jobs)
+    engine.synchronize()
+    for spec, vals, want, src, dst in keep:
+        n = len(vals)
+        assert np.array_equal(dst.download(n * spec.value_size).reshape(n, spec.value_size), want), spec.name
+        assert np.array_equal(src.download(n * spec.value_size).reshape(n, spec.value_size), vals), spec.name
+    spec, _, _, src, _ = keep[0]
+    with pytest.raises(abi.TbcError):
+        engine.sort_values_batch([(spec, src, 100, src.ptr + 16 * spec.value_size)])
+
+
+def test_memtable_make_immutable(engine, oracle_lib):
+    """tbc_memtable_make_immutable at a bar end: each mutable table's values
+    become its immutable table's in key order (sorted out of place, or the
+    buffers traded for a table put in order), the mutable tables empty and
+    ready for the next bar's puts; a non-empty immutable table is refused."""
+    from tigerbeetle_amd import Memtable
+    cases = [c for c in _bar_end_tables(oracle_lib, np.random.default_rng(16)) if len(c[1])]
+    pairs = []
+    for spec, vals, want in cases:
+        m, im = Memtable(engine, spec, capacity=len(vals) + 8), Memtable(engine, spec, capacity=len(vals) + 8)
+        m.put(vals)
+        pairs.append((m, im, spec.name == "transfers.timestamp"))
+    Memtable.make_immutable(engine, pairs)
+    for (spec, vals, want), (m, im, _) in zip(cases, pairs):
+        ptr, n = im.values()
+        assert n == len(vals) and m.values()[1] == 0
+        got = np.zeros((n, spec.value_size), dtype=np.uint8)
+        engine.synchronize()
+        abi.check(abi.lib().tbc_copy_to_host(engine.handle, got.ctypes.data, ptr, got.nbytes), "copy")
+        assert np.array_equal(got, want), spec.name
+    # The next bar: puts into the emptied mutable tables, then its bar end
+    # after the immutable tables were flushed (reset).
+    spec, vals, want = cases[0]
+    m, im, _ = pairs[0]
+    m.put(vals[::-1].copy())
+    with pytest.raises(abi.TbcError):  # the immutable table still holds the previous bar
+        Memtable.make_immutable(engine, [(m, im, False)])
+    im.reset()
+    Memtable.make_immutable(engine, [(m, im, False)])
+    ptr, n = im.values()
+    got = np.zeros((n, spec.value_size), dtype=np.uint8)
+    engine.synchronize()
+    abi.check(abi.lib().tbc_copy_to_host(engine.handle, got.ctypes.data, ptr, got.nbytes), "copy")
+    t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                        spec.value_count_max, 1 << 20)
+    assert np.array_equal(got, oracle_lib.sort_values(t, vals[::-1].copy()))
+    for m, im, _ in pairs:
+        m.close()
+        im.close()
 
 
 def test_compaction_parity_throughput_regime(engine_small, oracle_lib):

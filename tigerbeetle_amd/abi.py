@@ -37,7 +37,7 @@ COMPACTION_GRID = 2
 COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped
 COMPACTION_COUNT_ONLY = 8  # the merge alone: survivor counts (phase A of a split job)
 SPECULATION_NONE, SPECULATION_HELD, SPECULATION_BROKEN = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class TbcError(RuntimeError):
@@ -86,7 +86,7 @@ class Segment(ctypes.Structure):
 
 class SortJob(ctypes.Structure):
     _fields_ = [("tree", Tree), ("values", ctypes.c_void_p), ("count", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("reserved", ctypes.c_uint32), ("values_out", ctypes.c_void_p)]
 
 
 class Copy(ctypes.Structure):
@@ -211,6 +211,7 @@ _SIGNATURES = {
     "tbc_memtable_put": (ctypes.c_int, [_P, _P, ctypes.c_uint32]),
     "tbc_memtable_values": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint32)]),
     "tbc_memtable_reset": (ctypes.c_int, [_P]),
+    "tbc_memtable_make_immutable": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, ctypes.c_uint32]),
 }
 
 _lib = None

@@ -250,6 +250,20 @@ struct tbc_memtable {
     uint32_t capacity = 0, count = 0;
 };
 
+// hipEventQuery / hipStreamQuery answer "not ready" through the runtime's
+// last-error slot, where a later `hipGetLastError() != hipSuccess` check
+// after a kernel launch would take it for a launch failure: consume it.
+static hipError_t event_query(hipEvent_t ev) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipErrorNotReady) (void)hipGetLastError();
+    return q;
+}
+static hipError_t stream_query(hipStream_t s) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipErrorNotReady) (void)hipGetLastError();
+    return q;
+}
+
 static hipEvent_t take_event(tbc_engine *e) {
     if (e->event_pool.empty()) {
         hipEvent_t ev;
@@ -455,7 +469,7 @@ static void debug_stage(hipStream_t s, const char *name) {
     static const bool on = getenv("TBC_DEBUG_SYNC") != nullptr;
     if (!on) return;
     for (int i = 0; i < 5000; i++) {
-        const hipError_t q = hipStreamQuery(s);
+        const hipError_t q = stream_query(s);
         if (q == hipSuccess) {
             fprintf(stderr, "tbc debug: stage %s done\n", name);
             return;
@@ -483,7 +497,7 @@ static void mark_cb(void *ctx, const char *name) {
 static void retire_sorts(tbc_engine *e) {
     auto &ps = e->pending_sorts;
     for (size_t i = 0; i < ps.size();) {
-        if (hipEventQuery(ps[i].done) == hipSuccess) {
+        if (event_query(ps[i].done) == hipSuccess) {
             e->event_pool.push_back(ps[i].done);
             ps.erase(ps.begin() + (long)i);
         } else {
@@ -514,6 +528,7 @@ static bool join_sorts(tbc_engine *e) {
 // Every stream of the engine drained (internal: no deferred-error report).
 static bool sync_streams(tbc_engine *e);
 static void flush_tail(tbc_engine *e);
+static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count);
 
 // Later work on the engine stream that touches grid blocks (staging blocks in
 // or out, synchronous checks) waits for every batch tail enqueued so far.
@@ -737,6 +752,7 @@ tbc_status tbc_grid_block_pointer(const tbc_grid *g, uint64_t address, void **ou
 }
 
 tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *blocks, uint32_t count) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
@@ -776,6 +792,7 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
 }
 
 tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *const *blocks, uint32_t count) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
@@ -791,6 +808,7 @@ tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *con
 
 tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *host_images,
                                      uint32_t count, uint64_t previous_address, const uint64_t *previous_checksum) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !host_images))) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
@@ -817,7 +835,13 @@ tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, con
     }
     if (!count) return TBC_OK;
     hipSetDevice(e->device);
-    if (!join_tails(e)) return TBC_ERR_DEVICE;
+    // No wait for the tails still running (round 4 joined them, stalling the
+    // engine stream for up to a chain time per close): a manifest block's
+    // address comes from the log's own reservation, so no running tail
+    // writes it or reads it (a released address is reused only after the
+    // next checkpoint, and the replica checkpoints with no grid IO in
+    // flight); the chain reads only the previous manifest block, closed
+    // earlier on this stream; the verified bytes it sets are its own blocks'.
     // Addresses and the previous checksum go through a pinned staging slot
     // (reusable once the stream has passed this close), the images through
     // the staging ring into their grid slots.
@@ -893,6 +917,7 @@ void tbc_memtable_deinit(tbc_memtable *m) {
 }
 
 tbc_status tbc_memtable_put(tbc_memtable *m, const void *values, uint32_t count) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     if (!m || (count && !values)) return TBC_ERR_INVALID_ARGUMENT;
     if ((uint64_t)m->count + count > m->capacity) return TBC_ERR_CAPACITY; // table_memory.zig:80
     if (!count) return TBC_OK;
@@ -915,6 +940,39 @@ tbc_status tbc_memtable_values(const tbc_memtable *m, void **out_values, uint32_
 tbc_status tbc_memtable_reset(tbc_memtable *m) {
     if (!m) return TBC_ERR_INVALID_ARGUMENT;
     m->count = 0;
+    return TBC_OK;
+}
+
+tbc_status tbc_memtable_make_immutable(tbc_engine *e, tbc_memtable *const *mutables, tbc_memtable *const *immutables,
+                                       const uint8_t *in_order, uint32_t count) {
+    if (!e || (count && (!mutables || !immutables))) return TBC_ERR_INVALID_ARGUMENT;
+    std::vector<tbc_sort_job> jobs;
+    for (uint32_t i = 0; i < count; i++) {
+        const tbc_memtable *m = mutables[i], *im = immutables[i];
+        if (!m || !im || m == im || m->engine != e || im->engine != e || im->count ||
+            m->capacity != im->capacity || memcmp(&m->tree, &im->tree, sizeof m->tree))
+            return TBC_ERR_INVALID_ARGUMENT;
+    }
+    auto sorted = [&](uint32_t i) { return mutables[i]->count && !(in_order && in_order[i]); };
+    for (uint32_t i = 0; i < count; i++) {
+        if (!sorted(i)) continue;
+        tbc_sort_job j{};
+        j.tree = mutables[i]->tree;
+        j.values = mutables[i]->values;
+        j.count = mutables[i]->count;
+        j.values_out = immutables[i]->values;
+        jobs.push_back(j);
+    }
+    if (!jobs.empty()) {
+        const tbc_status st = sort_batch(e, jobs.data(), (uint32_t)jobs.size());
+        if (st != TBC_OK) return st;
+    }
+    for (uint32_t i = 0; i < count; i++) {
+        tbc_memtable *m = mutables[i], *im = immutables[i];
+        if (!sorted(i)) std::swap(m->values, im->values); // in key order (or empty): the buffer changes hands
+        im->count = m->count;
+        m->count = 0;
+    }
     return TBC_OK;
 }
 
@@ -967,7 +1025,6 @@ tbc_status tbc_device_alloc(tbc_engine *e, uint64_t bytes, void **out_ptr) {
 }
 
 tbc_status tbc_device_free(tbc_engine *e, void *ptr) {
-    flush_tail(e);
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     return hipFree(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
@@ -1002,6 +1059,7 @@ tbc_status tbc_copy_device_async(tbc_engine *e, void *dst, const void *src, uint
 }
 
 tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t count) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     if (!e || (count && !copies)) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
         if (copies[i].bytes && (!copies[i].dst || !copies[i].src)) return TBC_ERR_INVALID_ARGUMENT;
@@ -1089,6 +1147,7 @@ tbc_status tbc_synchronize(tbc_engine *e) {
 
 tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const uint64_t *lengths, uint32_t count,
                               uint8_t *checksums_out) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(e);
     if (!e || (count && (!messages || !lengths || !checksums_out))) return TBC_ERR_INVALID_ARGUMENT;
     if (!count) return TBC_OK;
@@ -1126,6 +1185,7 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
 
 tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const uint64_t *expect_checksums,
                                const uint64_t *expect_addresses, uint32_t count, uint8_t *results_out) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(e);
     if (!e || (count && (!blocks || !expect_checksums || !expect_addresses || !results_out)))
         return TBC_ERR_INVALID_ARGUMENT;
@@ -1164,14 +1224,21 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
 }
 
 static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     if (!e || (count && !jobs)) return TBC_ERR_INVALID_ARGUMENT;
     std::vector<SortItem> items(count);
     for (uint32_t k = 0; k < count; k++) {
         const tbc_sort_job &j = jobs[k];
         Layout L;
-        if (!compute_layout(&j.tree, e->block_size, &L) || (j.count && !j.values) || ((uintptr_t)j.values & 15))
+        if (!compute_layout(&j.tree, e->block_size, &L) || (j.count && !j.values) || ((uintptr_t)j.values & 15) ||
+            ((uintptr_t)j.values_out & 15))
             return TBC_ERR_INVALID_ARGUMENT;
-        items[k] = SortItem{j.values, j.count, j.tree.value_size, j.tree.timestamp_offset, j.tree.key_kind};
+        const uint64_t nb = (uint64_t)j.count * j.tree.value_size;
+        if (j.values_out && j.count && (uint8_t *)j.values_out < (uint8_t *)j.values + nb &&
+            (uint8_t *)j.values < (uint8_t *)j.values_out + nb)
+            return TBC_ERR_INVALID_ARGUMENT; // overlapping out of place
+        items[k] = SortItem{j.values, j.count, j.tree.value_size, j.tree.timestamp_offset, j.tree.key_kind,
+                            j.values_out};
     }
     hipSetDevice(e->device);
     // The bar-end sort runs on the engine stream. A sort stream of its own
@@ -1232,14 +1299,21 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, e->sort_status,
                                e->sort_status_words, &e->sort_epoch, host, ss);
     if (hipEventRecord(slot_ev, ss) != hipSuccess) rc = -1;
+    if (rc) {
+        const hipError_t err = hipGetLastError();
+        fprintf(stderr, "tbc: bar-end sort of %u tables not enqueued (step %d): %s (%d)\n", count, rc,
+                hipGetErrorString(err), (int)err);
+    }
     (small ? e->desc.used[slot] : e->staging.used[slot]) = true;
     if (ss != e->stream && rc == 0) {
         tbc_engine::PendingSort ps;
         ps.done = take_event(e);
         for (uint32_t k = 0; k < count; k++)
             if (jobs[k].count)
-                ps.ranges.push_back({(uint64_t)(uintptr_t)jobs[k].values,
-                                     (uint64_t)(uintptr_t)jobs[k].values + (uint64_t)jobs[k].count * jobs[k].tree.value_size});
+                for (const void *p : {(const void *)jobs[k].values, (const void *)jobs[k].values_out})
+                    if (p) // read (and written in place), or written
+                        ps.ranges.push_back({(uint64_t)(uintptr_t)p,
+                                             (uint64_t)(uintptr_t)p + (uint64_t)jobs[k].count * jobs[k].tree.value_size});
         if (!ps.done || hipEventRecord(ps.done, ss) != hipSuccess || hipEventRecord(e->sort_last, ss) != hipSuccess)
             rc = -1;
         else
@@ -1277,6 +1351,7 @@ struct KPairHost {
 
 tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams,
                                  uint32_t stream_count, uint32_t descending, void *out_values, tbc_kway **out) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(e);
     Layout L;
     if (!e || !tree || !out || (stream_count && !streams) || stream_count > TBC_KWAY_STREAMS_MAX ||
@@ -1457,7 +1532,7 @@ tbc_status tbc_kway_poll(tbc_kway *k) {
     if (!k) return TBC_ERR_INVALID_ARGUMENT;
     if (k->complete) return k->result;
     hipSetDevice(k->engine->device);
-    const hipError_t q = hipEventQuery(k->done);
+    const hipError_t q = event_query(k->done);
     if (q == hipErrorNotReady) return TBC_PENDING;
     if (q != hipSuccess) fprintf(stderr, "tbc: k-way merge failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
     k->complete = true;
@@ -1521,7 +1596,7 @@ static bool publish_chains(tbc_engine *e, tbc_batch *b, const JobDesc *d_jobs, i
     if (!e->server || !dblocks) return true;
     if (dblocks > kChainMaxTasks) return false;
     auto &f = e->slot_fifo;
-    while (!f.empty() && hipEventQuery(e->slot_ev[f.front()]) == hipSuccess) f.erase(f.begin());
+    while (!f.empty() && event_query(e->slot_ev[f.front()]) == hipSuccess) f.erase(f.begin());
     while (f.size() >= kChainSlots) {
         if (hipEventSynchronize(e->slot_ev[f.front()]) != hipSuccess) return false;
         f.erase(f.begin());
@@ -1639,6 +1714,7 @@ static void flush_tail(tbc_engine *e) {
 
 static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, bool pipeline,
                               tbc_batch **out) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     hipSetDevice(e->device);
@@ -2275,7 +2351,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
         hipSetDevice(e->device);
         auto &pend = e->tail_out;
         for (size_t k = 0; k < pend.size();) {
-            if (hipEventQuery(pend[k].done) == hipSuccess) { // that tail is done with its outputs
+            if (event_query(pend[k].done) == hipSuccess) { // that tail is done with its outputs
                 e->event_pool.push_back(pend[k].done);
                 pend.erase(pend.begin() + (long)k);
                 continue;
@@ -2351,6 +2427,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
 }
 
 tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **out) {
+    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
     flush_tail(e);
     if (!e || !sl || !out) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
@@ -2479,7 +2556,7 @@ tbc_status tbc_batch_poll(tbc_batch *b) {
     if (b->complete) return b->result;
     if (!b->children.empty()) return parent_finish(b, false);
     hipSetDevice(b->engine->device);
-    hipError_t q = hipEventQuery(b->done);
+    hipError_t q = event_query(b->done);
     if (q == hipErrorNotReady) return TBC_PENDING;
     if (q != hipSuccess) {
         fprintf(stderr, "tbc: batch failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
@@ -2502,7 +2579,7 @@ tbc_status tbc_batch_wait(tbc_batch *b) {
     // (20 us sleeps), so a long batch does not hold a host core.
     hipError_t q;
     const auto t0 = std::chrono::steady_clock::now();
-    while ((q = hipEventQuery(b->done)) == hipErrorNotReady) {
+    while ((q = event_query(b->done)) == hipErrorNotReady) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
             const timespec ts{0, 20000};
             nanosleep(&ts, nullptr);

@@ -224,7 +224,10 @@ int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream)
     hipLaunchKernelGGL(k_upload, dim3((uint32_t)(blocks < 512 ? (blocks ? blocks : 1) : 512)), dim3(256), 0, s,
                        (uint64_t *)dst, (const uint64_t *)host_src, n8, (uint8_t *)dst + 8 * n8,
                        (const uint8_t *)host_src + 8 * n8, tail);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) fprintf(stderr, "tbc: upload of %llu bytes: %s (%d)\n", (unsigned long long)bytes,
+                                   hipGetErrorString(err), (int)err);
+    return err == hipSuccess ? 0 : -1;
 }
 
 } // namespace tbc

@@ -61,6 +61,7 @@ __device__ __forceinline__ const uint8_t *elem_ptr(const Stream &s, uint32_t seg
 // --------------------------------------------------------------------------
 // All key kinds of a batch in ONE launch (the split's job picks the key
 // loader): a batch mixing trees paid one latency-bound launch per kind.
+// One thread per split: a binary search (~21 dependent probes).
 template <int KIND>
 __device__ __forceinline__ uint32_t merge_path_split(const JobDesc &j, uint32_t d) {
     const uint32_t na = j.a.n, nb = j.b.n;
@@ -78,39 +79,7 @@ __device__ __forceinline__ uint32_t merge_path_split(const JobDesc &j, uint32_t 
     return lo;
 }
 
-__global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int njobs, uint32_t nsplits,
-                                                       SplitDesc *splits, const JobResultDev *res, uint32_t phase) {
-    const uint32_t gsplit = blockIdx.x * 256 + threadIdx.x;
-    if (gsplit >= nsplits) return;
-    const int ji = find_job(jobs, njobs, gsplit, [](const JobDesc &d) { return d.split_base; });
-    const JobDesc &j = jobs[ji];
-    if (phase_skips(j, res, phase)) return;
-    const uint32_t t = gsplit - j.split_base;
-    const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
-    const uint32_t d = (uint64_t)t * j.merge_tile < n ? t * j.merge_tile : n;
-    uint32_t lo;
-    switch (j.key_kind) {
-    case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
-    case kKeyIdU128: lo = merge_path_split<kKeyIdU128>(j, d); break;
-    case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
-    default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
-    }
-    SplitDesc s;
-    s.i = lo;
-    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
-    const uint32_t jb = d - lo;
-    s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
-    s.pad = 0;
-    splits[gsplit] = s;
-}
-
-// Speculated jobs (TBC_COMPACTION_UNIQUE_KEYS): with every value surviving,
-// data block k holds merged positions [k * vcm, (k + 1) * vcm); its producer
-// starts from the merge-path split at k * vcm. The thread of block 0 also
-// writes the job's speculative results (write_blocks' shape for n values,
-// compaction.zig:806-850); a broken speculation has them rewritten by the
-// recomputation's k_tile_scan.
-// One wave per block: a 64-ary merge-path search (each round, the 64 lanes
+// One wave per split: a 64-ary merge-path search (each round, the 64 lanes
 // probe 64 evenly spaced candidates and a ballot keeps the interval between
 // the last true and the first false), 4 dependent rounds for 2^24 values
 // instead of ~24 single-lane probes.
@@ -140,6 +109,58 @@ __device__ __forceinline__ uint32_t merge_path_split_wave(const JobDesc &j, uint
     return lo;
 }
 
+// A batch with few splits (config 1's half-bars: a few thousand) searches
+// one split per wave, 4 dependent rounds instead of ~21 (k_partition_all
+// ~50 -> ~36 us per batch); with many splits (configs 2-5: tens of
+// thousands) the 64 probes per round cost more bandwidth than the rounds
+// save (config 2's k_partition_unique 49 -> 135 us), so one thread per split.
+constexpr uint32_t kWaveSplitsMax = 4096;
+
+template <int KIND, bool Wave>
+__device__ __forceinline__ uint32_t split_at(const JobDesc &j, uint32_t d) {
+    if constexpr (Wave) return merge_path_split_wave<KIND>(j, d);
+    else return merge_path_split<KIND>(j, d);
+}
+
+template <bool Wave>
+__device__ __forceinline__ uint32_t split_index() {
+    return Wave ? blockIdx.x * 4 + (threadIdx.x >> 6) : blockIdx.x * 256 + threadIdx.x;
+}
+
+template <bool Wave>
+__global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int njobs, uint32_t nsplits,
+                                                       SplitDesc *splits, const JobResultDev *res, uint32_t phase) {
+    const uint32_t gsplit = split_index<Wave>();
+    if (gsplit >= nsplits) return; // wave-uniform
+    const int ji = find_job(jobs, njobs, gsplit, [](const JobDesc &d) { return d.split_base; });
+    const JobDesc &j = jobs[ji];
+    if (phase_skips(j, res, phase)) return;
+    const uint32_t t = gsplit - j.split_base;
+    const uint32_t na = j.a.n, nb = j.b.n, n = na + nb;
+    const uint32_t d = (uint64_t)t * j.merge_tile < n ? t * j.merge_tile : n;
+    uint32_t lo;
+    switch (j.key_kind) {
+    case kKeyTimestamp: lo = split_at<kKeyTimestamp, Wave>(j, d); break;
+    case kKeyIdU128: lo = split_at<kKeyIdU128, Wave>(j, d); break;
+    case kKeyCompositeU64: lo = split_at<kKeyCompositeU64, Wave>(j, d); break;
+    default: lo = split_at<kKeyCompositeU128, Wave>(j, d); break;
+    }
+    if (Wave && (threadIdx.x & 63) != 0) return;
+    SplitDesc s;
+    s.i = lo;
+    s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
+    const uint32_t jb = d - lo;
+    s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
+    s.pad = 0;
+    splits[gsplit] = s;
+}
+
+// Speculated jobs (TBC_COMPACTION_UNIQUE_KEYS): with every value surviving,
+// data block k holds merged positions [k * vcm, (k + 1) * vcm); its producer
+// starts from the merge-path split at k * vcm. The thread of block 0 also
+// writes the job's speculative results (write_blocks' shape for n values,
+// compaction.zig:806-850); a broken speculation has them rewritten by the
+// recomputation's k_tile_scan.
 __global__ __launch_bounds__(256) void k_partition_blocks(const JobDesc *jobs, int njobs, uint32_t total,
                                                           SplitDesc *bsplits, JobResultDev *res) {
     const uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -200,9 +221,10 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 // tombstones are dropped. A broken job is marked (JobResultDev.spec) and
 // recomputed through the merge path by the batch's phase 1.
 // --------------------------------------------------------------------------
+template <bool Wave>
 __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, int njobs, uint32_t nsplits,
                                                           UniqueSplit *usplits, JobResultDev *res) {
-    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t g = split_index<Wave>();
     if (g >= nsplits) return;
     const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.usplit_base; });
     const JobDesc &j = jobs[ji];
@@ -212,11 +234,12 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
     const uint32_t d = (uint64_t)t * kUniqueTile < n ? t * kUniqueTile : n;
     uint32_t lo;
     switch (j.key_kind) {
-    case kKeyTimestamp: lo = merge_path_split<kKeyTimestamp>(j, d); break;
-    case kKeyIdU128: lo = merge_path_split<kKeyIdU128>(j, d); break;
-    case kKeyCompositeU64: lo = merge_path_split<kKeyCompositeU64>(j, d); break;
-    default: lo = merge_path_split<kKeyCompositeU128>(j, d); break;
+    case kKeyTimestamp: lo = split_at<kKeyTimestamp, Wave>(j, d); break;
+    case kKeyIdU128: lo = split_at<kKeyIdU128, Wave>(j, d); break;
+    case kKeyCompositeU64: lo = split_at<kKeyCompositeU64, Wave>(j, d); break;
+    default: lo = split_at<kKeyCompositeU128, Wave>(j, d); break;
     }
+    if (Wave && (threadIdx.x & 63) != 0) return;
     UniqueSplit s;
     s.i = lo;
     s.pad = 0;
@@ -463,7 +486,11 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     const uint32_t nsplits = l.usplit_base + (l.unique ? l.utile_count + 1 : 0);
     const uint32_t ntiles = l.utile_base + l.utile_count;
     if (!nsplits || !ntiles) return 0;
-    hipLaunchKernelGGL(k_partition_unique, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
+    if (nsplits <= kWaveSplitsMax)
+        hipLaunchKernelGGL(k_partition_unique<true>, dim3((nsplits + 3) / 4), dim3(256), 0, s, d_jobs, njobs, nsplits,
+                       (UniqueSplit *)d_usplits, d_results);
+    else
+        hipLaunchKernelGGL(k_partition_unique<false>, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
                        (UniqueSplit *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
@@ -817,7 +844,11 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     {
         const JobDesc &l = h_jobs[njobs - 1];
         const uint32_t nsplits = l.split_base + l.tile_count + 1;
-        hipLaunchKernelGGL(k_partition_all, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
+        if (nsplits <= kWaveSplitsMax)
+            hipLaunchKernelGGL(k_partition_all<true>, dim3((nsplits + 3) / 4), dim3(256), 0, s, d_jobs, njobs, nsplits,
+                           d_splits, (const JobResultDev *)d_results, phase);
+        else
+            hipLaunchKernelGGL(k_partition_all<false>, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
                            d_splits, (const JobResultDev *)d_results, phase);
         if (hipGetLastError() != hipSuccess) return -1;
     }

@@ -76,8 +76,10 @@ constexpr uint64_t kCountMask = (1ull << 30) - 1;
 
 struct SortSeg {
     uint64_t key_or[kMaxLimbs], key_and[kMaxLimbs]; // over the table (extract)
-    uint8_t *values;
-    uint8_t *copy; // n * vs bytes: the table as put, the gather's source
+    uint8_t *values;     // where the sorted table goes
+    uint8_t *copy;       // n * vs bytes: the table as put, the gather's source
+    const uint8_t *src;  // the table as put, for extract and pack (values in place, copy out of place)
+    uint32_t oop;        // out of place: values is written, never read; copy is the caller's input
     uint32_t n, vs, ts_off, kind;
     uint32_t kl; // key limbs of the table's key kind
     uint32_t item_base, tile_base, tiles;
@@ -142,8 +144,8 @@ __device__ __forceinline__ uint32_t *seg_hist(uint32_t *hist, uint32_t s) { retu
 // row_load issues them, row_next forms the neighbours once they are in.
 __device__ __forceinline__ void row_load(const SortSeg &S, uint32_t li, uint64_t k[3], uint64_t kx[3]) {
     k[0] = k[1] = k[2] = kx[0] = kx[1] = kx[2] = 0;
-    if (li < S.n) key_of(S.kind, S.values + (size_t)li * S.vs, S.ts_off, k);
-    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.values + (size_t)(li + 1) * S.vs, S.ts_off, kx);
+    if (li < S.n) key_of(S.kind, S.src + (size_t)li * S.vs, S.ts_off, k);
+    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.src + (size_t)(li + 1) * S.vs, S.ts_off, kx);
 }
 __device__ __forceinline__ void row_next(uint32_t li, uint32_t n, const uint64_t k[3], const uint64_t kx[3],
                                          uint64_t kn[3]) {
@@ -177,7 +179,24 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
         if (lt * kSortTile + r * kSortThreads >= n) break; // wave-uniform (whole row past the end)
         const bool in = li < n;
         // The row's first 128 bytes of every value are loaded with its keys
-        // (one round trip), then stored; longer values loop.
+        // (one round trip), then stored; longer values loop. Out of place,
+        // the caller's input is the gather's source: keys only.
+        if (S.oop) {
+            uint64_t k[3], kn[3];
+            row_keys(S, li, k, kn);
+            if (!in) continue;
+            for (uint32_t l = 0; l < kl; l++) {
+                o[l] |= k[l];
+                a[l] &= k[l];
+            }
+            if (li + 1 < n) {
+                int cmp = 0;
+                for (uint32_t l = 0; l < kl; l++)
+                    if (k[l] != kn[l]) cmp = k[l] > kn[l] ? 1 : -1;
+                uns |= cmp > 0 ? 1u : 0u;
+            }
+            continue;
+        }
         u32x4 v[8];
         if (in) {
 #pragma unroll
@@ -712,11 +731,18 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
     const uint32_t tile = blockIdx.x / (kSortTile / kFinishItems);
     const uint32_t sg = tile_seg[tile];
     const SortSeg S = segs[sg];
-    if (!S.nact) return; // uniform: in order, untouched
-    const uint64_t *wv = (S.final_buf ? words1 : words0) + S.item_base; // the table's sorted words
-    const uint64_t imask = low_mask(S.ib);
     const uint32_t n = S.n, vs = S.vs, tid = threadIdx.x;
     const uint32_t first = (tile - S.tile_base) * kSortTile + (blockIdx.x % (kSortTile / kFinishItems)) * kFinishItems;
+    if (!S.nact) { // uniform: in order; in place untouched, out of place copied as is
+        if (!S.oop || first >= n) return;
+        const uint32_t last = first + kFinishItems < n ? first + kFinishItems : n;
+        const uint32_t chunks = (last - first) * (vs >> 4);
+        for (uint32_t c = tid; c < chunks; c += 256)
+            gst<u32x4>(S.values + (size_t)first * vs + 16 * c, gld<u32x4>(S.copy + (size_t)first * vs + 16 * c));
+        return;
+    }
+    const uint64_t *wv = (S.final_buf ? words1 : words0) + S.item_base; // the table's sorted words
+    const uint64_t imask = low_mask(S.ib);
     if (first >= n) return;
     const uint32_t last = first + kFinishItems < n ? first + kFinishItems : n;
     if (!S.fix) {
@@ -885,7 +911,7 @@ static SortScratch scratch_layout(const SortItem *items, uint32_t count) {
         if (items[j].n < 2) continue;
         N += items[j].n;
         tiles += tiles_of(items[j].n);
-        vals += align256((uint64_t)items[j].n * items[j].value_size);
+        if (!items[j].out) vals += align256((uint64_t)items[j].n * items[j].value_size);
         nseg++;
         kl = kl > key_limbs(items[j].key_kind) ? kl : key_limbs(items[j].key_kind);
     }
@@ -939,7 +965,7 @@ uint64_t sort_host_bytes(const SortItem *items, uint32_t count) {
 int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint64_t scratch_bytes, uint64_t *status,
                       uint64_t status_words, uint32_t *epoch, void *host, void *stream) {
     const SortScratch L = scratch_layout(items, count);
-    if (scratch_bytes < L.total || status_words < sort_status_words(items, count)) return -1;
+    if (scratch_bytes < L.total || status_words < sort_status_words(items, count)) return -2;
     hipStream_t s = (hipStream_t)stream;
     uint8_t *base = (uint8_t *)scratch, *hbase = (uint8_t *)host;
     SortSeg *hsegs = (SortSeg *)(hbase + L.segs);
@@ -949,12 +975,23 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     uint64_t copy_off = L.copies;
     for (uint32_t j = 0; j < count; j++) {
         const SortItem &it = items[j];
-        if (it.n < 2) continue;
+        if (it.n < 2) {
+            if (it.n == 1 && it.out && hipMemcpyAsync(it.out, it.values, it.value_size, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return -3;
+            continue;
+        }
         SortSeg g{};
         for (uint32_t l = 0; l < kMaxLimbs; l++) g.key_and[l] = ~0ull;
-        g.values = (uint8_t *)it.values;
-        g.copy = base + copy_off;
-        copy_off += align256((uint64_t)it.n * it.value_size);
+        g.src = (const uint8_t *)it.values;
+        if (it.out) { // out of place: the input is the gather's source, no copy
+            g.values = (uint8_t *)it.out;
+            g.copy = (uint8_t *)it.values;
+            g.oop = 1;
+        } else {
+            g.values = (uint8_t *)it.values;
+            g.copy = base + copy_off;
+            copy_off += align256((uint64_t)it.n * it.value_size);
+        }
         g.n = it.n;
         g.vs = it.value_size;
         g.ts_off = it.timestamp_offset;
@@ -996,9 +1033,15 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     uint32_t *hist = (uint32_t *)(base + L.hist), *bins = (uint32_t *)(base + L.bins);
     uint32_t *counters = (uint32_t *)(base + L.counters);
     SortBatch *d_batch = (SortBatch *)(base + L.batch);
-    if (launch_upload(base, hbase, L.hist, s) != 0 ||
-        hipMemsetAsync(hist, 0, L.bins - L.hist, s) != hipSuccess)
-        return -1;
+    if (launch_upload(base, hbase, L.hist, s) != 0) return -4;
+    {
+        const hipError_t err = hipMemsetAsync(hist, 0, L.bins - L.hist, s);
+        if (err != hipSuccess) {
+            fprintf(stderr, "tbc: sort memset %p %llu: %s\n", (void *)hist, (unsigned long long)(L.bins - L.hist),
+                    hipGetErrorString(err));
+            return -6;
+        }
+    }
     hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile);
     hipLaunchKernelGGL(k_sort_layout, dim3(nseg), dim3(64), 0, s, d_segs);
     hipLaunchKernelGGL(k_sort_pack, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, words0, hist);
@@ -1012,7 +1055,7 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_pass, kSortThreads, 0) != hipSuccess ||
             hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1)
-            return -1;
+            return -5;
         resident = (uint32_t)(per_cu * cus);
     }
     const uint32_t pgrid = ntiles < resident ? ntiles : resident;

@@ -466,6 +466,7 @@ uint64_t copy_chunk_bytes();
 struct SortItem {
     void *values;
     uint32_t n, value_size, timestamp_offset, key_kind;
+    void *out; // null: sorted in place; else the sorted values go here and `values` is only read
 };
 // Enqueues the whole sort of a batch of memtables (no host wait); `host` is
 // pinned staging of sort_host_bytes() that must outlive the enqueued copy.

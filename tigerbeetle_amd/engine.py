@@ -202,6 +202,21 @@ class Memtable:
     def reset(self) -> None:
         check(lib().tbc_memtable_reset(self.handle), "tbc_memtable_reset")
 
+    @staticmethod
+    def make_immutable(engine: "Engine", pairs: list) -> None:
+        """tbc_memtable_make_immutable: [(mutable, immutable, in_order)] — each
+        mutable table's values become its (empty) immutable table's, in key
+        order (one out-of-place sort of every table not in order), and the
+        mutable tables are emptied."""
+        n = len(pairs)
+        if not n:
+            return
+        muts = (ctypes.c_void_p * n)(*[m.handle for m, _, _ in pairs])
+        imms = (ctypes.c_void_p * n)(*[im.handle for _, im, _ in pairs])
+        order = (ctypes.c_uint8 * n)(*[1 if o else 0 for _, _, o in pairs])
+        check(lib().tbc_memtable_make_immutable(engine.handle, muts, imms, ctypes.cast(order, ctypes.c_void_p), n),
+              "tbc_memtable_make_immutable")
+
     def close(self) -> None:
         if self.handle:
             lib().tbc_memtable_deinit(self.handle)
@@ -258,7 +273,8 @@ class Batch:
 
     def __del__(self):
         try:
-            self.release()
+            if self.handle and self.engine.handle:  # a closed engine took its batches' memory with it
+                self.release()
         except Exception:
             pass
 
@@ -409,14 +425,16 @@ class Engine:
         check(lib().tbc_copy_device_batch(self.handle, arr, len(copies)), "tbc_copy_device_batch")
 
     def sort_values_batch(self, tables: list) -> None:
-        """Bar end: [(TreeSpec, DeviceBuffer | device ptr, count)] sorted by one
-        segmented launch sequence (tbc_sort_values_batch), enqueued on the
-        engine stream."""
+        """Bar end: [(TreeSpec, DeviceBuffer | device ptr, count[, out])] sorted
+        by one segmented launch sequence (tbc_sort_values_batch), enqueued on
+        the engine stream; with `out` (a device pointer) a table is sorted out
+        of place into it and its values are only read."""
         arr = (abi.SortJob * max(1, len(tables)))()
-        for i, (tree, buf, n) in enumerate(tables):
+        for i, (tree, buf, n, *out) in enumerate(tables):
             arr[i].tree = tree.ctype()
             arr[i].values = buf if isinstance(buf, int) else buf.ptr
             arr[i].count = n
+            arr[i].values_out = out[0] if out else None
         check(lib().tbc_sort_values_batch(self.handle, arr, len(tables)), "tbc_sort_values_batch")
 
     def kway_merge(self, tree: TreeSpec, streams: list, out: DeviceBuffer, descending: bool = False) -> int:

@@ -627,40 +627,44 @@ class GridExecutor:
         self.puts_bytes += values.nbytes
 
     def swap(self, names: list) -> None:
-        """Every memtable becomes immutable; the ones named are sorted."""
+        """Bar end: every mutable table becomes immutable (its immutable table
+        was flushed by the bar's first half); the ones named are sorted, by
+        one out-of-place sort into the immutable tables' buffers
+        (tbc_memtable_make_immutable), the others trade buffers."""
+        sort = set(names)
+        pairs = []
         for name in list(self.mutable):
-            self.mutable[name], self.immutable[name] = self.immutable[name], self.mutable[name]
-            self.mutable[name].reset()
-        # Recording: an immutable table that needs no sort (its puts arrived
-        # in key order) is compacted from a copy of its own, so that a replay
-        # of the record reads this bar's values rather than whatever the
-        # memtable buffer holds by then (a sorted table is re-landed before
-        # its sort instead, below).
-        self.frozen = {}
+            self.immutable[name].reset()  # make_mutable after its flush
+            pairs.append((name, self.mutable[name], self.immutable[name]))
+        # Recording: each table as put is copied first, so that a replay of
+        # the record sorts it again from that copy (straight into the
+        # immutable buffer, as here), and a table that needs no sort is
+        # compacted from its copy (the buffer holds a later bar by then).
+        archived = {}
         if self.recording:
-            for name, mt in self.immutable.items():
-                ptr, n = mt.values()
-                if name in names or n == 0:
+            for name, m, _ in pairs:
+                ptr, n = m.values()
+                if n == 0:
                     continue
                 nbytes = n * trees.BY_NAME[name].value_size
                 copy = self.engine.alloc(nbytes)
                 self.engine.copy_device_async(copy.ptr, ptr, nbytes)
                 self.archive.append(copy)
-                self.frozen[name] = (copy.ptr, n)
-        jobs = []
-        for name in names:
-            ptr, n = self.immutable[name].values()
-            jobs.append((trees.BY_NAME[name], ptr, n))
-        if jobs:
-            landings = []
-            if self.recording:
-                for s, p, n in jobs:
-                    copy = self.engine.alloc(max(1, n * s.value_size))
-                    self.engine.copy_device_async(copy.ptr, p, n * s.value_size)
-                    self.archive.append(copy)
-                    landings.append((p, copy.ptr, n * s.value_size))
-                self.record.append(("sort", jobs, landings))
-            self.engine.sort_values_batch(jobs)
+                archived[name] = (copy.ptr, n)
+        self._Memtable.make_immutable(self.engine, [(m, im, name not in sort) for name, m, im in pairs])
+        self.frozen = {}
+        if self.recording:
+            jobs = []
+            for name, _, im in pairs:
+                if name not in archived:
+                    continue
+                if name in sort:
+                    out, n = im.values()
+                    jobs.append((trees.BY_NAME[name], archived[name][0], n, out))
+                else:
+                    self.frozen[name] = archived[name]
+            if jobs:
+                self.record.append(("sort", jobs))
 
     def flushed(self, name: str) -> None:
         pass  # the immutable memtable is reset when it becomes mutable again (swap)
