@@ -163,7 +163,9 @@ class SplitPart:
     the survivor counts (RCCL over xGMI with the nccl backend), the range's
     bodies written in place at their global positions, the partial block's
     values to its owner, the owned data blocks finished in place, one table's
-    index entries to its owner, the owned index blocks sealed."""
+    index entries to its owner, the owned index blocks sealed. With nccl the
+    step's enqueue waits on the host once (the gathered counts); the rank
+    holds only its own output slots (split.slot_range)."""
 
     def __init__(self, eng: Engine, js, gid: int, rank: int, world: int, exchange, bs: int):
         from tigerbeetle_amd import split, workloads
@@ -601,13 +603,33 @@ def main() -> None:
         wl.input_bytes += part.input_bytes
     eng.synchronize()
 
+    class SplitStep:
+        """A split step's handle: the whole jobs' batch and the split's
+        enqueued work (bodies, seals), waited for together."""
+
+        def __init__(self, b, res):
+            self.b, self.res = b, res
+
+        def wait(self):
+            self.b.wait()
+            self.res.finish()
+
+        def kernel_times(self):
+            return self.b.kernel_times()
+
+        def result(self, i):
+            return self.b.result(i)
+
+        def release(self):
+            self.b.release()
+
     def submit():
         """Enqueue one step; returns its batch (not waited for)."""
         if part is None:
             return wl.submit(eng)
         held = []
-        part.run(eng, before_phase2=lambda: held.append(wl.submit(eng)))
-        return held[0] if held else wl.submit(eng)
+        res = part.run(eng, before_phase2=lambda: held.append(wl.submit(eng)))
+        return SplitStep(held[0] if held else wl.submit(eng), res)
 
     def step():
         b = submit()
@@ -621,8 +643,9 @@ def main() -> None:
     # `depth` sets; stream order keeps the mask buffer consistent), so the
     # device never idles for the host and consecutive steps' AEGIS chains
     # share the chip (the engine pipelines a UNIQUE_KEYS batch submitted
-    # while another is running). A split step (config 4, N > 1) exchanges
-    # between its phases: sequential.
+    # while another is running). A split step (config 4, N > 1) reuses its
+    # exchange buffers and output slots each step: sequential (its enqueue
+    # waits once, for the gathered counts, split.compact_split).
     overlap = not args.no_overlap and part is None
     depth = max(1, args.depth) if overlap else 1
     out_sets = wl.rotate(eng, depth) if overlap else 1

@@ -135,7 +135,9 @@ typedef struct tbc_segment {
 #define TBC_COMPACTION_UNIQUE_KEYS 4u
 /* COUNT_ONLY: the merge alone (survivor rules included); the result's
  * value_count is the number of survivors and nothing is written
- * (output_blocks may be NULL). Phase A of a job split by key range
+ * (output_blocks may be NULL; if not, the count is also stored there as a
+ * u64 on the device, in engine-stream order, for a caller that exchanges it
+ * without a host wait). Phase A of a job split by key range
  * (tbc_compaction.output_offset, tbc_compaction_seal). */
 #define TBC_COMPACTION_COUNT_ONLY 8u
 
@@ -352,6 +354,10 @@ typedef struct tbc_copy {
 } tbc_copy;
 tbc_status tbc_copy_device_batch(tbc_engine *engine, const tbc_copy *copies, uint32_t count);
 tbc_status tbc_memset_device(tbc_engine *engine, void *dst, int value, uint64_t bytes);
+/* The engine stream (a hipStream_t): work a caller orders with the engine's
+ * (a collective over the split's exchange buffers, torch.cuda.ExternalStream)
+ * goes on it. */
+tbc_status tbc_engine_stream(tbc_engine *engine, void **out_stream);
 /* Waits for every enqueued call; TBC_ERR_BLOCK_INVALID (once) if the device
  * found an error in a call that had already returned (a refused manifest
  * close). */

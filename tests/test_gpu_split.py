@@ -87,7 +87,7 @@ def _run_rank(name, rank, world, exchange):
         assert split.staged_bytes(cuts, rank, spec.value_size) == a_mine.nbytes + b_mine.nbytes
         job = Job(spec, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48,
                   np.asarray(addrs, dtype=np.uint64), None)
-        res = split.compact_split(eng, job, cuts, exchange, rank, staged=True)
+        res = split.compact_split(eng, job, cuts, exchange, rank, staged=True).finish()
         whole = run_oracle(oracle, ji, bs, addrs)
         assert whole.status == 0
         plan = res.plan
@@ -96,11 +96,11 @@ def _run_rank(name, rank, world, exchange):
         if res.exchanged["heads"] > (vcm - 1) * spec.value_size or \
                 res.exchanged["entries"] > (dbcm - 1) * split.entry_bytes(spec.key_size):
             return False, f"rank {rank}: exchanged {res.exchanged}"
-        got = res.arena.download().reshape(-1, bs)
+        got = res.arena.download().reshape(-1, bs)  # this rank's slots only (split.slot_range)
         slots = [split.data_block_slot(k, dbcm) for k in range(*res.blocks)]
         slots += [split.index_block_slot(t, plan.k_last(t)) for t in range(*res.tables)]
         for slot in slots:
-            if not np.array_equal(disk_image(got[slot]), disk_image(whole.blocks[slot])):
+            if not np.array_equal(disk_image(got[slot - res.base_slot]), disk_image(whole.blocks[slot])):
                 return False, f"rank {rank}: block slot {slot} differs"
         t0, t1 = res.tables
         if not np.array_equal(res.table_infos, whole.table_infos[t0:t1]):

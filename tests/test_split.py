@@ -235,7 +235,7 @@ class _OracleEngine:
             self.copy_device_async(dst, src, n)
 
     def synchronize(self):
-        pass
+        self.waits += 1
 
     def submit(self, jobs):
         from tigerbeetle_amd import abi
@@ -245,6 +245,8 @@ class _OracleEngine:
                      np.arange(1, workloads.worst_case_blocks(self.spec, max(1, len(a) + len(b)), BS) + 2,
                                dtype=np.uint64))
         surv = data_values_from_blocks(r.blocks, self.spec.value_size)
+        if j.flags & abi.COMPACTION_COUNT_ONLY and j.output is not None:  # the count into a device word
+            self.mem[j.output.ptr:j.output.ptr + 8] = np.frombuffer(len(surv).to_bytes(8, "little"), np.uint8)
         if j.flags & abi.COMPACTION_VALUES_ONLY:
             vs = self.spec.value_size
             for i, v in enumerate(surv):
@@ -253,8 +255,26 @@ class _OracleEngine:
                 at = j.output.ptr + split.data_block_slot(k, self.dbcm) * BS + 256 + (g - k * self.vcm) * vs
                 self.mem[at:at + vs] = v
         res = SimpleNamespace(value_count=len(surv), status=0, table_count=0)
-        return SimpleNamespace(wait=lambda: None, release=lambda: None,
-                               result=lambda i: (res, np.zeros((0, 128), np.uint8)))
+        return self._batch(res, np.zeros((0, 128), np.uint8))
+
+    def _batch(self, res, infos):
+        eng = self
+
+        class _B:
+            def wait(self):
+                eng.waits += 1
+
+            def release(self):
+                pass
+
+            def result(self, i):
+                return res, infos
+        return _B()
+
+    waits = 0  # Batch.wait and synchronize calls (test_split_step_waits_once)
+
+    def seal_submit(self, *args):
+        return self._batch(*self.seal(*args))
 
     def seal(self, tree, cluster, snapshot_min, level_b, addresses, arena, value_count, blocks, tables):
         spec, vs, ks, vcm, dbcm = self.spec, self.spec.value_size, self.spec.key_size, self.vcm, self.dbcm
@@ -325,10 +345,38 @@ class _ThreadExchange:
         ex = self
 
         class Rank:
-            def all_gather_counts(self, count):
-                return ex._gather(r, int(count))
+            """As TorchExchange over host memory (gloo): each exchange waits."""
 
-            def all_gather_heads(self, engine, segments, nbytes):
+            def count_buffer(self, engine, scratch):
+                return engine.alloc(256)
+
+            def gather_counts(self, engine, batch, buf, scratch):
+                batch.wait()
+                return ex._gather(r, int(batch.result(0)[0].value_count))
+
+            def all_gather_bytes(self, engine, segments, nbytes, key, scratch):
+                engine.synchronize()
+                mine = b"".join(engine.mem[p:p + n].tobytes() for p, n in segments).ljust(nbytes, b"\0")
+                got = ex._gather(r, mine)
+                bufs = [engine.upload(np.frombuffer(g, np.uint8)) if nbytes else None for g in got]
+                return bufs, [b.ptr if b else 0 for b in bufs]
+        return Rank()
+
+    def device_rank(self, r, eng):
+        """As TorchExchange on the device (nccl): the count merge's word and
+        the byte buffers are exchanged in stream order; the one host wait is
+        reading the gathered counts (here: the count word, read once)."""
+        ex = self
+
+        class Rank:
+            def count_buffer(self, engine, scratch):
+                return engine.alloc(256)
+
+            def gather_counts(self, engine, batch, buf, scratch):
+                engine.waits += 1  # reading the gathered counts
+                return ex._gather(r, int.from_bytes(engine.mem[buf.ptr:buf.ptr + 8].tobytes(), "little"))
+
+            def all_gather_bytes(self, engine, segments, nbytes, key, scratch):
                 mine = b"".join(engine.mem[p:p + n].tobytes() for p, n in segments).ljust(nbytes, b"\0")
                 got = ex._gather(r, mine)
                 bufs = [engine.upload(np.frombuffer(g, np.uint8)) if nbytes else None for g in got]
@@ -359,7 +407,9 @@ def _run_split(spec, ji, addrs, world, cuts, exchanges, engines):
                 segs.append([(buf.ptr, len(vals))] if buf else [])
             job = Job(spec, segs[0], segs[1], ji.a_immutable, ji.drop_tombstones, LEVEL_B, CLUSTER, SNAPSHOT_MIN,
                       np.asarray(addrs, np.uint64), None)
-            results[p] = split.compact_split(eng, job, cuts, exchanges[p], p, staged=True)
+            res = split.compact_split(eng, job, cuts, exchanges[p], p, staged=True)
+            eng.step_waits = eng.waits  # host waits of the enqueue (finish() waits for the rest)
+            results[p] = res.finish()
         except Exception as e:  # noqa: BLE001 - reported below, other threads must not hang
             errors.append((p, repr(e)))
             exchanges[p]  # noqa: B018
@@ -381,11 +431,20 @@ def _check_union(spec, ji, addrs, world, results, engines):
     vcm, dbcm = lay["block_value_count_max"], lay["data_block_count_max"]
     got = {}
     for p, res in enumerate(results):
-        arena = engines[p].mem[res.arena.ptr:res.arena.ptr + res.arena.nbytes].reshape(-1, BS)
+        mem = engines[p].mem
+
+        def block(slot):
+            at = res.slot_ptr(slot)
+            return mem[at:at + BS]
         for k in range(*res.blocks):
-            got[split.data_block_slot(k, dbcm)] = arena[split.data_block_slot(k, dbcm)]
+            got[split.data_block_slot(k, dbcm)] = block(split.data_block_slot(k, dbcm))
         for t in range(*res.tables):
-            got[split.index_block_slot(t, plan.k_last(t))] = arena[split.index_block_slot(t, plan.k_last(t))]
+            got[split.index_block_slot(t, plan.k_last(t))] = block(split.index_block_slot(t, plan.k_last(t)))
+        # Only this rank's own slots are held: its blocks, its head block and
+        # the index blocks of the tables its blocks belong to.
+        lo, hi = split.slot_range(plan, p)
+        assert res.arena.nbytes == (hi - lo) * BS
+        assert hi - lo <= -(-plan.counts[p] // vcm) + 2 + dbcm + 1
     assert sorted(got) == list(range(len(whole.blocks)))
     for i, w in enumerate(whole.blocks):
         assert np.array_equal(disk_image(got[i]), disk_image(w)), i
@@ -406,6 +465,25 @@ def test_split_job_equals_unsplit_job(oracle_lib, case, world, method):
     tex = _ThreadExchange(world)
     results = _run_split(spec, ji, addrs, world, cuts, [tex.rank(p, engines[p]) for p in range(world)], engines)
     _check_union(spec, ji, addrs, world, results, engines)
+
+
+@pytest.mark.parametrize("case", [0, 3])
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_step_waits_once(oracle_lib, case, world):
+    """With the exchange on the device (TorchExchange over nccl), a split
+    step waits on the host once — for the gathered counts — and enqueues the
+    rest (bodies, heads, seals, entries); over host memory (gloo) it also
+    waits before each of its two byte all-gathers. Both give the unsplit
+    job's bytes."""
+    spec, ji, addrs = _inputs(case)
+    cuts = _block_cuts(spec, ji, world)
+    for device, most in ((True, 1), (False, 3)):
+        engines = [_OracleEngine(spec) for _ in range(world)]
+        tex = _ThreadExchange(world)
+        ranks = [(tex.device_rank if device else tex.rank)(p, engines[p]) for p in range(world)]
+        results = _run_split(spec, ji, addrs, world, cuts, ranks, engines)
+        _check_union(spec, ji, addrs, world, results, engines)
+        assert max(e.step_waits for e in engines) <= most, [e.step_waits for e in engines]
 
 
 # --- the same flow with the exchange over gloo (TorchExchange), world 2 and 3 --
@@ -435,13 +513,16 @@ def _worker(rank, world, port, case, q):
         segs.append([(buf.ptr, len(vals))] if buf else [])
     job = Job(spec, segs[0], segs[1], ji.a_immutable, ji.drop_tombstones, LEVEL_B, CLUSTER, SNAPSHOT_MIN,
               np.asarray(addrs, np.uint64), None)
-    res = split.compact_split(eng, job, cuts, split.TorchExchange(dist), rank, staged=True)
-    arena = eng.mem[res.arena.ptr:res.arena.ptr + res.arena.nbytes].reshape(-1, BS)
+    res = split.compact_split(eng, job, cuts, split.TorchExchange(dist), rank, staged=True).finish()
     dbcm = spec.layout(BS)["data_block_count_max"]
-    mine = {split.data_block_slot(k, dbcm): bytes(disk_image(arena[split.data_block_slot(k, dbcm)]))
+
+    def block(slot):
+        at = res.slot_ptr(slot)
+        return eng.mem[at:at + BS]
+    mine = {split.data_block_slot(k, dbcm): bytes(disk_image(block(split.data_block_slot(k, dbcm))))
             for k in range(*res.blocks)}
     mine.update({split.index_block_slot(t, res.plan.k_last(t)):
-                 bytes(disk_image(arena[split.index_block_slot(t, res.plan.k_last(t))])) for t in range(*res.tables)})
+                 bytes(disk_image(block(split.index_block_slot(t, res.plan.k_last(t))))) for t in range(*res.tables)})
     q.put((rank, mine, res.table_infos.tobytes(), res.exchanged))
     dist.barrier()
     dist.destroy_process_group()
@@ -530,14 +611,14 @@ def _heads_worker(rank, world, port, q):
     need = [0, 7, 3][rank]
     segs = [(buf.ptr, 16 * min(need, 4)), (buf.ptr + 64, 16 * max(0, need - 4))]  # head in two pieces
     ex = split.TorchExchange(dist)
-    _, ptrs = ex.all_gather_heads(eng, [s for s in segs if s[1]], 7 * 16)
+    _, ptrs = ex.all_gather_bytes(eng, [s for s in segs if s[1]], 7 * 16, "heads", {})
     got = [bytes(eng.mem.read(p, 7 * 16)) for p in ptrs]
     q.put((rank, got))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_all_gather_heads_host_path_over_gloo():
+def test_all_gather_bytes_host_path_over_gloo():
     world = 3
     port = _free_port()
     ctx = mp.get_context("spawn")

@@ -211,6 +211,7 @@ _SIGNATURES = {
     "tbc_memtable_put": (ctypes.c_int, [_P, _P, ctypes.c_uint32]),
     "tbc_memtable_values": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint32)]),
     "tbc_memtable_reset": (ctypes.c_int, [_P]),
+    "tbc_engine_stream": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "tbc_memtable_make_immutable": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, ctypes.c_uint32]),
 }
 

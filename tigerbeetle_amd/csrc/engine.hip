@@ -1127,6 +1127,12 @@ static bool sync_streams(tbc_engine *e) {
     return ok;
 }
 
+tbc_status tbc_engine_stream(tbc_engine *e, void **out_stream) {
+    if (!e || !out_stream) return TBC_ERR_INVALID_ARGUMENT;
+    *out_stream = (void *)e->stream;
+    return TBC_OK;
+}
+
 tbc_status tbc_synchronize(tbc_engine *e) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!sync_streams(e)) return TBC_ERR_DEVICE;
@@ -2197,6 +2203,12 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
                               d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
+        // A job with output_blocks also gets its count there (u64, device,
+        // stream order), for a caller that exchanges it on the device.
+        for (uint32_t i = 0; ok && i < count; i++)
+            if (jobs_in[i].output_blocks)
+                ok = hipMemcpyAsync(jobs_in[i].output_blocks, &d_res[i].value_count, 8, hipMemcpyDeviceToDevice, s) ==
+                     hipSuccess;
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res, hipMemcpyDeviceToHost, s) == hipSuccess;
         ok = ok && hipEventRecord(b->done, s) == hipSuccess;
     } else if (any_unique && spec_pipe) {

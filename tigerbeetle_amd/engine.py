@@ -480,12 +480,33 @@ class Engine:
         check(lib().tbc_compaction_submit(self.handle, arr, len(jobs), ctypes.byref(h)), "tbc_compaction_submit")
         return Batch(self, h.value, jobs)
 
-    def seal(self, tree: TreeSpec, cluster: int, snapshot_min: int, level_b: int, addresses, arena: DeviceBuffer,
+    def stream_handle(self) -> int:
+        """The engine stream (tbc_engine_stream), for torch.cuda.ExternalStream."""
+        p = ctypes.c_void_p()
+        check(lib().tbc_engine_stream(self.handle, ctypes.byref(p)), "tbc_engine_stream")
+        return p.value
+
+    def seal(self, tree: TreeSpec, cluster: int, snapshot_min: int, level_b: int, addresses, arena,
              value_count: int, blocks: tuple, tables: tuple):
         """tbc_compaction_seal of one split job (blocking): finish data blocks
         [blocks[0], blocks[1]) in place (headers, checksums, index entries),
         then seal tables [tables[0], tables[1]) from the entries in their index
         block slots. Returns (result, TableInfos of the sealed tables)."""
+        b = self.seal_submit(tree, cluster, snapshot_min, level_b, addresses, arena, value_count, blocks, tables)
+        try:
+            b.wait()
+            r, infos = b.result(0)
+            check(r.status, "tbc_compaction_seal")
+            return r, infos
+        finally:
+            b.release()
+
+    def seal_submit(self, tree: TreeSpec, cluster: int, snapshot_min: int, level_b: int, addresses, arena,
+                    value_count: int, blocks: tuple, tables: tuple) -> Batch:
+        """tbc_compaction_seal, enqueued: returns the batch (wait, then
+        result(0) for the sealed tables' TableInfos). `arena.ptr` is the
+        job's output slot 0 (a rank holding only its own slots passes its
+        allocation minus the slots before them)."""
         addrs = np.ascontiguousarray(addresses, dtype=np.uint64)
         sl = abi.Seal()
         sl.tree = tree.ctype()
@@ -501,13 +522,8 @@ class Engine:
         h = ctypes.c_void_p()
         check(lib().tbc_compaction_seal(self.handle, ctypes.byref(sl), ctypes.byref(h)), "tbc_compaction_seal")
         b = Batch(self, h.value, [None])
-        try:
-            b.wait()
-            r, infos = b.result(0)
-            check(r.status, "tbc_compaction_seal")
-            return r, infos
-        finally:
-            b.release()
+        b._keep = addrs  # the host address array outlives the enqueue
+        return b
 
 
 def stage_blocks(engine: Engine, tables: list, value_size: int, block_size: int = BLOCK_SIZE):

@@ -307,36 +307,75 @@ def entry_bytes(key_size: int) -> int:
 # The exchange (torch.distributed: RCCL over xGMI with "nccl", gloo on CPU).
 
 class TorchExchange:
+    """All-gathers of a split step over torch.distributed.
+
+    On device (nccl: RCCL over xGMI, `device` a cuda device) every exchange is
+    a collective enqueued on the ENGINE stream (torch.cuda.ExternalStream over
+    tbc_engine_stream): the count merge writes its count into a device word,
+    the counts are all-gathered behind it, and the one host wait of the step
+    is reading the gathered counts (the host computes the plan from them).
+    Heads and index entries are copied into exchange buffers, all-gathered
+    and copied into place all in engine-stream order, with no host wait.
+    Over gloo (host tensors; the CPU tests and a rehearsal with ranks sharing
+    one GPU) each exchange goes through host memory."""
+
     def __init__(self, dist, device=None):
         self.dist, self.device = dist, device
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.on_device = device is not None and str(device).startswith("cuda")
 
-    def all_gather_counts(self, count: int) -> list:
+    def _stream(self, engine):
         import torch
-        t = torch.tensor([count], dtype=torch.int64, device=self.device)
+        return torch.cuda.ExternalStream(engine.stream_handle(), device=self.device)
+
+    def count_buffer(self, engine, scratch: dict):
+        """Where the count merge stores its count (device, u64)."""
+        if self.on_device:
+            import torch
+            t = scratch.get("count_t")
+            if t is None:
+                t = scratch["count_t"] = torch.zeros(2, dtype=torch.int64, device=self.device)
+            return _Ptr(t.data_ptr())
+        buf = scratch.get("count_buf")
+        if buf is None:
+            buf = scratch["count_buf"] = engine.alloc(256)
+        return buf
+
+    def gather_counts(self, engine, count_batch, count_buf, scratch: dict) -> list:
+        import torch
+        if self.on_device:
+            with torch.cuda.stream(self._stream(engine)):
+                out = scratch.get("counts_t")
+                if out is None:
+                    out = scratch["counts_t"] = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+                self.dist.all_gather_into_tensor(out, scratch["count_t"][:1])
+                return [int(x) for x in out.cpu()]  # the step's one host wait
+        count_batch.wait()
+        t = torch.tensor([int(count_batch.result(0)[0].value_count)], dtype=torch.int64)
         out = [torch.zeros_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t)
         return [int(x.item()) for x in out]
 
-    def all_gather_heads(self, engine, segments: list, nbytes: int):
-        """All-gather each rank's head (`segments`, device, ≤ nbytes) into
+    def all_gather_bytes(self, engine, segments: list, nbytes: int, key: str, scratch: dict):
+        """All-gather each rank's bytes (`segments`, device, <= nbytes) into
         per-rank device buffers. Returns (keep-alive objects, [ptr per rank])."""
         import torch
         if nbytes == 0:
             return [], [0] * self.world
-        on_device = self.device is not None and str(self.device).startswith("cuda")
-        if on_device:
-            mine = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
-            torch.cuda.synchronize(self.device)
-            off = 0
+        if self.on_device:
+            mine, out = scratch.get(key + "_mine"), scratch.get(key + "_out")
+            if mine is None or mine.numel() < nbytes:
+                mine = scratch[key + "_mine"] = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+                out = scratch[key + "_out"] = torch.zeros(self.world * nbytes, dtype=torch.uint8, device=self.device)
+            copies, off = [], 0
             for ptr, n in segments:
-                engine.copy_device_async(mine.data_ptr() + off, ptr, n)
+                copies.append((mine.data_ptr() + off, ptr, n))
                 off += n
-            engine.synchronize()
-            out = [torch.empty_like(mine) for _ in range(self.world)]
-            self.dist.all_gather(out, mine)
-            torch.cuda.synchronize(self.device)
-            return out, [x.data_ptr() for x in out]
+            if copies:
+                engine.copy_device_batch(copies)  # engine stream, after the bodies
+            with torch.cuda.stream(self._stream(engine)):
+                self.dist.all_gather_into_tensor(out[:self.world * nbytes], mine[:nbytes])
+            return [mine, out], [out.data_ptr() + q * nbytes for q in range(self.world)]
         host = np.zeros(nbytes, dtype=np.uint8)
         staging = engine.alloc(nbytes)
         off = 0
@@ -356,12 +395,24 @@ class SingleRank:
     """The exchange of a world of one (no communication)."""
     rank, world = 0, 1
 
-    def all_gather_counts(self, count: int) -> list:
-        return [count]
+    def count_buffer(self, engine, scratch: dict):
+        buf = scratch.get("count_buf")
+        if buf is None:
+            buf = scratch["count_buf"] = engine.alloc(256)
+        return buf
 
-    def all_gather_heads(self, engine, segments: list, nbytes: int):
+    def gather_counts(self, engine, count_batch, count_buf, scratch: dict) -> list:
+        count_batch.wait()
+        return [int(count_batch.result(0)[0].value_count)]
+
+    def all_gather_bytes(self, engine, segments: list, nbytes: int, key: str, scratch: dict):
         assert nbytes == 0
         return [], [0]
+
+
+@dataclass
+class _Ptr:
+    ptr: int
 
 
 # ---------------------------------------------------------------------------
@@ -371,36 +422,84 @@ class SingleRank:
 class SplitResult:
     blocks: tuple          # (k0, k1): the job's data blocks this rank finished
     tables: tuple          # (t0, t1): the job's tables this rank sealed
-    result: object         # tbc_compaction_result of the sealing of those tables (None if none)
-    table_infos: np.ndarray
-    arena: object          # DeviceBuffer: the job's output blocks (slot layout); this rank's are final
     plan: SplitPlan
     exchanged: dict        # bytes this rank sent per exchange: counts, heads, entries
+    arena: object          # DeviceBuffer: this rank's slots [base_slot, base_slot + arena.nbytes / block_size)
+    base_slot: int
+    block_size: int
+    pending: list          # enqueued batches (count merge, bodies, seals), waited for by finish()
+    table_batch: object = None
+    keep: list = None      # exchange buffers the enqueued copies read
+    result: object = None  # tbc_compaction_result of the sealing of the tables (finish; None if none)
+    table_infos: np.ndarray = None
+
+    def slot_ptr(self, slot: int) -> int:
+        """Device address of the job's output slot `slot` (one this rank holds)."""
+        assert self.base_slot <= slot < self.base_slot + self.arena.nbytes // self.block_size, slot
+        return self.arena.ptr + (slot - self.base_slot) * self.block_size
+
+    def finish(self) -> "SplitResult":
+        """Wait for the step's enqueued work; the sealed tables' result and
+        TableInfos."""
+        for b in self.pending:
+            b.wait()
+        self.table_infos = np.zeros((0, 128), dtype=np.uint8)
+        if self.table_batch is not None:
+            self.result, self.table_infos = self.table_batch.result(0)
+            if self.result.status != 0:
+                raise RuntimeError(f"split seal: status {self.result.status}")
+        for b in self.pending:
+            b.release()
+        self.pending, self.keep = [], None
+        return self
+
+
+def slot_range(plan: SplitPlan, p: int) -> tuple:
+    """[lo, hi): the output slots rank p writes — the data blocks its
+    survivors fall in (the head block an earlier rank owns included) and the
+    index blocks of the tables its blocks belong to (which may lie past its
+    blocks, inside the next rank's range)."""
+    o, c = plan.offsets[p], plan.counts[p]
+    if c == 0:
+        return (0, 1)
+    vcm, dbcm = plan.vcm, plan.dbcm
+    lo = data_block_slot(o // vcm, dbcm)
+    hi = data_block_slot((o + c - 1) // vcm, dbcm)
+    k0, k1 = plan.blocks(p)
+    if k1 > k0:
+        for t in range(k0 // dbcm, (k1 - 1) // dbcm + 1):
+            hi = max(hi, index_block_slot(t, plan.k_last(t)))
+    return (lo, hi + 1)
 
 
 def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = False, scratch: dict | None = None,
                   before_phase2=None) -> SplitResult:
-    """Run rank `rank`'s share of `job` split at `cuts` (block_cuts or
-    split_points). With staged=True the job's segments hold only this rank's
-    range [cuts[rank], cuts[rank+1]) of A and of B (what rank_blocks named,
-    staged on this GPU); otherwise the whole job's inputs, sliced here.
-    `scratch` (a dict kept by a caller that repeats the split) keeps the
-    output arena between calls; `before_phase2` runs once the counts are
+    """Enqueue rank `rank`'s share of `job` split at `cuts` (block_cuts or
+    split_points); call `.finish()` on the result to wait for it. With
+    staged=True the job's segments hold only this rank's range
+    [cuts[rank], cuts[rank+1]) of A and of B (what rank_blocks named, staged
+    on this GPU); otherwise the whole job's inputs, sliced here. `scratch` (a
+    dict kept by a caller that repeats the split) keeps the output slots and
+    exchange buffers between steps; `before_phase2` runs once the counts are
     exchanged, just before the bodies are placed (a caller enqueues its other
-    work there)."""
+    work there).
+
+    Host waits: one, reading the gathered counts (the plan — every offset,
+    block and table range — is host arithmetic on them), when the exchange
+    is on the device; everything after that is enqueued on the engine stream
+    (bodies, heads, seals, entries, seals). An exchange through host memory
+    (gloo) also waits before each of its two byte all-gathers.
+
+    The rank holds only its own output slots (`slot_range`): the job's
+    output_blocks base handed to the engine is that allocation minus the
+    slots before it, and the engine touches no slot outside the range."""
     from .abi import COMPACTION_COUNT_ONLY
     from .engine import Job
     tree, bs = job.tree, engine.block_size
     lay = engine.layout(tree)
     vcm, dbcm, vs, ks = lay.block_value_count_max, lay.data_block_count_max, tree.value_size, tree.key_size
     addrs = np.asarray(job.addresses, dtype=np.uint64)
-    nbytes = len(addrs) * bs
-    if scratch is None:
-        arena = engine.alloc(nbytes)
-    else:
-        arena = scratch.get("arena")
-        if arena is None or arena.nbytes < nbytes:
-            arena = scratch["arena"] = engine.alloc(nbytes)
+    scratch = {} if scratch is None else scratch
 
     def sub(segs, lo, hi):
         return [(segs[s][0] + st * vs, n) for s, st, n in range_segments([n for _, n in segs], lo, hi)]
@@ -413,36 +512,38 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     else:
         seg_a, seg_b = sub(job.segments_a, a_lo, a_hi), sub(job.segments_b, b_lo, b_hi)
 
-    def run(jobs):
-        b = engine.submit(jobs)
-        b.wait()
-        r, infos = b.result(0)
-        b.release()
-        if r.status != 0:
-            raise RuntimeError(f"split on rank {rank}: status {r.status}")
-        return r, infos
+    def job_of(flags, output, offset=0, addresses=addrs):
+        return Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
+                   job.snapshot_min, addresses, output, flags=flags, output_offset=offset)
 
-    # Counts (the merge alone), then every rank's global output offset.
-    r0, _ = run([Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
-                     job.snapshot_min, addrs[:0], None, flags=COMPACTION_COUNT_ONLY)])
-    plan = plan_split(exchange.all_gather_counts(int(r0.value_count)), vcm, dbcm)
+    # Counts (the merge alone, its count into a device word), then every
+    # rank's global output offset.
+    count_buf = exchange.count_buffer(engine, scratch)
+    b0 = engine.submit([job_of(COMPACTION_COUNT_ONLY, count_buf, addresses=addrs[:0])])
+    pending = [b0]
+    plan = plan_split(exchange.gather_counts(engine, b0, count_buf, scratch), vcm, dbcm)
     sent = {"counts": 8, "heads": 0, "entries": 0}
     if before_phase2 is not None:
         before_phase2()
+    lo, hi = slot_range(plan, rank)
+    arena = scratch.get("arena")
+    if arena is None or arena.nbytes < (hi - lo) * bs:
+        arena = scratch["arena"] = engine.alloc((hi - lo) * bs)
+    out = _Ptr(arena.ptr - lo * bs)  # slot 0 of the job's layout
+
     # Bodies at their global positions in the job's own block layout.
     if plan.counts[rank]:
-        r1, _ = run([Job(tree, seg_a, seg_b, job.a_immutable, job.drop_tombstones, job.level_b, job.cluster,
-                         job.snapshot_min, addrs, arena, flags=VALUES_ONLY, output_offset=plan.offsets[rank])])
-        assert r1.value_count == plan.counts[rank]
+        pending.append(engine.submit([job_of(VALUES_ONLY, out, plan.offsets[rank])]))
 
     def position_ptr(pos: int) -> int:
         k = pos // vcm
-        return arena.ptr + data_block_slot(k, dbcm) * bs + HEADER_SIZE + (pos - k * vcm) * vs
+        return out.ptr + data_block_slot(k, dbcm) * bs + HEADER_SIZE + (pos - k * vcm) * vs
 
     # The partial block's values to its owner.
     pos, h = plan.head(rank)
     sent["heads"] = h * vs
-    keep, ptrs = exchange.all_gather_heads(engine, [(position_ptr(pos), h * vs)] if h else [], plan.head_max * vs)
+    keep1, ptrs = exchange.all_gather_bytes(engine, [(position_ptr(pos), h * vs)] if h else [],
+                                            plan.head_max * vs, "heads", scratch)
     copies = []
     for q in range(len(plan.counts)):
         qpos, qh = plan.head(q)
@@ -450,38 +551,35 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
             copies.append((position_ptr(qpos), ptrs[q], qh * vs))
     if copies:
         engine.copy_device_batch(copies)
-        engine.synchronize()  # the gathered buffers are released below
-    del keep
     k0, k1 = plan.blocks(rank)
     t0, t1 = plan.tables(rank)
 
     def seal(blocks, tables):
-        return engine.seal(tree, job.cluster, job.snapshot_min, job.level_b, addrs, arena, plan.total, blocks, tables)
+        return engine.seal_submit(tree, job.cluster, job.snapshot_min, job.level_b, addrs, out, plan.total, blocks,
+                                  tables)
 
     if k1 > k0:
-        seal((k0, k1), (t0, t0))
+        pending.append(seal((k0, k1), (t0, t0)))
     # The index entries of a table an earlier rank owns, to that owner.
     t, s0, e = plan.entries(rank)
     sent["entries"] = e * entry_bytes(ks)
     mine = []
     if e:
-        image = arena.ptr + index_block_slot(t, plan.k_last(t)) * bs
-        mine = entry_ranges(image, s0, e, dbcm, ks)
-    keep, ptrs = exchange.all_gather_heads(engine, mine, plan.entries_max * entry_bytes(ks))
+        mine = entry_ranges(out.ptr + index_block_slot(t, plan.k_last(t)) * bs, s0, e, dbcm, ks)
+    keep2, ptrs = exchange.all_gather_bytes(engine, mine, plan.entries_max * entry_bytes(ks), "entries", scratch)
     copies = []
     for q in range(len(plan.counts)):
         qt, qs0, qe = plan.entries(q)
         if q != rank and qe and plan.table_owner(qt) == rank:
-            image = arena.ptr + index_block_slot(qt, plan.k_last(qt)) * bs
+            image = out.ptr + index_block_slot(qt, plan.k_last(qt)) * bs
             off = 0
             for dst, n in entry_ranges(image, qs0, qe, dbcm, ks):
                 copies.append((dst, ptrs[q] + off, n))
                 off += n
     if copies:
         engine.copy_device_batch(copies)
-        engine.synchronize()
-    del keep
-    result, infos = None, np.zeros((0, 128), dtype=np.uint8)
+    table_batch = None
     if t1 > t0:
-        result, infos = seal((k0, k0), (t0, t1))
-    return SplitResult((k0, k1), (t0, t1), result, infos, arena, plan, sent)
+        table_batch = seal((k0, k0), (t0, t1))
+        pending.append(table_batch)
+    return SplitResult((k0, k1), (t0, t1), plan, sent, arena, lo, bs, pending, table_batch, [keep1, keep2])
