@@ -2543,10 +2543,23 @@ int launch_blocks_front(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, 
 int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
                        JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
-                       void *stream, void (*mark)(void *, const char *), void *mark_ctx) {
+                       void *stream, void (*mark)(void *, const char *), void *mark_ctx, bool compact) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t waves = (total_dblocks + 1) / 2;
-    if (total_dblocks) {
+    if (total_dblocks && compact) {
+        // Grid batches: compact tables (72 KiB of LDS instead of 136), so the
+        // next batches' mask merges of multi-limb keys (33-49 KiB of keys in
+        // LDS: id and composite trees) and bar-end sorts fit beside them.
+        // Config 1 44.5 -> 41.9 ms (mask merges 13.7 -> 10.7 ms per step; the
+        // chains 115 -> 142 ms of summed time, off the critical path),
+        // gpurun_out/r05w. Non-grid batches keep the full tables (§4.1).
+        uint32_t c = waves > 512 ? 8u : 4u;
+        if (c > waves) c = waves;
+        hipLaunchKernelGGL((k_data_blocks<false, StepCompact>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs,
+                           njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
+                           d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
+        if (hipGetLastError() != hipSuccess) return -1;
+    } else if (total_dblocks) {
         if (waves <= 1024) { // latency regime: one chain per SIMD, round keys by VALU lane moves
             // A chain workgroup holds a whole CU's LDS (the tables), so
             // concurrent tails share the chip by CUs: pack four chain waves
@@ -2598,7 +2611,7 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
 // chain waves per workgroup, 8 above 512 waves); the round key comes by
 // VALU lane moves unless a half runs two chains per SIMD.
 int launch_blocks_tail_pair(const TailHalf &a, const TailHalf &b, void *stream, void (*mark)(void *, const char *),
-                            void *ctx_a, void *ctx_b) {
+                            void *ctx_a, void *ctx_b, bool compact) {
     hipStream_t s = (hipStream_t)stream;
     auto half = [](const TailHalf &t) {
         ChainHalf h{t.jobs, t.njobs, t.dblocks, t.res, t.ready, 0u, 0u};
@@ -2612,7 +2625,9 @@ int launch_blocks_tail_pair(const TailHalf &a, const TailHalf &b, void *stream, 
     const ChainHalf ha = half(a), hb = half(b);
     const uint32_t c = ha.c > hb.c ? ha.c : hb.c;
     if (ha.wgs + hb.wgs) {
-        if (c >= 8)
+        if (compact)
+            hipLaunchKernelGGL((k_data_blocks_pair<StepCompact>), dim3(ha.wgs + hb.wgs), dim3(64 * c), 0, s, ha, hb);
+        else if (c >= 8)
             hipLaunchKernelGGL((k_data_blocks_pair<StepBpermute>), dim3(ha.wgs + hb.wgs), dim3(64 * c), 0, s, ha, hb);
         else
             hipLaunchKernelGGL((k_data_blocks_pair<StepValuKey>), dim3(ha.wgs + hb.wgs), dim3(64 * c), 0, s, ha, hb);

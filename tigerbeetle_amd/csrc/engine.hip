@@ -1633,7 +1633,7 @@ static bool tail_chains(tbc_engine *e, tbc_batch *b, hipStream_t T, const JobDes
                         unsigned long long *d_done, bool wide) {
     if (!e->server)
         return launch_blocks_tail(d_jobs, njobs, dblocks, tables, d_res, d_infos, d_status, e->masks, d_block_tile,
-                                  d_splits, d_ready, T, mark_cb, b) == 0;
+                                  d_splits, d_ready, T, mark_cb, b, b->gt.grid != nullptr) == 0;
     if (!dblocks) return true;
     bool ok = hipStreamWaitEvent(e->chain_stream, b->fork, 0) == hipSuccess &&
               launch_chain_server(e->ring, b->chain_seq, wide ? e->wide_wgs : e->narrow_wgs,
@@ -1704,7 +1704,7 @@ static bool grid_tail_pair(tbc_engine *e, tbc_batch *p, tbc_batch *b) {
     p->mark_stream = b->mark_stream = T;
     mark_cb(p, "tail_wait");
     mark_cb(b, "tail_wait_paired");
-    ok = ok && launch_blocks_tail_pair(p->gt.half, b->gt.half, T, mark_cb, p, b) == 0;
+    ok = ok && launch_blocks_tail_pair(p->gt.half, b->gt.half, T, mark_cb, p, b, true) == 0;
     return ok && grid_tail_rest(e, p, ti) && grid_tail_rest(e, b, ti);
 }
 

@@ -405,11 +405,11 @@ struct ChainHalf { // k_data_blocks_pair's kernel argument
     uint32_t c, wgs; // chain waves per workgroup, workgroups
 };
 int launch_blocks_tail_pair(const TailHalf &a, const TailHalf &b, void *stream, void (*mark)(void *, const char *),
-                            void *ctx_a, void *ctx_b);
+                            void *ctx_a, void *ctx_b, bool compact = false);
 int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks, uint32_t total_tables,
                        JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
-                       void *stream, void (*mark)(void *, const char *), void *mark_ctx);
+                       void *stream, void (*mark)(void *, const char *), void *mark_ctx, bool compact = false);
 int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables, JobResultDev *d_results,
                         uint8_t *d_infos, void *stream);
 // tbc_compaction_seal (one seal job): chains + headers of its data blocks and
