@@ -1508,13 +1508,13 @@ constexpr uint32_t kMaxChainOnlyWaves = 16;
 // Above this many chain waves (2 per SIMD) the two-pass path wins.
 constexpr uint32_t kFusedMaxChainWaves = 2048;
 
-template <bool Fused, class ChainStep = StepBpermute>
+template <bool Fused, class ChainStep = StepBpermute, uint32_t kHdrMax = (Fused ? kMaxChainWaves : kMaxChainOnlyWaves)>
 __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res,
                                             const uint64_t *status, const uint64_t *masks,
                                             const uint32_t *block_tile, const SplitDesc *splits,
                                             uint32_t chain_waves, const uint32_t *ready, const SplitDesc *bsplits,
                                             uint32_t phase, uint32_t bid) {
-    constexpr uint32_t kHdrWaves = Fused ? kMaxChainWaves : kMaxChainOnlyWaves;
+    constexpr uint32_t kHdrWaves = kHdrMax; // header scratch: one row per chain wave of the workgroup
     using Layout = TableLayout<ChainStep>;
     __shared__ uint32_t sT[Layout::kDwords];
     __shared__ uint32_t sHdr[kHdrWaves][2][64];
@@ -1640,13 +1640,16 @@ __device__ __forceinline__ void data_blocks(const JobDesc *jobs, int njobs, uint
                                                           writer);
 }
 
-template <bool Fused, class ChainStep = StepBpermute>
+// kHdrMax: the most chain waves a launch's workgroups hold (their header
+// rows in LDS: 512 B each); tails of at most 8 chain waves per workgroup
+// take 4 KiB instead of 8, room for one more front workgroup on their CUs.
+template <bool Fused, class ChainStep = StepBpermute, uint32_t kHdrMax = (Fused ? kMaxChainWaves : kMaxChainOnlyWaves)>
 __global__ __launch_bounds__(Fused ? 3 * 64 * kMaxChainWaves : 1024) void k_data_blocks(
     const JobDesc *jobs, int njobs, uint32_t total, const JobResultDev *res, const uint64_t *status,
     const uint64_t *masks, const uint32_t *block_tile, const SplitDesc *splits, uint32_t chain_waves,
     const uint32_t *ready, const SplitDesc *bsplits, uint32_t phase) {
-    data_blocks<Fused, ChainStep>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves, ready,
-                                  bsplits, phase, blockIdx.x);
+    data_blocks<Fused, ChainStep, kHdrMax>(jobs, njobs, total, res, status, masks, block_tile, splits, chain_waves,
+                                           ready, bsplits, phase, blockIdx.x);
 }
 
 // Two grid batches' chains in one launch (tail pairing, engine.hip
@@ -1656,8 +1659,8 @@ template <class ChainStep>
 __global__ __launch_bounds__(1024) void k_data_blocks_pair(ChainHalf a, ChainHalf b) {
     const bool second = blockIdx.x >= a.wgs;
     const ChainHalf &x = second ? b : a;
-    data_blocks<false, ChainStep>(x.jobs, x.njobs, x.total, x.res, nullptr, nullptr, nullptr, nullptr, x.c, x.ready,
-                                  nullptr, 0u, second ? blockIdx.x - a.wgs : blockIdx.x);
+    data_blocks<false, ChainStep, 8>(x.jobs, x.njobs, x.total, x.res, nullptr, nullptr, nullptr, nullptr, x.c,
+                                     x.ready, nullptr, 0u, second ? blockIdx.x - a.wgs : blockIdx.x);
 }
 
 // The recomputation of broken speculations (phase 1) in its own symbol, so
@@ -2555,7 +2558,7 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
         // gpurun_out/r05w. Non-grid batches keep the full tables (§4.1).
         uint32_t c = waves > 512 ? 8u : 4u;
         if (c > waves) c = waves;
-        hipLaunchKernelGGL((k_data_blocks<false, StepCompact>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs,
+        hipLaunchKernelGGL((k_data_blocks<false, StepCompact, 8>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s, d_jobs,
                            njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks, d_block_tile,
                            d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -2575,11 +2578,11 @@ int launch_blocks_tail(const JobDesc *d_jobs, int njobs, uint32_t total_dblocks,
             // throughput regime does.
             const bool bperm = c >= 8;
             if (bperm)
-                hipLaunchKernelGGL((k_data_blocks<false, StepBpermute>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                hipLaunchKernelGGL((k_data_blocks<false, StepBpermute, 8>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
                                    d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
                                    d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
             else
-                hipLaunchKernelGGL((k_data_blocks<false, StepValuKey>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
+                hipLaunchKernelGGL((k_data_blocks<false, StepValuKey, 8>), dim3((waves + c - 1) / c), dim3(64 * c), 0, s,
                                    d_jobs, njobs, total_dblocks, (const JobResultDev *)d_results, d_status, d_masks,
                                    d_block_tile, d_splits, c, d_ready, (const SplitDesc *)nullptr, 0u);
         } else {
