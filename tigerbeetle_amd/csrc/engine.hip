@@ -527,7 +527,7 @@ static bool join_sorts(tbc_engine *e) {
 
 // Every stream of the engine drained (internal: no deferred-error report).
 static bool sync_streams(tbc_engine *e);
-static void flush_tail(tbc_engine *e);
+static void flush_tail(tbc_engine *e, bool drain = false);
 static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count);
 
 // Later work on the engine stream that touches grid blocks (staging blocks in
@@ -1119,7 +1119,7 @@ tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes
 
 static bool sync_streams(tbc_engine *e) {
     hipSetDevice(e->device);
-    flush_tail(e);
+    flush_tail(e, true);
     bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
     for (int t = 0; t < e->ntails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
     ok = ok && (!e->sort_stream || hipStreamSynchronize(e->sort_stream) == hipSuccess);
@@ -1630,10 +1630,10 @@ static bool publish_chains(tbc_engine *e, tbc_batch *b, const JobDesc *d_jobs, i
 static bool tail_chains(tbc_engine *e, tbc_batch *b, hipStream_t T, const JobDesc *d_jobs, int njobs, uint32_t dblocks,
                         uint32_t tables, JobResultDev *d_res, uint8_t *d_infos, const uint64_t *d_status,
                         const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
-                        unsigned long long *d_done, bool wide) {
+                        unsigned long long *d_done, bool wide, bool compact) {
     if (!e->server)
         return launch_blocks_tail(d_jobs, njobs, dblocks, tables, d_res, d_infos, d_status, e->masks, d_block_tile,
-                                  d_splits, d_ready, T, mark_cb, b, b->gt.grid != nullptr) == 0;
+                                  d_splits, d_ready, T, mark_cb, b, compact) == 0;
     if (!dblocks) return true;
     bool ok = hipStreamWaitEvent(e->chain_stream, b->fork, 0) == hipSuccess &&
               launch_chain_server(e->ring, b->chain_seq, wide ? e->wide_wgs : e->narrow_wgs,
@@ -1673,8 +1673,12 @@ static int take_tail(tbc_engine *e) {
     return ti;
 }
 
-// A grid batch's whole tail on the next tail stream, after its front.
-static bool grid_tail_alone(tbc_engine *e, tbc_batch *b) {
+static const bool drain_full = getenv("TBC_DRAIN_COMPACT") == nullptr; // A/B: drains on compact tables too
+
+// A grid batch's whole tail on the next tail stream, after its front. A
+// drain (the caller waits next: no front follows to share the CUs with)
+// runs the chains on the full tables, one chain per SIMD (latency regime).
+static bool grid_tail_alone(tbc_engine *e, tbc_batch *b, bool drain) {
     const auto &g = b->gt;
     const int ti = take_tail(e);
     hipStream_t T = e->tail[ti];
@@ -1683,7 +1687,7 @@ static bool grid_tail_alone(tbc_engine *e, tbc_batch *b) {
     mark_cb(b, "tail_wait");
     if (ok && g.half.njobs)
         ok = tail_chains(e, b, T, g.half.jobs, g.half.njobs, g.half.dblocks, g.half.tables, g.half.res, g.half.infos,
-                         g.status, g.block_tile, g.splits, g.half.ready, g.done_ctr, g.wide);
+                         g.status, g.block_tile, g.splits, g.half.ready, g.done_ctr, g.wide, !(drain && drain_full));
     return ok && grid_tail_rest(e, b, ti);
 }
 
@@ -1708,11 +1712,11 @@ static bool grid_tail_pair(tbc_engine *e, tbc_batch *p, tbc_batch *b) {
     return ok && grid_tail_rest(e, p, ti) && grid_tail_rest(e, b, ti);
 }
 
-static void flush_tail(tbc_engine *e) {
+static void flush_tail(tbc_engine *e, bool drain) {
     tbc_batch *p = e ? e->deferred : nullptr;
     if (!p) return;
     e->deferred = nullptr;
-    if (!grid_tail_alone(e, p)) {
+    if (!grid_tail_alone(e, p, drain)) {
         p->complete = true;
         p->result = TBC_ERR_DEVICE;
     }
@@ -2160,7 +2164,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
             e->deferred = b;
         } else if (ok) {
             flush_tail(e);
-            ok = grid_tail_alone(e, b);
+            ok = grid_tail_alone(e, b, false);
         }
     } else if (pipeline) {
         // A group of a split batch: front (merge + bodies) on the engine
@@ -2183,7 +2187,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         mark_cb(b, "tail_wait");
         if (ok && count)
             ok = tail_chains(e, b, T, (const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
-                             d_block_tile, d_splits, d_ready, d_done, wide_front);
+                             d_block_tile, d_splits, d_ready, d_done, wide_front, false);
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {
@@ -2241,7 +2245,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         b->mark_stream = T;
         mark_cb(b, "tail_wait");
         ok = ok && tail_chains(e, b, T, dj, (int)count, dblocks, tables, d_res, d_infos, d_status, d_block_tile,
-                               d_splits, d_ready, d_done, wide_front);
+                               d_splits, d_ready, d_done, wide_front, false);
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {
@@ -2580,7 +2584,7 @@ tbc_status tbc_batch_poll(tbc_batch *b) {
 }
 
 tbc_status tbc_batch_wait(tbc_batch *b) {
-    flush_tail(b ? b->engine : nullptr);
+    flush_tail(b ? b->engine : nullptr, true);
     if (!b) return TBC_ERR_INVALID_ARGUMENT;
     if (b->complete) return b->result;
     if (!b->children.empty()) return parent_finish(b, true);
