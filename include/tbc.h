@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TBC_ABI_VERSION 5u
+#define TBC_ABI_VERSION 6u
 
 typedef enum tbc_status {
     TBC_OK = 0,
@@ -471,6 +471,11 @@ tbc_status tbc_batch_result(tbc_batch *batch, uint32_t index, tbc_compaction_res
 #define TBC_SPECULATION_HELD 1u
 #define TBC_SPECULATION_BROKEN 2u
 tbc_status tbc_batch_speculation(tbc_batch *batch, uint32_t index, uint32_t *out_outcome);
+/* TBC_CONFIG_PROFILE on (1) or off (0) for the batches submitted after this
+ * call; a batch keeps what it was submitted with. The marks cost the engine
+ * stream time (config 1: ~1.3 ms per 40 ms step), so a timed loop runs
+ * without them and profiled steps follow it. */
+tbc_status tbc_engine_set_profile(tbc_engine *engine, uint32_t on);
 /* Per-kernel device times of the batch in microseconds (TBC_CONFIG_PROFILE).
  * names/us are host arrays of `capacity` entries; returns the entry count in *out_count. */
 tbc_status tbc_batch_kernel_times(tbc_batch *batch, const char **names, double *us, uint32_t capacity,

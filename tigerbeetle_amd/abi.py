@@ -37,7 +37,7 @@ COMPACTION_GRID = 2
 COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped
 COMPACTION_COUNT_ONLY = 8  # the merge alone: survivor counts (phase A of a split job)
 SPECULATION_NONE, SPECULATION_HELD, SPECULATION_BROKEN = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class TbcError(RuntimeError):
@@ -212,6 +212,7 @@ _SIGNATURES = {
     "tbc_memtable_values": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint32)]),
     "tbc_memtable_reset": (ctypes.c_int, [_P]),
     "tbc_engine_stream": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    "tbc_engine_set_profile": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "tbc_memtable_make_immutable": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, ctypes.c_uint32]),
 }
 

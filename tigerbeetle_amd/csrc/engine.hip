@@ -488,7 +488,7 @@ static void mark_cb(void *ctx, const char *name) {
     tbc_batch *b = (tbc_batch *)ctx;
     hipStream_t s = b->mark_stream ? b->mark_stream : b->engine->stream;
     debug_stage(s, name);
-    if (!(b->engine->flags & TBC_CONFIG_PROFILE) || b->nmarks >= kMaxMarks) return;
+    if (!b->marks[0] || b->nmarks >= kMaxMarks) return; // profiled iff submitted with TBC_CONFIG_PROFILE
     hipEventRecord(b->marks[b->nmarks], s);
     b->mark_names[b->nmarks++] = name;
 }
@@ -542,6 +542,12 @@ static bool join_tails(tbc_engine *e) {
 extern "C" {
 
 uint32_t tbc_abi_version(void) { return TBC_ABI_VERSION; }
+
+tbc_status tbc_engine_set_profile(tbc_engine *e, uint32_t on) {
+    if (!e) return TBC_ERR_INVALID_ARGUMENT;
+    e->flags = on ? (e->flags | TBC_CONFIG_PROFILE) : (e->flags & ~(uint32_t)TBC_CONFIG_PROFILE);
+    return TBC_OK;
+}
 
 tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     if (!config || !out_engine) return TBC_ERR_INVALID_ARGUMENT;

@@ -480,6 +480,11 @@ class Engine:
         check(lib().tbc_compaction_submit(self.handle, arr, len(jobs), ctypes.byref(h)), "tbc_compaction_submit")
         return Batch(self, h.value, jobs)
 
+    def set_profile(self, on: bool) -> None:
+        """Profile marks (kernel_times) for the batches submitted from now on
+        (tbc_engine_set_profile): timed loops run without them."""
+        check(lib().tbc_engine_set_profile(self.handle, 1 if on else 0), "tbc_engine_set_profile")
+
     def stream_handle(self) -> int:
         """The engine stream (tbc_engine_stream), for torch.cuda.ExternalStream."""
         p = ctypes.c_void_p()
