@@ -2106,9 +2106,9 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                 for (const auto &g : seg_in[2 * (size_t)i + side])
                     if (g.first && !(ok = wait_sorts(e, g.first, g.first + (uint64_t)g.second * hj[i].value_size)))
                         break;
-    ok = ok && launch_upload(d_in, h_in, sz_in, s) == 0;
-    // Tile status, block tiles and results start zeroed (contiguous).
-    ok = ok && hipMemsetAsync(d_status, 0, sz_tiles + sz_res, s) == hipSuccess;
+    // The descriptors up; tile status, block tiles and results zeroed
+    // (contiguous) by the same launch.
+    ok = ok && launch_upload(d_in, h_in, sz_in, s, d_status, sz_tiles + sz_res) == 0;
     mark_cb(b, "start");
     if (grid_mode) {
         // Pipelined: the front (input data blocks found through their index

@@ -206,24 +206,33 @@ uint64_t copy_chunk_bytes() { return kCopyChunk; }
 // The host rewrites a slot once the stream has passed its previous upload,
 // so the source is read at system scope (no cache may hold the old bytes).
 __global__ __launch_bounds__(256) void k_upload(uint64_t *dst, const uint64_t *src, uint64_t n8, uint8_t *dst_tail,
-                                               const uint8_t *src_tail, uint32_t tail) {
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256)
+                                               const uint8_t *src_tail, uint32_t tail, uint64_t *zero, uint64_t zero8) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride)
         dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (blockIdx.x == 0 && threadIdx.x < tail)
         dst_tail[threadIdx.x] = __hip_atomic_load(src_tail + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < zero8; i += stride) zero[i] = 0;
 }
 
-int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream) {
+int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream, void *zero, uint64_t zero_bytes) {
     hipStream_t s = (hipStream_t)stream;
-    if (!bytes) return 0;
-    if (((uintptr_t)dst | (uintptr_t)host_src) & 7)
-        return hipMemcpyAsync(dst, host_src, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
-    const uint64_t n8 = bytes / 8;
+    if (zero_bytes && (((uintptr_t)zero | zero_bytes) & 7)) { // not whole words: a fill of its own
+        if (hipMemsetAsync(zero, 0, zero_bytes, s) != hipSuccess) return -1;
+        zero_bytes = 0;
+    }
+    if (!bytes && !zero_bytes) return 0;
+    if (((uintptr_t)dst | (uintptr_t)host_src) & 7) {
+        if (bytes && hipMemcpyAsync(dst, host_src, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+        bytes = 0;
+        if (!zero_bytes) return 0;
+    }
+    const uint64_t n8 = bytes / 8, z8 = zero_bytes / 8;
     const uint32_t tail = (uint32_t)(bytes - 8 * n8);
-    const uint64_t blocks = (n8 + 255) / 256;
+    const uint64_t blocks = ((n8 > z8 ? n8 : z8) + 255) / 256;
     hipLaunchKernelGGL(k_upload, dim3((uint32_t)(blocks < 512 ? (blocks ? blocks : 1) : 512)), dim3(256), 0, s,
                        (uint64_t *)dst, (const uint64_t *)host_src, n8, (uint8_t *)dst + 8 * n8,
-                       (const uint8_t *)host_src + 8 * n8, tail);
+                       (const uint8_t *)host_src + 8 * n8, tail, (uint64_t *)zero, z8);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) fprintf(stderr, "tbc: upload of %llu bytes: %s (%d)\n", (unsigned long long)bytes,
                                    hipGetErrorString(err), (int)err);

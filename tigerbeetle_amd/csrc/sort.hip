@@ -1040,15 +1040,8 @@ int launch_sort_batch(const SortItem *items, uint32_t count, void *scratch, uint
     uint32_t *hist = (uint32_t *)(base + L.hist), *bins = (uint32_t *)(base + L.bins);
     uint32_t *counters = (uint32_t *)(base + L.counters);
     SortBatch *d_batch = (SortBatch *)(base + L.batch);
-    if (launch_upload(base, hbase, L.hist, s) != 0) return -4;
-    {
-        const hipError_t err = hipMemsetAsync(hist, 0, L.bins - L.hist, s);
-        if (err != hipSuccess) {
-            fprintf(stderr, "tbc: sort memset %p %llu: %s\n", (void *)hist, (unsigned long long)(L.bins - L.hist),
-                    hipGetErrorString(err));
-            return -6;
-        }
-    }
+    // Descriptors up and the histograms, counters and batch words zeroed, one launch.
+    if (launch_upload(base, hbase, L.hist, s, hist, L.bins - L.hist) != 0) return -4;
     hipLaunchKernelGGL(k_sort_extract, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile);
     hipLaunchKernelGGL(k_sort_layout, dim3(nseg), dim3(64), 0, s, d_segs);
     hipLaunchKernelGGL(k_sort_pack, dim3(ntiles), dim3(kSortThreads), 0, s, d_segs, d_tile, words0, hist);

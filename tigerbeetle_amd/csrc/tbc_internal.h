@@ -361,7 +361,10 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 // the recomputation phase).
 // A pinned host buffer to device memory by a compute kernel on `stream`
 // (grid.hip k_upload).
-int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream);
+// zero_bytes at `zero` are cleared by the same launch (a batch's zeroed
+// scratch: one kernel instead of an upload and a fill).
+int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream, void *zero = nullptr,
+                  uint64_t zero_bytes = 0);
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
                         JobResultDev *d_results, uint32_t *d_ticket, void *stream, void (*mark)(void *, const char *),
                         void *mark_ctx);
