@@ -395,6 +395,35 @@ def test_sort_values_batch_out_of_place(engine, oracle_lib):
         engine.sort_values_batch([(spec, src, 100, src.ptr + 16 * spec.value_size)])
 
 
+def test_sort_values_batch_more_tiles_than_workgroups(engine, oracle_lib):
+    """A batch of more 4,096-item tiles than the pass kernel keeps resident
+    (3 x 256 workgroups): its passes take tiles by ticket; smaller batches
+    give each tile its own workgroup (sort.hip sort_pass_tiles). Both
+    orders, bit-exact vs the oracle's stable sort: random u128 ids (top-digit
+    passes + run fixup) and a composite index with repeated accounts."""
+    rng = np.random.default_rng(21)
+    cases = []
+    for name, n in (("transfers.id", 2_600_000), ("transfers.debit_account_id", 900_000)):
+        spec = trees.BY_NAME[name]
+        limbs = workloads.random_keys(spec, n, rng, field_max=None if name == "transfers.id" else 10_000)
+        vals = workloads.values_from_keys(spec, limbs, rng.random(n) < 0.01, rng)
+        t = oracle_lib.tree(spec.tree_id, spec.key_kind, spec.usage, spec.value_size, spec.timestamp_offset,
+                            spec.value_count_max, 1 << 20)
+        cases.append((spec, vals, oracle_lib.sort_values(t, vals)))
+    assert sum(-(-len(v) // 4096) for _, v, _ in cases) > 3 * 256
+    jobs, keep = [], []
+    for spec, vals, want in cases:
+        src = engine.upload(vals, pad=16)
+        dst = engine.upload(np.zeros_like(vals), pad=16)
+        keep.append((spec, vals, want, dst))
+        jobs.append((spec, src, len(vals), dst.ptr))
+    engine.sort_values_batch(jobs)
+    engine.synchronize()
+    for spec, vals, want, dst in keep:
+        n = len(vals)
+        assert np.array_equal(dst.download(n * spec.value_size).reshape(n, spec.value_size), want), spec.name
+
+
 def test_memtable_make_immutable(engine, oracle_lib):
     """tbc_memtable_make_immutable at a bar end: each mutable table's values
     become its immutable table's in key order (sorted out of place, or the
