@@ -206,6 +206,10 @@ struct tbc_engine {
     // it only grows (after a stream drain), which a steady-state caller sees once.
     uint64_t *masks = nullptr;
     uint64_t mask_words = 0;
+    // The last seal (tbc_compaction_seal, on a tail stream): engine-stream
+    // copies wait for it (they may read the index entries it wrote).
+    hipEvent_t seal_ev = nullptr;
+    bool seal_pending = false;
     // Memtable sort scratch (keys, indices, histograms, look-back words, the
     // tables' copies): grown on demand like the masks.
     uint8_t *sort_scratch = nullptr;
@@ -539,6 +543,13 @@ static bool join_tails(tbc_engine *e) {
     return join_sorts(e);
 }
 
+// Engine-stream copies may read what the last seal (on a tail) wrote.
+static bool wait_seal(tbc_engine *e) {
+    if (!e->seal_pending) return true;
+    e->seal_pending = false; // the engine stream is ordered after it from here on
+    return hipStreamWaitEvent(e->stream, e->seal_ev, 0) == hipSuccess;
+}
+
 extern "C" {
 
 uint32_t tbc_abi_version(void) { return TBC_ABI_VERSION; }
@@ -608,6 +619,7 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     for (int t = 0; ok && t < e->ntails; t++)
         ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, high ? prio_greatest : 0) == hipSuccess &&
              hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&e->seal_ev, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
     // The sort stream exists only when asked for (TBC_SORT_STREAM=1): a
@@ -698,6 +710,7 @@ void tbc_engine_deinit(tbc_engine *e) {
         if (e->tail_ev[t]) hipEventDestroy(e->tail_ev[t]);
         if (e->tail[t]) hipStreamDestroy(e->tail[t]);
     }
+    if (e->seal_ev) hipEventDestroy(e->seal_ev);
     hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1041,7 +1054,8 @@ tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (!wait_sorts_ptr(e, dst, bytes) || hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    if (!wait_seal(e) || !wait_sorts_ptr(e, dst, bytes) ||
+        hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
         return TBC_ERR_DEVICE;
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
@@ -1051,7 +1065,7 @@ tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t 
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (!wait_sorts_ptr(e, src, bytes) || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+    if (!wait_seal(e) || !wait_sorts_ptr(e, src, bytes) || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
         return TBC_ERR_DEVICE;
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
@@ -1059,7 +1073,7 @@ tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t 
 tbc_status tbc_copy_device_async(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
     if (!e || (bytes && (!dst || !src))) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    if (!wait_sorts_ptr(e, dst, bytes) || !wait_sorts_ptr(e, src, bytes)) return TBC_ERR_DEVICE;
+    if (!wait_seal(e) || !wait_sorts_ptr(e, dst, bytes) || !wait_sorts_ptr(e, src, bytes)) return TBC_ERR_DEVICE;
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, e->stream) == hipSuccess ? TBC_OK
                                                                                           : TBC_ERR_DEVICE;
 }
@@ -1070,6 +1084,7 @@ tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t
     for (uint32_t i = 0; i < count; i++)
         if (copies[i].bytes && (!copies[i].dst || !copies[i].src)) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
+    if (!wait_seal(e)) return TBC_ERR_DEVICE;
     std::vector<CopyItem> items;
     uint64_t chunks = 0;
     const uint64_t cb = copy_chunk_bytes();
@@ -1118,7 +1133,7 @@ tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (!wait_sorts_ptr(e, dst, bytes) || hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess)
+    if (!wait_seal(e) || !wait_sorts_ptr(e, dst, bytes) || hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess)
         return TBC_ERR_DEVICE;
     return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
 }
@@ -2532,13 +2547,34 @@ tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **ou
     b->h_results = (JobResultDev *)(hbase + sz_job + sz_addr);
     b->h_infos = hbase + sz_job + sz_addr + sz_res;
     b->done = take_event(e);
-    hipStream_t s = e->stream;
-    bool ok = b->done != nullptr && join_tails(e) &&
-              hipMemcpyAsync(dbase, hbase, sz_job + sz_addr + sz_res, hipMemcpyHostToDevice, s) == hipSuccess &&
-              launch_seal((const JobDesc *)dbase, sl->block_count, sl->table_count, d_res,
-                          dbase + sz_job + sz_addr + sz_res, s) == 0 &&
-              hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, s) == hipSuccess &&
-              hipEventRecord(b->done, s) == hipSuccess;
+    b->fork = take_event(e);
+    // On a tail stream (round 5): after the engine stream's work so far (the
+    // bodies it seals) and after every tail (blocks an earlier seal or batch
+    // tail still writes), so the engine stream runs on — a split's seal
+    // chains beside the next fronts. Engine-stream copies that read what a
+    // seal wrote wait for it (seal_ev, tbc_copy_device_batch).
+    const int ti = take_tail(e);
+    hipStream_t T = e->tail[ti];
+    bool ok = b->done != nullptr && b->fork != nullptr && hipEventRecord(b->fork, e->stream) == hipSuccess &&
+              hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
+    for (int o = 0; ok && o < e->ntails; o++)
+        if (o != ti) ok = hipStreamWaitEvent(T, e->tail_ev[o], 0) == hipSuccess;
+    ok = ok && hipMemcpyAsync(dbase, hbase, sz_job + sz_addr + sz_res, hipMemcpyHostToDevice, T) == hipSuccess &&
+         launch_seal((const JobDesc *)dbase, sl->block_count, sl->table_count, d_res, dbase + sz_job + sz_addr + sz_res,
+                     T) == 0 &&
+         hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess &&
+         hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess &&
+         hipEventRecord(e->seal_ev, T) == hipSuccess;
+    e->seal_pending = ok;
+    if (ok) { // a later batch into these blocks starts after this seal (submit's tail_out check)
+        tbc_engine::TailOutputs to;
+        to.done = take_event(e);
+        ok = to.done && hipEventRecord(to.done, T) == hipSuccess;
+        const uint64_t lo = (uint64_t)(uintptr_t)sl->output_blocks;
+        to.ranges.push_back({lo, lo + (uint64_t)sl->address_count * e->block_size});
+        if (ok) e->tail_out.push_back(std::move(to));
+        else if (to.done) e->event_pool.push_back(to.done);
+    }
     if (!ok) {
         sync_streams(e);
         tbc_batch_release(b);

@@ -382,7 +382,9 @@ class TorchExchange:
         for ptr, n in segments:
             engine.copy_device_async(staging.ptr + off, ptr, n)
             off += n
-        engine.synchronize()
+        # The download waits for the engine stream (the copies above, after
+        # the bodies) and the last seal (the entries it wrote), not for other
+        # batches' tails.
         host[:] = staging.download(nbytes)
         mine = torch.from_numpy(host)
         out = [torch.empty_like(mine) for _ in range(self.world)]
@@ -480,9 +482,9 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     [cuts[rank], cuts[rank+1]) of A and of B (what rank_blocks named, staged
     on this GPU); otherwise the whole job's inputs, sliced here. `scratch` (a
     dict kept by a caller that repeats the split) keeps the output slots and
-    exchange buffers between steps; `before_phase2` runs once the counts are
-    exchanged, just before the bodies are placed (a caller enqueues its other
-    work there).
+    exchange buffers between steps; `before_phase2` runs once the bodies,
+    the partial blocks and the data-block seal are enqueued (a caller enqueues
+    its other work there: the seal's chains run on a tail stream beside it).
 
     Host waits: one, reading the gathered counts (the plan — every offset,
     block and table range — is host arithmetic on them), when the exchange
@@ -523,8 +525,6 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
     pending = [b0]
     plan = plan_split(exchange.gather_counts(engine, b0, count_buf, scratch), vcm, dbcm)
     sent = {"counts": 8, "heads": 0, "entries": 0}
-    if before_phase2 is not None:
-        before_phase2()
     lo, hi = slot_range(plan, rank)
     arena = scratch.get("arena")
     if arena is None or arena.nbytes < (hi - lo) * bs:
@@ -560,6 +560,11 @@ def compact_split(engine, job, cuts: list, exchange, rank: int, staged: bool = F
 
     if k1 > k0:
         pending.append(seal((k0, k1), (t0, t0)))
+    # The caller's other work (the rank's whole jobs) goes on the engine
+    # stream here: the data-block seal's chains run on a tail beside it, and
+    # an exchange through host memory waits for it only at the entries.
+    if before_phase2 is not None:
+        before_phase2()
     # The index entries of a table an earlier rank owns, to that owner.
     t, s0, e = plan.entries(rank)
     sent["entries"] = e * entry_bytes(ks)
