@@ -114,7 +114,15 @@ __device__ __forceinline__ uint32_t merge_path_split_wave(const JobDesc &j, uint
 // ~50 -> ~36 us per batch); with many splits (configs 2-5: tens of
 // thousands) the 64 probes per round cost more bandwidth than the rounds
 // save (config 2's k_partition_unique 49 -> 135 us), so one thread per split.
+// The mask merges' partitions switch at 12,288 splits (config 1's
+// partitions 2.45 -> 2.16 ms per step; at 32,768 config 5's grew 192 -> 500
+// us), the unique merges' at 4,096.
 constexpr uint32_t kWaveSplitsMax = 4096;
+constexpr uint32_t kWaveSplitsMaxMask = 12288;
+static uint32_t wave_splits_max() { // A/B: TBC_WAVE_SPLITS
+    static const uint32_t v = getenv("TBC_WAVE_SPLITS") ? (uint32_t)atoi(getenv("TBC_WAVE_SPLITS")) : kWaveSplitsMaxMask;
+    return v;
+}
 
 template <int KIND, bool Wave>
 __device__ __forceinline__ uint32_t split_at(const JobDesc &j, uint32_t d) {
@@ -844,7 +852,7 @@ int launch_merge(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitD
     {
         const JobDesc &l = h_jobs[njobs - 1];
         const uint32_t nsplits = l.split_base + l.tile_count + 1;
-        if (nsplits <= kWaveSplitsMax)
+        if (nsplits <= wave_splits_max())
             hipLaunchKernelGGL(k_partition_all<true>, dim3((nsplits + 3) / 4), dim3(256), 0, s, d_jobs, njobs, nsplits,
                            d_splits, (const JobResultDev *)d_results, phase);
         else
