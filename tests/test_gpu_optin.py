@@ -18,6 +18,10 @@ changes; each of those tests compares with the oracle.
   TBC_SERVER_WAVES=4,                      leave at once and poll slowly; two
   TBC_CHAIN_LINGER_US=0,                   job groups in the throughput regime
   TBC_CHAIN_BACKOFF=128, TBC_GROUPS=2
+  TBC_SORT_TICKETS=1, TBC_WAVE_SPLITS=4096,  sort passes take tiles by ticket,
+  TBC_DRAIN_COMPACT=1                      mask-merge partitions by thread above
+                                           4,096 splits, drained grid tails on
+                                           the compact tables (round 5 A/B)
 
 GPU_MAX_HW_QUEUES is HIP's own (the engine sizes its tails from it).
 """
@@ -95,3 +99,13 @@ def test_chain_server_bit_exact():
 def test_small_chain_server_bit_exact():
     _child({"TBC_CHAIN_SERVER": "1", "TBC_SERVER_WGS": "64", "TBC_SERVER_WAVES": "4", "TBC_CHAIN_LINGER_US": "0",
             "TBC_CHAIN_BACKOFF": "128", "TBC_GROUPS": "2"}, FILES, PIPELINED)
+
+
+@pytest.mark.gpu
+def test_round5_ab_knobs_bit_exact():
+    """The round-5 A/B knobs restore the earlier paths: the sort and grid
+    tests (tickets in every pass, thread partitions, compact drained tails)
+    and the 11-bar config-1 lockstep."""
+    env = {"TBC_SORT_TICKETS": "1", "TBC_WAVE_SPLITS": "4096", "TBC_DRAIN_COMPACT": "1"}
+    _child(env, FILES, PIPELINED + " or test_sort_values")
+    _child(env, ("test_gpu_config1.py",), "checkpoint", timeout=300)
