@@ -264,7 +264,8 @@ class ReplayWorkload:
             if kind == "sort":  # from the put-order copy straight into the immutable buffer
                 eng.sort_values_batch(rest[0])
             elif kind == "checkpoint":  # the replica checkpoints with no grid IO in flight
-                eng.synchronize()
+                if not os.environ.get("TBC_BENCH_NO_CHECKPOINT_WAIT"):  # A/B: what the drain costs
+                    eng.synchronize()
             elif kind == "restart":
                 raise RuntimeError("a benchmark replay never restarts")
             elif kind == "manifest":  # ManifestLog.close_block on the device (manifest.py)
