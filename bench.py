@@ -537,7 +537,7 @@ def measure_pcie(eng: Engine, blocks_in: int, blocks_out: int, bs: int, cap: int
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=[1] + sorted(configs.GENERATORS))
     ap.add_argument("--transfers", type=int, default=benchmark_load.TRANSFER_COUNT,

@@ -59,18 +59,48 @@ def test_arena_bounded_with_a_batch_in_flight(engine):
         b.release()
         assert engine.arena_usage() == after_held
     assert peak[0] < after_held[0] + (1 << 20) and peak[1] < after_held[1] + (1 << 20)
-    # Out of order: the lower region closes first, the top stays until the upper one closes.
+    # Out of order: the older region is reclaimed as soon as it closes.
     b1, b2 = engine.submit([keep1[2]]), engine.submit([keep1[2]])
     b1.wait()
     b2.wait()
     top2 = engine.arena_usage()
     b1.release()
-    assert engine.arena_usage()[:2] == top2[:2]
+    mid = engine.arena_usage()
+    assert mid[0] < top2[0] and mid[1] < top2[1] and mid[2] == top2[2] - 2
     b2.release()
     assert engine.arena_usage() == after_held
     held.wait()
     held.release()
     assert engine.arena_usage() == base
+
+
+def test_arena_reclaims_a_pipelined_stream_of_batches(engine):
+    """A caller that always keeps batches in flight and releases the oldest
+    first (a replica's steady state): the arena's use stays that of the
+    batches in flight over many times its size in total (round 4's stack
+    reclaimed nothing until every newer region closed, and ran out)."""
+    spec = trees.BY_NAME["transfers.id"]
+    rng = np.random.default_rng(0xA7F)
+    base = engine.arena_usage()
+    jobs = [_small_job(engine, spec, rng) for _ in range(3)]
+    b = engine.submit([jobs[0][2]])
+    one = [u - v for u, v in zip(engine.arena_usage()[:2], base[:2])]  # one batch's device and pinned bytes
+    b.wait()
+    b.release()
+    pending, peak = [], (0, 0)
+    for i in range(600):
+        pending.append(engine.submit([jobs[i % 3][2]]))
+        peak = max(peak, engine.arena_usage()[:2])
+        if len(pending) == 3:
+            b = pending.pop(0)
+            b.wait()
+            assert b.result(0)[0].status == 0
+            b.release()
+    for b in pending:
+        b.wait()
+        b.release()
+    assert engine.arena_usage() == base
+    assert peak[0] <= base[0] + 3 * one[0] and peak[1] <= base[1] + 3 * one[1]
 
 
 def test_pipelined_grid_batches_in_flight(engine, oracle_lib):

@@ -38,37 +38,49 @@ uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // below it, so regions released out of order are reclaimed as soon as the
 // ones above them are; the top never grows past the live regions' extent.
 // (Synchronous calls take scratch above the top with alloc() and restore it.)
+// Device scratch and pinned staging of the batches in flight. Regions are
+// closed in any order (a pipelined caller releases its oldest batch first
+// while newer ones run); an allocation takes the first gap at or after the
+// end of the last one, else the first gap from the start (next fit), so a
+// steady stream of batches cycles through the arena. (Round 4's stack freed
+// a region only once every region above it had closed: a caller that always
+// kept a batch in flight never reclaimed anything and ran out after a few
+// hundred batches.)
 struct Arena {
     struct Region {
-        uint64_t start, end;
-        bool open;
+        uint64_t start, end, id;
     };
     uint8_t *base = nullptr;
-    uint64_t size = 0, top = 0;
-    std::vector<Region> regions;
-    uint8_t *alloc(uint64_t bytes) {
-        uint64_t start = align_up(top, 256);
-        if (start + bytes > size) return nullptr;
-        top = start + bytes;
-        return base + start;
+    uint64_t size = 0, cursor = 0, next_id = 1, used = 0;
+    std::vector<Region> regions; // open, by start
+    // A region of `bytes`; *id identifies it for close().
+    uint8_t *open(uint64_t bytes, uint64_t *id) {
+        bytes = align_up(bytes ? bytes : 1, 256);
+        for (int pass = 0; pass < 2; pass++) {
+            uint64_t prev = 0;
+            for (size_t i = 0; i <= regions.size(); i++) {
+                const uint64_t gap_end = i < regions.size() ? regions[i].start : size;
+                uint64_t s = prev;
+                if (pass == 0) s = std::max(s, cursor); // next fit: at or after the last allocation
+                if (s + bytes <= gap_end) {
+                    regions.insert(regions.begin() + (long)i, Region{s, s + bytes, next_id});
+                    *id = next_id++;
+                    cursor = s + bytes;
+                    used += bytes;
+                    return base + s;
+                }
+                if (i < regions.size()) prev = regions[i].end;
+            }
+        }
+        return nullptr;
     }
-    // A region of `bytes`; *end identifies it for close().
-    uint8_t *open(uint64_t bytes, uint64_t *end) {
-        const uint64_t start = top;
-        uint8_t *p = alloc(bytes);
-        if (!p) return nullptr;
-        regions.push_back(Region{start, top, true});
-        *end = top;
-        return p;
-    }
-    void close(uint64_t end) {
-        for (auto it = regions.rbegin(); it != regions.rend(); ++it)
-            if (it->open && it->end == end) {
-                it->open = false;
+    void close(uint64_t id) {
+        for (size_t i = 0; i < regions.size(); i++)
+            if (regions[i].id == id) {
+                used -= regions[i].end - regions[i].start;
+                regions.erase(regions.begin() + (long)i);
                 break;
             }
-        while (!regions.empty() && !regions.back().open) regions.pop_back();
-        top = regions.empty() ? 0 : regions.back().end;
     }
     size_t live() const { return regions.size(); }
 };
@@ -717,8 +729,8 @@ void tbc_engine_deinit(tbc_engine *e) {
 
 tbc_status tbc_engine_arena_usage(const tbc_engine *e, uint64_t *dev_bytes, uint64_t *host_bytes, uint32_t *regions) {
     if (!e || !dev_bytes || !host_bytes || !regions) return TBC_ERR_INVALID_ARGUMENT;
-    *dev_bytes = e->dev.top;
-    *host_bytes = e->host.top;
+    *dev_bytes = e->dev.used;
+    *host_bytes = e->host.used;
     *regions = (uint32_t)(e->dev.live() + e->host.live());
     return TBC_OK;
 }
@@ -1182,12 +1194,11 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
         if (lengths[i] > 0xffffffffull || (lengths[i] && !messages[i])) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     if (!join_tails(e)) return TBC_ERR_DEVICE; // the messages may be blocks a batch tail still writes
-    const uint64_t dt = e->dev.top, ht = e->host.top;
-    uint8_t *d = e->dev.alloc(16ull * count + 16ull * count);
-    uint8_t *h = e->host.alloc(16ull * count + 16ull * count);
+    uint64_t rd = 0, rh = 0; // regions for this synchronous call, closed before it returns
+    uint8_t *d = e->dev.open(16ull * count + 16ull * count, &rd);
+    uint8_t *h = d ? e->host.open(16ull * count + 16ull * count, &rh) : nullptr;
     if (!d || !h) {
-        e->dev.top = dt;
-        e->host.top = ht;
+        if (d) e->dev.close(rd);
         return TBC_ERR_OUT_OF_MEMORY;
     }
     uint64_t *hp = (uint64_t *)h;
@@ -1205,8 +1216,8 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
         hipStreamSynchronize(e->stream) != hipSuccess)
         st = TBC_ERR_DEVICE;
     if (st == TBC_OK) memcpy(checksums_out, h + 16ull * count, 16ull * count);
-    e->dev.top = dt;
-    e->host.top = ht;
+    e->dev.close(rd);
+    e->host.close(rh);
     return st;
 }
 
@@ -1222,12 +1233,11 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
     hipSetDevice(e->device);
     if (!join_tails(e)) return TBC_ERR_DEVICE; // the messages may be blocks a batch tail still writes
     const uint64_t in_bytes = 32ull * count, out_off = align_up(in_bytes, 256);
-    const uint64_t dt = e->dev.top, ht = e->host.top;
-    uint8_t *d = e->dev.alloc(out_off + count);
-    uint8_t *h = e->host.alloc(out_off + count);
+    uint64_t rd = 0, rh = 0; // regions for this synchronous call, closed before it returns
+    uint8_t *d = e->dev.open(out_off + count, &rd);
+    uint8_t *h = d ? e->host.open(out_off + count, &rh) : nullptr;
     if (!d || !h) {
-        e->dev.top = dt;
-        e->host.top = ht;
+        if (d) e->dev.close(rd);
         return TBC_ERR_OUT_OF_MEMORY;
     }
     uint64_t *hp = (uint64_t *)h, *hx = hp + count;
@@ -1245,8 +1255,8 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
         hipStreamSynchronize(e->stream) != hipSuccess)
         st = TBC_ERR_DEVICE;
     if (st == TBC_OK) memcpy(results_out, h + out_off, count);
-    e->dev.top = dt;
-    e->host.top = ht;
+    e->dev.close(rd);
+    e->host.close(rh);
     return st;
 }
 
