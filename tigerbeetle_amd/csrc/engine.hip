@@ -434,6 +434,7 @@ struct tbc_batch {
     std::vector<uint32_t> status;    // host-side validation status per job
     hipEvent_t done = nullptr;
     hipEvent_t fork = nullptr;                          // end of the front (pipelined batches)
+    hipEvent_t prep = nullptr;                          // descriptors + partition done ahead on a tail
     hipStream_t mark_stream = nullptr;                  // where mark_cb records
     // A batch split into job groups (tbc_compaction_submit): the groups'
     // batches, and per job its group and index there.
@@ -2131,9 +2132,34 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                 for (const auto &g : seg_in[2 * (size_t)i + side])
                     if (g.first && !(ok = wait_sorts(e, g.first, g.first + (uint64_t)g.second * hj[i].value_size)))
                         break;
+    // A pipelined batch of speculated jobs whose inputs no batch in flight
+    // is writing and no sort is sorting: its descriptors go up and its
+    // partition runs on the tail its chains will take (idle by then: three
+    // batches back), so the engine stream goes from the previous batch's
+    // merge straight to this one's (config 2: ~60 us of upload, partition
+    // and launch gaps per step off the engine stream).
+    hipStream_t P = s;
+    if (spec_pipe && !grid_mode && !e->server && !(e->flags & TBC_CONFIG_LATENCY)) {
+        bool early = count > 0;
+        for (uint32_t k = 0; k < count && early; k++) early = sj[k].unique != 0;
+        for (uint32_t i = 0; i < count && early; i++)
+            for (int side = 0; side < 2 && early; side++)
+                for (const auto &g : seg_in[2 * (size_t)i + side]) {
+                    const uint64_t lo = g.first, hi = g.first + (uint64_t)g.second * hj[i].value_size;
+                    for (const auto &t : e->tail_out)
+                        for (const auto &r : t.ranges) early = early && !(lo < r.second && r.first < hi);
+                    for (const auto &ps : e->pending_sorts)
+                        for (const auto &r : ps.ranges) early = early && !(lo < r.second && r.first < hi);
+                    if (!early) break;
+                }
+        if (early) {
+            b->prep = take_event(e);
+            if (b->prep) P = e->tail[e->next_tail];
+        }
+    }
     // The descriptors up; tile status, block tiles and results zeroed
     // (contiguous) by the same launch.
-    ok = ok && launch_upload(d_in, h_in, sz_in, s, d_status, sz_tiles + sz_res) == 0;
+    ok = ok && launch_upload(d_in, h_in, sz_in, P, d_status, sz_tiles + sz_res) == 0;
     mark_cb(b, "start");
     if (grid_mode) {
         // Pipelined: the front (input data blocks found through their index
@@ -2255,7 +2281,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         const JobDesc *dj = (const JobDesc *)d_in;
         bool any_plain = false; // jobs not speculated: mask merge and assembly
         for (uint32_t k = 0; k < count; k++) any_plain |= !sj[k].unique;
-        ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s, mark_cb, b) == 0;
+        ok = ok && launch_merge_unique(dj, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s, mark_cb, b,
+                                       P != s ? (void *)P : nullptr, (void *)b->prep) == 0;
         ok = ok && launch_merge(dj, sj.data(), (int)count, d_splits, d_status, e->masks, d_block_tile, d_order,
                                 d_res, s, mark_cb, b, 0) == 0;
         if (any_plain) {
@@ -2760,6 +2787,7 @@ void tbc_batch_release(tbc_batch *b) {
         if (b->marks[m]) e->event_pool.push_back(b->marks[m]);
     if (b->done) e->event_pool.push_back(b->done);
     if (b->fork) e->event_pool.push_back(b->fork);
+    if (b->prep) e->event_pool.push_back(b->prep);
     if (b->h_results) {
         e->dev.close(b->dev_region);
         e->host.close(b->host_region);

@@ -487,13 +487,24 @@ __global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *
 
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
                         JobResultDev *d_results, uint32_t *d_ticket, void *stream, void (*mark)(void *, const char *),
-                        void *mark_ctx) {
-    hipStream_t s = (hipStream_t)stream;
-    if (!njobs) return 0;
-    const JobDesc &l = h_jobs[njobs - 1];
-    const uint32_t nsplits = l.usplit_base + (l.unique ? l.utile_count + 1 : 0);
-    const uint32_t ntiles = l.utile_base + l.utile_count;
-    if (!nsplits || !ntiles) return 0;
+                        void *mark_ctx, void *part_stream, void *part_done) {
+    hipStream_t s = (hipStream_t)part_stream ? (hipStream_t)part_stream : (hipStream_t)stream;
+    // The partition may run ahead on another stream (the batch's descriptors
+    // were uploaded there): the merge, and whatever follows on `stream`, wait.
+    auto join = [&]() {
+        if (s == (hipStream_t)stream) return true;
+        const bool ok = hipEventRecord((hipEvent_t)part_done, s) == hipSuccess &&
+                        hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)part_done, 0) == hipSuccess;
+        s = (hipStream_t)stream;
+        return ok;
+    };
+    uint32_t nsplits = 0, ntiles = 0;
+    if (njobs) {
+        const JobDesc &l = h_jobs[njobs - 1];
+        nsplits = l.usplit_base + (l.unique ? l.utile_count + 1 : 0);
+        ntiles = l.utile_base + l.utile_count;
+    }
+    if (!nsplits || !ntiles) return join() ? 0 : -1;
     if (nsplits <= kWaveSplitsMax)
         hipLaunchKernelGGL(k_partition_unique<true>, dim3((nsplits + 3) / 4), dim3(256), 0, s, d_jobs, njobs, nsplits,
                        (UniqueSplit *)d_usplits, d_results);
@@ -501,6 +512,7 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
         hipLaunchKernelGGL(k_partition_unique<false>, dim3((nsplits + 255) / 256), dim3(256), 0, s, d_jobs, njobs, nsplits,
                        (UniqueSplit *)d_usplits, d_results);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (!join()) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
     (void)d_ticket;
     const uint32_t pw = 1; // one tile per workgroup (2 and 4 measured slower)

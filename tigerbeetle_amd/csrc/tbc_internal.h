@@ -367,7 +367,7 @@ int launch_upload(void *dst, const void *host_src, uint64_t bytes, void *stream,
                   uint64_t zero_bytes = 0);
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
                         JobResultDev *d_results, uint32_t *d_ticket, void *stream, void (*mark)(void *, const char *),
-                        void *mark_ctx);
+                        void *mark_ctx, void *part_stream = nullptr, void *part_done = nullptr);
 int launch_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t total_dblocks, uint32_t total_tables,
                   uint32_t *d_ready,
                   JobResultDev *d_results, uint8_t *d_infos, const uint64_t *d_status, const uint64_t *d_masks,
