@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TBC_ABI_VERSION 6u
+#define TBC_ABI_VERSION 7u
 
 typedef enum tbc_status {
     TBC_OK = 0,
@@ -289,13 +289,18 @@ tbc_status tbc_grid_get_blocks(tbc_grid *grid, const uint64_t *addresses, void *
  * `previous_checksum` is NULL, the block at `previous_address` must be a
  * verified manifest block of this grid (closed by an earlier call); if it is
  * not, nothing is linked: the new blocks keep a zero header checksum (every
- * later read fails validation), are marked unverified, and the next
- * tbc_synchronize returns TBC_ERR_BLOCK_INVALID (the device found it after
- * this call returned).
+ * later read fails validation), are marked unverified, and the grid's next
+ * tbc_manifest_close_status returns TBC_ERR_BLOCK_INVALID (the device found
+ * it after this call returned).
  * TBC_ERR_INVALID_ARGUMENT if a packed header contradicts its address, the
  * chain or ManifestNode.metadata's asserts (schema.zig:534-554). */
 tbc_status tbc_manifest_close_blocks(tbc_grid *grid, const uint64_t *addresses, const void *const *host_images,
                                      uint32_t count, uint64_t previous_address, const uint64_t *previous_checksum);
+/* Outcome of the grid's manifest closes enqueued so far (the log's
+ * close_block callback, manifest_log.zig:903-952): waits for them, then
+ * TBC_ERR_BLOCK_INVALID once if any refused to link since the last call,
+ * TBC_OK otherwise. Only this call reports (and clears) a refusal. */
+tbc_status tbc_manifest_close_status(tbc_grid *grid);
 
 /* ---- TableMemory on the device (src/lsm/table_memory.zig:79-124) ------------
  * Groove.insert/update -> Tree.put (groove.zig:911-1006, tree.zig:268-270)
@@ -358,9 +363,9 @@ tbc_status tbc_memset_device(tbc_engine *engine, void *dst, int value, uint64_t 
  * (a collective over the split's exchange buffers, torch.cuda.ExternalStream)
  * goes on it. */
 tbc_status tbc_engine_stream(tbc_engine *engine, void **out_stream);
-/* Waits for every enqueued call; TBC_ERR_BLOCK_INVALID (once) if the device
- * found an error in a call that had already returned (a refused manifest
- * close). */
+/* Waits for every enqueued call. (A refused manifest close is reported by
+ * tbc_manifest_close_status, not here.) Any call that launches work returns
+ * TBC_ERR_DEVICE if a HIP error of an earlier call is still unreported. */
 tbc_status tbc_synchronize(tbc_engine *engine);
 
 /* ---- vsr.checksum (src/vsr/checksum.zig:50-59) ------------------------------ */

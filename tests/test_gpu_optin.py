@@ -1,29 +1,19 @@
-"""Every environment knob libtbc.so still reads leaves
-the output bytes oracle-exact. The library reads them once per process, so
-each setting runs, in a child process, GPU tests that exercise the paths it
-changes; each of those tests compares with the oracle.
+"""Every environment knob libtbc.so still reads (VERDICT r4 item 7, r5 item
+8) leaves the output bytes oracle-exact. The library reads them once per
+process, so each setting runs, in a child process, GPU tests that exercise
+the paths it changes; each of those tests compares with the oracle.
 
-  TBC_SORT_STREAM=1, TBC_TAIL_PRIORITY=1   bar-end sorts on their own stream
-                                           (pending-sort waits), tails at the
-                                           highest stream priority
-  TBC_GRID_SPECULATION=1                   grid batches merge UNIQUE_KEYS jobs
-                                           tile by tile, recompute in front
-  TBC_TAILS=2                              two tail streams
-  TBC_DEBUG_SYNC=1                         stage-by-stage waits (nothing pipelines)
-  TBC_PAIR_TAILS=0                         grid tails never paired (test_gpu_pairing.py)
-  TBC_CHAIN_SERVER=1                       the chain server (round 5, opt-in):
-                                           every batch's chains claimed by one
-                                           server on its own stream
-  TBC_CHAIN_SERVER=1, TBC_SERVER_WGS=64,   a small server whose idle waves
-  TBC_SERVER_WAVES=4,                      leave at once and poll slowly; two
-  TBC_CHAIN_LINGER_US=0,                   job groups in the throughput regime
-  TBC_CHAIN_BACKOFF=128, TBC_GROUPS=2
-  TBC_SORT_TICKETS=1, TBC_WAVE_SPLITS=4096,  sort passes take tiles by ticket,
-  TBC_DRAIN_COMPACT=1                      mask-merge partitions by thread above
-                                           4,096 splits, drained grid tails on
-                                           the compact tables (round 5 A/B)
+  TBC_SORT_TICKETS=1   sort passes always take tiles by ticket (the fallback
+                       if the one-tile-per-workgroup path's dispatch-order
+                       premise ever fails, sort.hip k_sort_pass)
+  TBC_DEBUG_SYNC=1     stage-by-stage waits (tools; nothing pipelines)
+  TBC_PAIR_TAILS=0     grid tails never paired (test_gpu_pairing.py)
 
-GPU_MAX_HW_QUEUES is HIP's own (the engine sizes its tails from it).
+GPU_MAX_HW_QUEUES is HIP's own (the engine sizes its tails from it). The
+round-3 to round-5 A/B knobs whose paths lost every measurement (the chain
+server, a sort stream of its own, tail priority, tail count, grid
+speculation, job-group count, partition split threshold, drained tails on
+compact tables) were removed with their paths in round 6.
 """
 import os
 import subprocess
@@ -60,24 +50,6 @@ def _child(env_extra: dict, files, select=None, timeout=240):
 
 
 @pytest.mark.gpu
-def test_sort_stream_and_tail_priority_bit_exact():
-    _child({"TBC_SORT_STREAM": "1", "TBC_TAIL_PRIORITY": "1"}, FILES, PIPELINED)
-
-
-@pytest.mark.gpu
-def test_grid_speculation_bit_exact():
-    """TBC_GRID_SPECULATION=1: grid batches merge their UNIQUE_KEYS jobs tile
-    by tile (k_merge_unique), broken speculations recomputed in the front —
-    the grid tests and the 11-bar config-1 lockstep against the oracle."""
-    _child({"TBC_GRID_SPECULATION": "1"}, ("test_gpu_grid.py", "test_gpu_config1.py"), timeout=300)
-
-
-@pytest.mark.gpu
-def test_two_tails_bit_exact():
-    _child({"TBC_TAILS": "2"}, FILES, PIPELINED)
-
-
-@pytest.mark.gpu
 def test_debug_sync_bit_exact():
     """TBC_DEBUG_SYNC=1 waits for every stage, so nothing pipelines: the
     parity tests that do not require it."""
@@ -87,25 +59,9 @@ def test_debug_sync_bit_exact():
 
 
 @pytest.mark.gpu
-def test_chain_server_bit_exact():
-    """The chain server with its default geometry: the pipelined, grid and
-    throughput-regime tests, and the 11-bar config-1 lockstep with a
-    checkpoint and restart."""
-    _child({"TBC_CHAIN_SERVER": "1"}, FILES, PIPELINED)
-    _child({"TBC_CHAIN_SERVER": "1"}, ("test_gpu_config1.py",), "checkpoint", timeout=300)
-
-
-@pytest.mark.gpu
-def test_small_chain_server_bit_exact():
-    _child({"TBC_CHAIN_SERVER": "1", "TBC_SERVER_WGS": "64", "TBC_SERVER_WAVES": "4", "TBC_CHAIN_LINGER_US": "0",
-            "TBC_CHAIN_BACKOFF": "128", "TBC_GROUPS": "2"}, FILES, PIPELINED)
-
-
-@pytest.mark.gpu
-def test_round5_ab_knobs_bit_exact():
-    """The round-5 A/B knobs restore the earlier paths: the sort and grid
-    tests (tickets in every pass, thread partitions, compact drained tails)
-    and the 11-bar config-1 lockstep."""
-    env = {"TBC_SORT_TICKETS": "1", "TBC_WAVE_SPLITS": "4096", "TBC_DRAIN_COMPACT": "1"}
+def test_sort_tickets_bit_exact():
+    """TBC_SORT_TICKETS=1: every sort pass takes its tiles by ticket — the
+    sort tests, the pipelined tests and the 11-bar config-1 lockstep."""
+    env = {"TBC_SORT_TICKETS": "1"}
     _child(env, FILES, PIPELINED + " or test_sort_values")
     _child(env, ("test_gpu_config1.py",), "checkpoint", timeout=300)

@@ -166,3 +166,91 @@ def test_speculated_batches_pipelined_three_in_flight(engine, oracle_lib):
                     assert np.array_equal(disk_image(g), disk_image(w)), (s, ji.tree.name, k)
     for b in batches:
         b.release()
+
+
+@pytest.mark.gpu
+def test_early_prep_waits_for_engine_stream_writes(engine_pipe, oracle_lib):
+    """a pipelined speculated batch uploads its descriptors
+    and runs its merge-path partition ahead on a tail stream, off the engine
+    stream. Its inputs here are all still being written on the engine stream
+    when it is submitted — A put into a device memtable in random order and
+    sorted out of place (tbc_memtable_put, tbc_sort_values_batch), B landed
+    by a device copy (tbc_copy_device_batch) — with no host wait in between;
+    the partition must see the final bytes: blocks and TableInfos equal the
+    oracle's, twice (the second batch also overlaps the first one's tail)."""
+    from tigerbeetle_amd import Memtable, abi
+    from tigerbeetle_amd.engine import Job
+    bs = 1 << 20
+    eng = engine_pipe
+    spec = trees.BY_NAME["transfers.id"]
+    vcm = eng.layout(spec).block_value_count_max
+    rng = np.random.default_rng(521)
+    batches, keep = [], []
+    for step in range(2):
+        ji = workloads.make_job_inputs(spec, rng, n_a=spec.value_count_max, b_table_sizes=[8 * vcm, 8 * vcm],
+                                       a_immutable=True, overlap=0.0)
+        addrs = np.arange(1, workloads.worst_case_blocks(spec, 3 * spec.value_count_max, bs) + 3, dtype=np.uint64)
+        out = eng.alloc(len(addrs) * bs)
+        mem = Memtable(eng, spec)
+        a_sorted = eng.alloc(ji.a_values.nbytes)
+        b_host = np.concatenate(ji.b_tables)
+        b_src = eng.upload(b_host)  # synchronous: before any of the writes below
+        b_dst = eng.alloc(b_host.nbytes)
+        keep += [out, mem, a_sorted, b_src, b_dst]
+        eng.synchronize()
+        # Enqueued on the engine stream, no host wait from here to the submit.
+        mem.put(ji.a_values[rng.permutation(len(ji.a_values))])
+        ptr, n = mem.values()
+        eng.sort_values_batch([(spec, ptr, n, a_sorted.ptr)])
+        eng.copy_device_batch([(b_dst.ptr, b_src.ptr, b_host.nbytes)])
+        segs_b = [(b_dst.ptr + o * spec.value_size, len(t)) for o, t in
+                  zip(np.cumsum([0] + [len(t) for t in ji.b_tables[:-1]]), ji.b_tables)]
+        job = Job(spec, [(a_sorted.ptr, n)], segs_b, True, False, 1, 0x1234, 48, addrs, out,
+                  flags=abi.COMPACTION_UNIQUE_KEYS)
+        batches.append((eng.submit([job]), ji, addrs, out, job))
+    for b, ji, addrs, out, _ in batches:
+        b.wait()
+        assert "merge_unique" in b.kernel_times()  # the pipelined pass (TBC_CONFIG_PIPELINE)
+        r, infos = b.result(0)
+        o = run_oracle(oracle_lib, ji, bs, addrs)
+        assert r.status == 0 and o.status == 0 and r.block_count == len(o.blocks)
+        got = out.download(r.block_count * bs).reshape(-1, bs)
+        for k, (g, w) in enumerate(zip(got, o.blocks)):
+            assert np.array_equal(disk_image(g), disk_image(w)), k
+        assert np.array_equal(infos, o.table_infos)
+        b.release()
+    for m in keep:
+        if hasattr(m, "close"):
+            m.close()
+
+
+@pytest.mark.gpu
+def test_engine_closed_with_live_batches_then_a_new_engine(oracle_lib):
+    """an engine closed while batches are still in flight
+    (never waited for, never released) leaves no HIP error behind: a second
+    engine's compaction afterwards is bit-exact, and its calls report no
+    stale error (tbc returns TBC_ERR_DEVICE for an unreported one)."""
+    from helpers import gpu_run
+    from tigerbeetle_amd import Engine, abi
+    bs = 1 << 20
+    spec = trees.BY_NAME["transfers.id"]
+    rng = np.random.default_rng(77)
+    ji = workloads.make_job_inputs(spec, rng, n_a=200_000, b_table_sizes=[150_000, 100_000], a_immutable=True,
+                                   overlap=0.0)
+    addrs = np.arange(1, workloads.worst_case_blocks(spec, 450_000, bs) + 3, dtype=np.uint64)
+    e1 = Engine(device=0, block_size=bs)
+    keep = []
+    live = []
+    for _ in range(3):
+        live.append(e1.submit(_jobs(e1, [ji], [addrs], [e1.alloc(len(addrs) * bs)], keep, bs,
+                                    abi.COMPACTION_UNIQUE_KEYS)))
+    e1.close()  # batches still in flight: their handles die with the engine
+    with Engine(device=0, block_size=bs) as e2:
+        (r, infos, blocks), = gpu_run(e2, [ji], bs, [addrs], flags=abi.COMPACTION_UNIQUE_KEYS)[0]
+        o = run_oracle(oracle_lib, ji, bs, addrs)
+        assert r.status == 0 and r.block_count == len(o.blocks)
+        for g, w in zip(blocks, o.blocks):
+            assert np.array_equal(disk_image(g), disk_image(w))
+        assert np.array_equal(infos, o.table_infos)
+        e2.synchronize()
+    del live

@@ -59,8 +59,10 @@ def _inputs(name):
     return spec, bs, ji, addrs
 
 
-def _run_rank(name, rank, world, exchange):
-    """compact_split on this rank; returns (ok, message)."""
+def _run_rank(name, rank, world, exchange, max_engine_waits=None):
+    """compact_split on this rank; returns (ok, message). With
+    max_engine_waits, the engine-level host waits (Batch.wait, synchronize,
+    downloads) made while compact_split enqueues the step must not exceed it."""
     from helpers import disk_image, run_oracle
     from oracle import oracle
     from tigerbeetle_amd import Engine, split, workloads
@@ -87,7 +89,14 @@ def _run_rank(name, rank, world, exchange):
         assert split.staged_bytes(cuts, rank, spec.value_size) == a_mine.nbytes + b_mine.nbytes
         job = Job(spec, segs_a, segs_b, ji.a_immutable, ji.drop_tombstones, 1, 0x1234, 48,
                   np.asarray(addrs, dtype=np.uint64), None)
-        res = split.compact_split(eng, job, cuts, exchange, rank, staged=True).finish()
+        waits = _count_engine_waits() if max_engine_waits is not None else None
+        try:
+            res = split.compact_split(eng, job, cuts, exchange, rank, staged=True)
+        finally:
+            n_waits = waits() if waits else 0
+        if max_engine_waits is not None and n_waits > max_engine_waits:
+            return False, f"rank {rank}: {n_waits} engine waits while enqueuing the step"
+        res = res.finish()
         whole = run_oracle(oracle, ji, bs, addrs)
         assert whole.status == 0
         plan = res.plan
@@ -106,6 +115,26 @@ def _run_rank(name, rank, world, exchange):
         if not np.array_equal(res.table_infos, whole.table_infos[t0:t1]):
             return False, f"rank {rank}: TableInfo differs"
         return True, f"rank {rank}: blocks {res.blocks} tables {res.tables} OK ({len(slots)} slots)"
+
+
+def _count_engine_waits():
+    """Count the engine's host waits from now on; returns a function that
+    stops counting and gives the count."""
+    from tigerbeetle_amd import engine as E
+    n = [0]
+    saved = {(cls, m): getattr(cls, m) for cls, m in ((E.Batch, "wait"), (E.Engine, "synchronize"),
+                                                       (E.DeviceBuffer, "download"))}
+    for (cls, m), f in saved.items():
+        def counted(*a, _f=f, **k):
+            n[0] += 1
+            return _f(*a, **k)
+        setattr(cls, m, counted)
+
+    def stop():
+        for (cls, m), f in saved.items():
+            setattr(cls, m, f)
+        return n[0]
+    return stop
 
 
 def test_split_single_rank_bit_exact():
@@ -247,3 +276,127 @@ def test_count_only_and_values_at_offset(bs, name):
         want = np.concatenate([blocks[split.data_block_slot(k, dbcm), 256:256 + min(vcm, full.value_count - k * vcm)
                                       * vs].reshape(-1, vs) for k in range(full.data_block_count)])
         assert np.array_equal(np.concatenate(placed), want)
+
+
+# ---------------------------------------------------------------------------
+# The device exchange (TorchExchange on a cuda device: the count word, the
+# all-gathers on the engine stream through torch.cuda.ExternalStream), which
+# bench.py takes at N > 1 with the nccl backend.
+
+def _nccl_worker(names, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("nccl", rank=0, world_size=1)  # RCCL, before any other GPU work
+    from tigerbeetle_amd import split
+    try:
+        out = []
+        for name in names:
+            ex = split.TorchExchange(dist, "cuda:0")
+            assert ex.on_device
+            # The step's one host wait is reading the gathered counts (a
+            # torch copy); the engine itself is not waited for.
+            out.append(_run_rank(name, 0, 1, ex, max_engine_waits=0))
+        q.put((all(ok for ok, _ in out), [m for _, m in out]))
+    except Exception as e:
+        q.put((False, f"{type(e).__name__}: {e}"))
+    dist.destroy_process_group()
+
+
+def test_split_over_rccl_world_one_bit_exact():
+    """The nccl (RCCL) branch of the split exchange executed: a world of one
+    (RCCL refuses two ranks on one device, and the pool's boxes have one
+    GPU), so only the counts all-gather runs — on the engine stream, over
+    the device count word — for config 4's split job and a 4 KiB case; the
+    blocks and TableInfos equal the oracle's unsplit job."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(["c4_split", "debit_4k"], _free_port(), q))
+    p.start()
+    ok, msg = q.get(timeout=300)
+    p.join(timeout=60)
+    if p.is_alive():
+        p.kill()
+    assert ok, msg
+    assert p.exitcode == 0
+
+
+class _StreamDist:
+    """A torch.distributed stand-in for ranks that are threads of one
+    process on one GPU, for TorchExchange's device branch. Like RCCL's
+    collective, all_gather_into_tensor is ordered on each rank's CURRENT
+    stream (the engine stream the exchange put in front): each rank records
+    an event where its input is ready, and after a thread barrier every rank
+    waits (on its stream) for every rank's event and copies every rank's
+    input into its output on that stream; a second round keeps any rank from
+    reusing its input before all ranks have copied it."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.local = threading.local()
+        self.inputs = [None] * world
+        self.copied = [None] * world
+        self.calls = 0
+
+    def get_rank(self):
+        return self.local.rank
+
+    def get_world_size(self):
+        return self.world
+
+    def all_gather_into_tensor(self, out, inp):
+        import torch
+        r, s = self.local.rank, torch.cuda.current_stream()
+        ready = torch.cuda.Event()
+        ready.record(s)
+        self.inputs[r] = (inp, ready)
+        self.barrier.wait()
+        n = inp.numel()
+        for q, (t, ev) in enumerate(self.inputs):
+            s.wait_event(ev)
+            out[q * n:(q + 1) * n].copy_(t)
+        done = torch.cuda.Event()
+        done.record(s)
+        self.copied[r] = done
+        self.barrier.wait()
+        for ev in self.copied:
+            s.wait_event(ev)
+        if r == 0:
+            self.calls += 1
+        self.barrier.wait()
+
+
+@pytest.mark.parametrize("name,world", [("debit_4k", 2), ("id_1mib", 2), ("c4_split", 2)])
+def test_split_device_exchange_stream_order(name, world):
+    """TorchExchange's device branch end to end on the real engine: `world`
+    ranks as threads of this process, one Engine each on cuda:0, exchanging
+    through _StreamDist on their engine streams — the count word, the heads'
+    and the index entries' all-gathers and the copies into place, all in
+    engine-stream order with no engine wait while the step is enqueued. Every
+    rank's blocks and TableInfos equal the oracle's unsplit job."""
+    import threading
+    from tigerbeetle_amd import split
+    d = _StreamDist(world)
+    results = [None] * world
+
+    def run(r):
+        d.local.rank = r
+        try:
+            results[r] = _run_rank(name, r, world, split.TorchExchange(d, "cuda:0"), max_engine_waits=0)
+        except Exception as e:  # noqa: BLE001 - reported below
+            results[r] = (False, f"rank {r}: {type(e).__name__}: {e}")
+            d.barrier.abort()
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert all(res is not None and res[0] for res in results), results
+    # the counts, and (a straddling block: its heads) at 1 MiB blocks
+    assert d.calls >= (2 if name == "id_1mib" else 1), d.calls

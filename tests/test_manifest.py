@@ -109,10 +109,11 @@ def test_gpu_manifest_refuses_to_link_an_untrusted_block():
             for prev in (3, 7):  # 3: staged from storage (unverified); 7: never written (not a manifest block)
                 images = manifest.pack_blocks(_infos(31, 2), [9, 10], CLUSTER, bs, previous_address=prev)
                 manifest.close_on_grid(grid, images, [9, 10], previous_address=prev, previous_checksum=None)
+                eng.synchronize()  # an unrelated wait does not take the refusal
                 with pytest.raises(abi.TbcError) as err:  # the refusal is reported
-                    eng.synchronize()
+                    grid.manifest_close_status()
                 assert err.value.status == abi.TBC_ERR_BLOCK_INVALID
-                eng.synchronize()  # reported once
+                grid.manifest_close_status()  # reported once
                 got = grid.get_blocks([9, 10])
                 assert not got[:, :16].any(), prev  # header checksums left zero
                 res = eng.validate_blocks([grid.pointer(9), grid.pointer(10)], [0, 0], [9, 10])
@@ -123,11 +124,11 @@ def test_gpu_manifest_refuses_to_link_an_untrusted_block():
             images = manifest.pack_blocks(_infos(20, 3), [6], CLUSTER, bs, previous_address=7)
             manifest.close_on_grid(grid, images, [6], previous_address=7, previous_checksum=None)
             with pytest.raises(abi.TbcError):
-                eng.synchronize()
+                grid.manifest_close_status()
             images = manifest.pack_blocks(_infos(20, 4), [11], CLUSTER, bs, previous_address=6)
             manifest.close_on_grid(grid, images, [11], previous_address=6, previous_checksum=None)
             with pytest.raises(abi.TbcError):  # 6 is no longer trusted: refused
-                eng.synchronize()
+                grid.manifest_close_status()
             assert not grid.get_blocks([6, 11])[:, :16].any()
         finally:
             grid.close()

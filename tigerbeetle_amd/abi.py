@@ -37,7 +37,7 @@ COMPACTION_GRID = 2
 COMPACTION_UNIQUE_KEYS = 4  # speculated merge (tbc.h): no repeated key in A u B, no tombstone dropped
 COMPACTION_COUNT_ONLY = 8  # the merge alone: survivor counts (phase A of a split job)
 SPECULATION_NONE, SPECULATION_HELD, SPECULATION_BROKEN = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class TbcError(RuntimeError):
@@ -206,6 +206,7 @@ _SIGNATURES = {
     "tbc_grid_get_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P), ctypes.c_uint32]),
     "tbc_manifest_close_blocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_P),
                                                  ctypes.c_uint32, ctypes.c_uint64, _P]),
+    "tbc_manifest_close_status": (ctypes.c_int, [_P]),
     "tbc_memtable_init": (ctypes.c_int, [_P, ctypes.POINTER(Tree), ctypes.c_uint32, ctypes.POINTER(_P)]),
     "tbc_memtable_deinit": (None, [_P]),
     "tbc_memtable_put": (ctypes.c_int, [_P, _P, ctypes.c_uint32]),

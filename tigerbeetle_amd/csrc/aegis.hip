@@ -1966,351 +1966,6 @@ __global__ __launch_bounds__(256) void k_index_layout(const JobDesc *jobs, int n
     gst<uint64_t>(idx + j.idx_addresses_off + 8 * (k - t * j.dbcm), gld<uint64_t>(j.addresses + data_block_slot(k, j.dbcm)));
 }
 
-// --------------------------------------------------------------------------
-// Chain server (round 5).
-//
-// A batch's AEGIS chains used to be one kernel launch on one of three tail
-// streams: at most three batches' chains ran at once (one per hardware queue
-// beside the engine stream), and a small batch held a few dozen CUs for a
-// whole chain time (~2 ms per 1 MiB block) while the rest of the chip idled
-// (config 1: 58 such launches per step). Here every batch's data blocks are
-// tasks in ONE device ring (tbc_internal.h ChainRing): the batch's front
-// publishes them (k_chain_publish, engine stream, after its bodies are in
-// place) and the server's chain waves take them two at a time (one per
-// 32-lane group) whatever batch they belong to, so the number of chains in
-// flight is set by the server's workgroups, not by the hardware queues.
-//
-// A server instance is an ordinary launch on the chain stream: its waves
-// take tasks while there are any and leave after the ring has stayed empty
-// for `linger`; the front of every batch also queues an instance behind it
-// (stream order after the publish), so a task published after the last
-// wave of a running instance has left is always taken by a later one. The
-// instance never waits on anything but the ring, so it always ends.
-//
-// Per task (data block k of job j): the body's AEGIS-128L chain and the
-// header (data_block_finish, table.zig:306-384), then the block's index
-// entry — header checksum, key_min, key_max, address (TableIndex,
-// schema.zig:80-260) — straight into its table's index block image; the
-// table's counter counts the block, and the wave that counts its table's
-// last block seals the index block (index_block_finish, table.zig:403-457:
-// unused entries zeroed, body and header checksums, header) and writes the
-// TableInfo (schema.zig:489-509). No T-table workgroup of its own waits for
-// a free CU (k_index_blocks held 148 KiB of LDS for ~2 MB of work per
-// batch). Every output is stored write-through (sc1), and a task counts in
-// its batch's `done` only after its stores have completed (s_waitcnt), so a
-// kernel that runs after k_chain_wait sees them, as does the sealer after an
-// agent-scope acquire (MI355X_MICROARCH.md: sc1 payload -> vmcnt(0) ->
-// agent atomic; consumer acquire -> plain loads).
-// --------------------------------------------------------------------------
-constexpr uint32_t kServerWavesMax = 16;
-// The server's message prefetch: 4 windows (32 updates, ~2-3 us at two or
-// more chain waves per SIMD) ahead; its loads are direct (no indirection).
-#ifndef TBC_SERVER_GROUP
-#define TBC_SERVER_GROUP 4
-#endif
-constexpr uint32_t kServerGroup = TBC_SERVER_GROUP;
-
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Claim word fields (tbc_internal.h ChainRing.claim).
-__device__ __forceinline__ uint32_t claim_seq(unsigned long long w) { return (uint32_t)(w >> 40); }
-__device__ __forceinline__ uint32_t claim_tasks(unsigned long long w) { return (uint32_t)(w >> 20) & 0xFFFFFu; }
-__device__ __forceinline__ uint32_t claim_taken(unsigned long long w) { return (uint32_t)w & 0xFFFFFu; }
-
-// Batch `seq`: its descriptor, then (released) its claim word, then the
-// count of published batches.
-__global__ __launch_bounds__(64) void k_chain_publish(ChainRing r, ChainBatch cb, unsigned long long seq) {
-    if (threadIdx.x != 0) return;
-    const uint32_t slot = (uint32_t)(seq % kChainSlots);
-    r.batches[slot] = cb;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(r.claim + slot, (seq & 0xFFFFFFull) << 40 | (unsigned long long)cb.ntasks << 20,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(r.pub, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// A chain task (batch slot, block m of the batch) resolved to its job.
-struct ChainTask {
-    const ChainBatch *cb;
-    const JobDesc *j;
-    uint32_t m; // block of the batch (dblock_base numbering)
-    uint32_t k; // the job's data block
-    __device__ __forceinline__ void resolve(const ChainRing &r, uint32_t slot, uint32_t m_) {
-        cb = r.batches + slot;
-        m = m_;
-        const JobDesc *jobs = cb->jobs;
-        const int ji = find_job(jobs, cb->njobs, m, [](const JobDesc &d) { return d.dblock_base; });
-        j = jobs + ji;
-        k = m - j->dblock_base + j->block_lo;
-    }
-};
-
-// Seal table t of job j (its blocks' entries are in the image): zero the
-// unused entries, checksum the index body and the header, store the header,
-// the sector tail and the TableInfo. Both 32-lane groups run it (a group
-// with nothing to seal mirrors its partner's table with writer = false).
-template <class Step>
-__device__ __forceinline__ void seal_table(const uint32_t *sT, uint32_t *hdr, const JobDesc &j, const JobResultDev &res,
-                                           uint8_t *infos, uint32_t t, bool writer) {
-    const uint32_t g = threadIdx.x & 31;
-    const uint32_t db = res.data_block_count, dbcm = j.dbcm, ks = j.key_size;
-    const uint32_t k0 = t * dbcm, nblk = (db - k0) < dbcm ? (db - k0) : dbcm, k_last = k0 + nblk - 1;
-    const uint32_t index_slot = index_block_slot(t, k_last);
-    uint8_t *idx = block_ptr(j, index_slot);
-    if (writer && nblk < dbcm) { // the last table of the job: unused entries are zero
-        const uint32_t spans[4][2] = {{j.idx_checksums_off, 32}, {j.idx_keys_min_off, ks}, {j.idx_keys_max_off, ks},
-                                      {j.idx_addresses_off, 8}};
-#pragma unroll
-        for (int a = 0; a < 4; a++)
-            for (uint32_t o = spans[a][0] + nblk * spans[a][1] + 4 * g; o < spans[a][0] + dbcm * spans[a][1]; o += 128)
-                st32<true>(idx + o, 0u);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // our own write-through zeros, read back below
-    GlobalMsg body(idx + kHeaderSize, j.index_size - kHeaderSize);
-    const uint32_t body_tag = aegis_mac32<GlobalMsg, Step, kServerGroup>(sT, body);
-    HeaderFields h;
-    h.cluster_lo = j.cluster_lo;
-    h.cluster_hi = j.cluster_hi;
-    h.address = gld<uint64_t>(j.addresses + index_slot);
-    h.snapshot = j.snapshot_min;
-    h.size = j.index_size;
-    h.meta0 = nblk;      // TableIndex.Metadata.data_block_count
-    h.meta1 = dbcm;      // .data_block_count_max
-    h.meta2 = ks;        // .key_size
-    h.meta3 = j.tree_id; // .tree_id
-    h.block_type = 4;    // BlockType.index (schema.zig:64)
-    const uint32_t hdr_tag = finish_header<Step>(sT, hdr, h, body_tag);
-    if (g < 4) hdr[g] = hdr_tag;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (!writer) return;
-    st32<true>(idx + 4 * g, hdr[g]);
-    st32<true>(idx + 4 * (g + 32), hdr[g + 32]);
-    const uint32_t end = (uint32_t)sector_ceil(j.index_size);
-    for (uint32_t o = j.index_size + 4 * g; o < end; o += 128) st32<true>(idx + o, 0u);
-    // ManifestNode.TableInfo (schema.zig:489-509): key_min of the first entry,
-    // key_max of the last, the index block's checksum and address.
-    const uint64_t n_out = res.value_count;
-    const uint64_t vcount = (n_out - (uint64_t)k0 * j.vcm) < (uint64_t)nblk * j.vcm ? (n_out - (uint64_t)k0 * j.vcm)
-                                                                                   : (uint64_t)nblk * j.vcm;
-    uint32_t v = 0;
-    if (g < 8) v = 4 * g < ks ? gld<uint32_t>(idx + j.idx_keys_min_off + 4 * g) : 0u;
-    else if (g < 16) v = 4 * (g - 8) < ks ? gld<uint32_t>(idx + j.idx_keys_max_off + ks * (nblk - 1) + 4 * (g - 8)) : 0u;
-    else if (g < 20) v = hdr[g - 16];
-    else if (g == 24) v = (uint32_t)h.address;
-    else if (g == 25) v = (uint32_t)(h.address >> 32);
-    else if (g == 26) v = (uint32_t)j.snapshot_min;
-    else if (g == 27) v = (uint32_t)(j.snapshot_min >> 32);
-    else if (g == 28 || g == 29) v = 0xffffffffu; // snapshot_max = maxInt(u64)
-    else if (g == 30) v = (uint32_t)vcount;
-    else if (g == 31) v = (uint32_t)j.tree_id | ((uint32_t)((j.level_b & 0x3f) | (1u << 6)) << 16);
-    st32<true>(infos + (size_t)(j.info_base + t - j.table_lo) * kTableInfoSize + 4 * g, v);
-}
-
-// Whether batch q (< pub) still has unclaimed tasks; *stale: its slot has
-// been reused (q is long claimed).
-__device__ __forceinline__ bool claimable(const ChainRing &r, unsigned long long q, bool *stale) {
-    const unsigned long long w = ld_sc1(r.claim + q % kChainSlots);
-    *stale = claim_seq(w) != (uint32_t)(q & 0xFFFFFFu);
-    return !*stale && claim_taken(w) < claim_tasks(w);
-}
-
-template <class Step>
-__global__ __launch_bounds__(64 * kServerWavesMax) void k_chain_server(ChainRing r, unsigned long long first_seq) {
-    __shared__ uint32_t sT[kCompactTableDwords];
-    __shared__ uint32_t sHdr[kServerWavesMax][2][64];
-    __shared__ uint32_t s_go;
-    const uint32_t lane = threadIdx.x & 63, g = lane & 31;
-    const bool upper = lane >= 32;
-    // Every batch before first_seq was claimed before this instance started
-    // (the instance before it left only when nothing was claimable): one
-    // queued behind an instance that took everything leaves at once.
-    if (threadIdx.x == 0) {
-        bool any = false, stale;
-        const unsigned long long p = ld_sc1(r.pub);
-        for (unsigned long long q = first_seq; q < p && !any; q++) any = claimable(r, q, &stale);
-        s_go = any ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_go) return;
-    load_tables_compact(sT);
-    __syncthreads(); // the last workgroup barrier: from here on every wave runs on its own
-    uint32_t *hdr = sHdr[threadIdx.x >> 6][upper ? 1 : 0];
-    unsigned long long cur = first_seq; // (lane 0) every batch before it is claimed
-    for (;;) {
-        // Claim up to two tasks (lane 0): one fetch_add of 2 on the claim
-        // word of the oldest batch with unclaimed tasks; leave once nothing
-        // has been claimable for the linger time (idle polls back off to
-        // backoff_max pauses: every poll is a few cross-XCD loads of the
-        // same lines).
-        uint32_t slot = 0, t0 = 0, got = 0;
-        if (lane == 0) {
-            const uint64_t since = wall_clock64();
-            uint32_t backoff = 1;
-            for (;;) {
-                // The instance leaves as a whole: once one wave has decided to,
-                // no wave claims again (what is published from then on is the
-                // next instance's, with every wave).
-                if (ld_sc1(r.closing) == first_seq + 1) break;
-                const unsigned long long p = ld_sc1(r.pub);
-                for (unsigned long long q = cur; q < p && !got; q++) {
-                    bool stale;
-                    if (!claimable(r, q, &stale)) {
-                        if (q == cur) cur++;
-                        continue;
-                    }
-                    const unsigned long long w = __hip_atomic_fetch_add(r.claim + q % kChainSlots, 2ull,
-                                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // (If the slot has just been reused, these are the new batch's tasks.)
-                    const uint32_t n = claim_tasks(w), c = claim_taken(w);
-                    if (c < n) {
-                        slot = (uint32_t)(q % kChainSlots);
-                        t0 = c;
-                        got = n - c < 2 ? n - c : 2;
-                    }
-                }
-                if (got) {
-                    __hip_atomic_fetch_add(r.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                // An idle wave stays while any wave of the instance holds a
-                // task, and the instance leaves as a whole once none has
-                // held one for the linger time: a task published meanwhile
-                // finds every wave of this instance, or of the next one (a
-                // later instance waits behind this one on the chain stream).
-                if (wall_clock64() - since > r.linger &&
-                    __hip_atomic_load(r.active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                    __hip_atomic_store(r.closing, first_seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                for (uint32_t i = 0; i < backoff; i++) __builtin_amdgcn_s_sleep(63);
-                backoff = 2 * backoff < r.backoff_max ? 2 * backoff : r.backoff_max;
-            }
-        }
-        got = __builtin_amdgcn_readfirstlane(got);
-        if (!got) return;
-        slot = __builtin_amdgcn_readfirstlane(slot);
-        t0 = __builtin_amdgcn_readfirstlane(t0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // the batch's descriptor, results, bodies
-        // This group's task (a group beyond `got` shares task 0 and owns nothing).
-        const bool own = !upper || got == 2;
-        const uint32_t my_slot = slot, my_m = t0 + (upper && got == 2 ? 1u : 0u);
-        // The other group's task.
-        const uint32_t slot_p = slot, m_p = t0 + (!upper && got == 2 ? 1u : 0u);
-        ChainTask task;
-        task.resolve(r, my_slot, my_m);
-        unsigned long long *own_done = task.cb->done;
-        const bool live = own && task.k < task.cb->res[task.j->job_index].data_block_count;
-        const bool live_lo = __builtin_amdgcn_readlane((int)live, 0) != 0;
-        const bool live_hi = __builtin_amdgcn_readlane((int)live, 32) != 0;
-        if (live_lo || live_hi) {
-            // A group with no live block mirrors its partner's, writing nothing.
-            if (!live) task.resolve(r, slot_p, m_p);
-            const bool writer = live;
-            const JobDesc &j = *task.j;
-            JobResultDev &res = task.cb->res[j.job_index];
-            const uint32_t k = task.k;
-            const uint64_t n_out = res.value_count, first = (uint64_t)k * j.vcm;
-            const uint32_t cnt = (uint32_t)((n_out - first) < j.vcm ? (n_out - first) : j.vcm);
-            uint8_t *blk = block_ptr(j, data_block_slot(k, j.dbcm));
-            const uint32_t *ready = task.cb->ready;
-            const bool produced = (j.unique && res.spec != kSpecBroken) || j.seal || !ready;
-            if (writer && g == 0 && !produced &&
-                __hip_atomic_load(ready + task.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != cnt)
-                st32<true>(&res.invariant, 0xdeafu);
-            GlobalMsg body(blk + kHeaderSize, cnt * j.value_size);
-            const uint32_t body_tag = aegis_mac32<GlobalMsg, Step, kServerGroup>(sT, body);
-            finish_data_block<true, Step>(sT, hdr, j, k, cnt, body_tag, writer);
-            // Its index entry, into the table's index block image.
-            const uint32_t db = res.data_block_count, tb = k / j.dbcm, s = k - tb * j.dbcm;
-            const uint32_t k_last = ((tb + 1) * j.dbcm < db ? (tb + 1) * j.dbcm : db) - 1;
-            const uint32_t ks = j.key_size;
-            if (writer) {
-                uint8_t *image = block_ptr(j, index_block_slot(tb, k_last));
-                uint64_t kmin[4], kmax[4];
-                value_key(j, blk + kHeaderSize, kmin);
-                value_key(j, blk + kHeaderSize + (size_t)(cnt - 1) * j.value_size, kmax);
-                if (g < 8) st32<true>(image + j.idx_checksums_off + 32 * s + 4 * g, g < 4 ? hdr[g] : 0u);
-                if (4 * g < ks) {
-                    st32<true>(image + j.idx_keys_min_off + ks * s + 4 * g, (uint32_t)(kmin[g >> 1] >> (32 * (g & 1))));
-                    st32<true>(image + j.idx_keys_max_off + ks * s + 4 * g, (uint32_t)(kmax[g >> 1] >> (32 * (g & 1))));
-                }
-                if (g < 2) {
-                    const uint64_t a = gld<uint64_t>(j.addresses + data_block_slot(k, j.dbcm));
-                    st32<true>(image + j.idx_addresses_off + 8 * s + 4 * g, (uint32_t)(a >> (32 * g)));
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // Count the block in its table; the group that counts the last one seals it.
-            uint32_t seal = 0;
-            if (writer && g == 0) {
-                const uint32_t nblk = k_last - tb * j.dbcm + 1;
-                const uint32_t old = __hip_atomic_fetch_add(task.cb->table_cnt + j.table_base + tb - j.table_lo, 1u,
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                seal = old + 1 == nblk ? 1u : 0u;
-            }
-            const bool seal_lo = __builtin_amdgcn_readlane((int)seal, 0) != 0;
-            const bool seal_hi = __builtin_amdgcn_readlane((int)seal, 32) != 0;
-            if (seal_lo || seal_hi) {
-                // A sealing group's task is its own; the other group mirrors it.
-                const bool mine = upper ? seal_hi : seal_lo;
-                ChainTask st;
-                if (mine) st.resolve(r, my_slot, my_m);
-                else st.resolve(r, slot_p, m_p);
-                const JobDesc &sj = *st.j;
-                seal_table<Step>(sT, hdr, sj, st.cb->res[sj.job_index], st.cb->infos, st.k / sj.dbcm, mine);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (own && g == 0)
-            __hip_atomic_fetch_add(own_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) __hip_atomic_fetch_add(r.active, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// A batch's tail waits here (one lane) until every task of the batch has
-// counted; bounded (~15 s): then every job of the batch carries an
-// invariant error instead of the tail hanging.
-__global__ __launch_bounds__(64) void k_chain_wait(const unsigned long long *done, uint32_t target,
-                                                   JobResultDev *res, uint32_t njobs) {
-    if (threadIdx.x != 0) return;
-    for (uint32_t spins = 0;; spins++) {
-        if (ld_sc1(done) >= target) return;
-        if (spins > (1u << 22)) break;
-        __builtin_amdgcn_s_sleep(127);
-    }
-    for (uint32_t i = 0; i < njobs; i++) st32<true>(&res[i].invariant, 0x7a17u);
-}
-
-int launch_chain_publish(const ChainRing &r, const ChainBatch &cb, unsigned long long seq, void *stream) {
-    hipLaunchKernelGGL(k_chain_publish, dim3(1), dim3(64), 0, (hipStream_t)stream, r, cb, seq);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// Chain waves per workgroup: one workgroup per CU (the tables take 128 KiB
-// of LDS); two or more chain waves per SIMD take the round key by
-// ds_bpermute, one alone by VALU lane moves.
-int launch_chain_server(const ChainRing &r, unsigned long long first_seq, uint32_t wgs, uint32_t waves,
-                        void *stream) {
-    waves = waves < 1 ? 1 : (waves > kServerWavesMax ? kServerWavesMax : waves);
-    hipLaunchKernelGGL(k_chain_server<StepCompact>, dim3(wgs), dim3(64 * waves), 0, (hipStream_t)stream, r,
-                       first_seq);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_chain_wait(const unsigned long long *done, uint32_t target, JobResultDev *d_results, uint32_t njobs,
-                      void *stream) {
-    if (!target) return 0;
-    hipLaunchKernelGGL(k_chain_wait, dim3(1), dim3(64), 0, (hipStream_t)stream, done, target, d_results, njobs);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 // One workgroup per CU (the tables take 128 KiB of LDS): spread the waves
 // over all 256 CUs, at most 16 waves per workgroup.
 static uint32_t waves_per_block(uint32_t waves) {

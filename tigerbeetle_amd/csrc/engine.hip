@@ -174,37 +174,23 @@ struct tbc_engine {
     };
     std::vector<TailOutputs> tail_out;
     int next_tail = 0;
-    // Deferred device-side errors of calls that return before the device
-    // ran them (a manifest close that refused to link): one word, read and
-    // cleared by tbc_synchronize.
-    uint32_t *d_error = nullptr;
-    // Chain server (aegis.hip k_chain_server, round 5): pipelined and grid
-    // batches publish their data blocks (ChainRing: a descriptor and a claim
-    // word per batch) and a server instance on the chain stream (a hardware
-    // queue of its own) takes them, whatever batch they belong to; a batch's
-    // tail waits for its count. Opt-in (TBC_CHAIN_SERVER=1): it measured
-    // slower than one chain kernel per batch tail on every config (DESIGN
-    // 4.8). Host side: the batches published so far and the descriptor
-    // slots of those in flight (oldest first).
+    // Engine-stream writes to memory a caller may hand a later batch as
+    // input (memtable puts, bar-end sorts, device copies, the outputs of
+    // batches not listed in tail_out): a batch whose descriptors and
+    // partition go ahead on a tail stream (submit_impl's early prep) reads
+    // its inputs there, off the engine stream, so that tail waits for the
+    // last such write. `ext_dirty`: a write was enqueued since ext_ev was
+    // last recorded; `ext_live`: ext_ev may not have passed yet.
+    hipEvent_t ext_ev = nullptr;
+    bool ext_dirty = false, ext_live = false;
     // Tail pairing: a grid batch whose tail waits for the next grid batch,
     // so that both batches' chains run as one launch on one tail stream
     // (grid_tail_pair); launched alone by any other call (flush_tail).
+    // (Round 5's chain server — persistent chain waves taking any batch's
+    // blocks from a device ring — measured slower on every config and was
+    // removed in round 6: DESIGN 4.8.)
     tbc_batch *deferred = nullptr;
     bool pair_tails = true;
-    bool server = false;
-    hipStream_t chain_stream = nullptr;
-    ChainRing ring{};
-    uint8_t *ring_mem = nullptr;
-    unsigned long long published = 0; // batches published (the next batch's sequence number)
-    hipEvent_t slot_ev[kChainSlots] = {};
-    std::vector<uint32_t> slot_fifo; // descriptor slots of batches in flight, oldest first
-    // Server geometry per batch: a batch whose front fits beside a chain
-    // workgroup on every CU (k_merge_unique: 16.4 KiB of LDS; the
-    // timestamp-key mask merge: 18.9 KiB) gets one workgroup of 8 chain
-    // waves per CU; others (grid batches, composite-key mask merges, the
-    // bar-end sorts: 35-52 KiB of LDS) leave half the CUs whole: 128
-    // workgroups of 16. TBC_SERVER_WGS / TBC_SERVER_WAVES (A/B) set both.
-    uint32_t wide_wgs = 256, wide_waves = 8, narrow_wgs = 128, narrow_waves = 16;
     Arena dev, host;
     Staging staging;
     // Host ranges the caller registered (tbc_host_register: hipHostRegister):
@@ -237,19 +223,9 @@ struct tbc_engine {
     uint64_t copy_desc_size = 0;
     uint8_t *kway_scratch = nullptr;
     uint64_t kway_scratch_size = 0;
-    // Memtable sorts run on their own stream, after everything enqueued on
-    // the engine stream before them; later engine-stream work waits for a
-    // sort only if it touches that sort's tables (wait_sorts) — so a bar-end
-    // sort overlaps the next half-bar's level compactions, which do not read
-    // memtables — and conservatively where it cannot tell (join_sorts).
-    hipStream_t sort_stream = nullptr;
-    hipEvent_t sort_last = nullptr; // recorded after every sort batch
-    bool sort_recorded = false;
-    struct PendingSort {
-        std::vector<std::pair<uint64_t, uint64_t>> ranges; // [lo, hi) of the sorted tables
-        hipEvent_t done;
-    };
-    std::vector<PendingSort> pending_sorts;
+    // (Bar-end sorts run on the engine stream. Round 3's sort stream of its
+    // own measured slower — a fifth stream shares a hardware queue with a
+    // tail and inherits its order — and was removed in round 6: DESIGN 3.)
 };
 
 struct tbc_grid {
@@ -257,6 +233,10 @@ struct tbc_grid {
     uint8_t *base = nullptr;
     uint64_t block_count = 0;
     uint8_t *verified = nullptr; // device, per slot: written by the engine or validated (trusted like a cache hit)
+    // Manifest closes the device refused (ManifestLog.close_block onto an
+    // untrusted previous block): a device word set by the close's chain,
+    // read and cleared by tbc_manifest_close_status.
+    uint32_t *d_error = nullptr;
 };
 
 struct tbc_memtable {
@@ -278,6 +258,28 @@ static hipError_t stream_query(hipStream_t s) {
     const hipError_t q = hipStreamQuery(s);
     if (q == hipErrorNotReady) (void)hipGetLastError();
     return q;
+}
+
+// A failing call reports its HIP error through its status: consume it from
+// the runtime's last-error slot so that the next call does not report it too.
+static tbc_status failed(tbc_status st) {
+    (void)hipGetLastError();
+    return st;
+}
+
+// A HIP error no call has reported (a call whose result the engine ignores:
+// an event recorded for a profile mark, a synchronize at release): the next
+// call that launches work returns TBC_ERR_DEVICE for it rather than drop it
+// (the reference panics on a failure rather than continuing,
+// compaction.zig:307-318). The engine's own queries consume their "not
+// ready" (event_query, stream_query), and failing calls consume what they
+// report (failed()).
+static bool no_stale_error() {
+    const hipError_t err = hipGetLastError();
+    if (err == hipSuccess) return true;
+    fprintf(stderr, "tbc: an unreported HIP error of an earlier call is pending: %s (%d)\n", hipGetErrorString(err),
+            (int)err);
+    return false;
 }
 
 static hipEvent_t take_event(tbc_engine *e) {
@@ -450,8 +452,6 @@ struct tbc_batch {
     bool seal = false;
     tbc_compaction_result seal_result{};
     bool count_only = false; // TBC_COMPACTION_COUNT_ONLY: value_count only
-    uint32_t chain_slot = 0;       // chain server: the batch's descriptor slot
-    unsigned long long chain_seq = 0; // and sequence number
     // A grid batch's tail (chains, index blocks, input checks, results), as
     // enqueued when the batch is submitted or, deferred for pairing, later.
     struct GridTail {
@@ -459,8 +459,6 @@ struct tbc_batch {
         const uint64_t *status = nullptr;
         const uint32_t *block_tile = nullptr;
         const SplitDesc *splits = nullptr;
-        unsigned long long *done_ctr = nullptr;
-        bool wide = false;
         const ResolveItem *resolve = nullptr;
         uint32_t n_resolve = 0, n_checks = 0;
         InputCheck *checks = nullptr;
@@ -510,38 +508,6 @@ static void mark_cb(void *ctx, const char *name) {
     b->mark_names[b->nmarks++] = name;
 }
 
-// Engine-stream work after a sort waits for it when it touches its tables.
-static void retire_sorts(tbc_engine *e) {
-    auto &ps = e->pending_sorts;
-    for (size_t i = 0; i < ps.size();) {
-        if (event_query(ps[i].done) == hipSuccess) {
-            e->event_pool.push_back(ps[i].done);
-            ps.erase(ps.begin() + (long)i);
-        } else {
-            i++;
-        }
-    }
-}
-
-static bool wait_sorts(tbc_engine *e, uint64_t lo, uint64_t hi) {
-    for (const auto &p : e->pending_sorts)
-        for (const auto &r : p.ranges)
-            if (lo < r.second && r.first < hi) {
-                if (hipStreamWaitEvent(e->stream, p.done, 0) != hipSuccess) return false;
-                break;
-            }
-    return true;
-}
-
-static bool wait_sorts_ptr(tbc_engine *e, const void *p, uint64_t bytes) {
-    return e->pending_sorts.empty() || wait_sorts(e, (uint64_t)(uintptr_t)p, (uint64_t)(uintptr_t)p + bytes);
-}
-
-// Work that may read any device memory waits for every sort enqueued so far.
-static bool join_sorts(tbc_engine *e) {
-    return !e->sort_recorded || hipStreamWaitEvent(e->stream, e->sort_last, 0) == hipSuccess;
-}
-
 // Every stream of the engine drained (internal: no deferred-error report).
 static bool sync_streams(tbc_engine *e);
 static void flush_tail(tbc_engine *e, bool drain = false);
@@ -553,7 +519,7 @@ static bool join_tails(tbc_engine *e) {
     flush_tail(e);
     for (int t = 0; t < e->ntails; t++)
         if (hipStreamWaitEvent(e->stream, e->tail_ev[t], 0) != hipSuccess) return false;
-    return join_sorts(e);
+    return true;
 }
 
 // Engine-stream copies may read what the last seal (on a tail) wrote.
@@ -561,6 +527,21 @@ static bool wait_seal(tbc_engine *e) {
     if (!e->seal_pending) return true;
     e->seal_pending = false; // the engine stream is ordered after it from here on
     return hipStreamWaitEvent(e->stream, e->seal_ev, 0) == hipSuccess;
+}
+
+// An engine-stream write a later batch may take as input (tbc_engine::ext_ev).
+static void note_write(tbc_engine *e) { e->ext_dirty = true; }
+
+// Stream P (a batch's early prep on a tail) ordered after every such write
+// enqueued so far; no wait once the last one has passed.
+static bool order_after_writes(tbc_engine *e, hipStream_t P) {
+    if (e->ext_dirty) {
+        if (hipEventRecord(e->ext_ev, e->stream) != hipSuccess) return false;
+        e->ext_dirty = false;
+        e->ext_live = true;
+    }
+    if (e->ext_live && event_query(e->ext_ev) == hipSuccess) e->ext_live = false;
+    return !e->ext_live || hipStreamWaitEvent(P, e->ext_ev, 0) == hipSuccess;
 }
 
 extern "C" {
@@ -580,10 +561,10 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     if (bs < kSectorSize || (bs & (bs - 1)) || bs % kSectorSize) return TBC_ERR_INVALID_ARGUMENT;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= config->device || config->device < 0)
-        return TBC_ERR_DEVICE;
-    if (hipSetDevice(config->device) != hipSuccess) return TBC_ERR_DEVICE;
+        return failed(TBC_ERR_DEVICE);
+    if (hipSetDevice(config->device) != hipSuccess) return failed(TBC_ERR_DEVICE);
     tbc_engine *e = new (std::nothrow) tbc_engine();
-    if (!e) return TBC_ERR_OUT_OF_MEMORY;
+    if (!e) return failed(TBC_ERR_OUT_OF_MEMORY);
     e->device = config->device;
     e->block_size = bs;
     e->flags = config->flags;
@@ -593,53 +574,41 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     // config 1, 52.3 vs 52.0 ms: DESIGN 4.3.)
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
-        return TBC_ERR_DEVICE;
+        return failed(TBC_ERR_DEVICE);
     }
     if (hipMalloc((void **)&e->dev.base, e->dev.size) != hipSuccess) {
         hipStreamDestroy(e->stream);
         delete e;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     if (hipHostMalloc((void **)&e->host.base, e->host.size, hipHostMallocDefault) != hipSuccess) {
         hipFree(e->dev.base);
         hipStreamDestroy(e->stream);
         delete e;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     bool ok = true;
-    // Tails (chains, index blocks, input checks, results) at the engine
-    // stream's priority. Round 3 measured the highest tail priority (its
-    // workgroups dispatched ahead of the next front) on one box: config 1
-    // 130 -> 108 ms and config 5 15.0 -> 14.4 ms with equal priorities (the
-    // fronts are the critical path); TBC_TAIL_PRIORITY=1 (A/B only) restores it.
-    int prio_least = 0, prio_greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-    static const bool high = getenv("TBC_TAIL_PRIORITY") != nullptr; // A/B measurement only
+    // Streams, one per hardware queue of the process (GPU_MAX_HW_QUEUES,
+    // HIP's default 4): the engine stream and the tails. Tails (chains,
+    // index blocks, input checks, results) run at the engine stream's
+    // priority: round 3 measured the highest tail priority (its workgroups
+    // dispatched ahead of the next front) slower on one box, config 1 130 vs
+    // 108 ms and config 5 15.0 vs 14.4 ms (the fronts are the critical path).
     {
-        const char *q = getenv("GPU_MAX_HW_QUEUES"), *t = getenv("TBC_TAILS"), *cs = getenv("TBC_CHAIN_SERVER");
+        const char *q = getenv("GPU_MAX_HW_QUEUES");
         const int queues = q && atoi(q) > 0 ? atoi(q) : 4;
-        e->server = cs && cs[0] == '1';
-        const char *pt = getenv("TBC_PAIR_TAILS"); // A/B: 0 = every grid tail alone
+        const char *pt = getenv("TBC_PAIR_TAILS"); // 0 = every grid tail alone (test_gpu_pairing.py compares)
         e->pair_tails = !(pt && pt[0] == '0');
-        // Streams, one per hardware queue: the engine stream, the chain
-        // stream (server) and the tails.
-        const int want = t && atoi(t) > 0 ? atoi(t) : queues - (e->server ? 2 : 1);
+        const int want = queues - 1;
         e->ntails = want < 1 ? 1 : (want > tbc_engine::kMaxTails ? tbc_engine::kMaxTails : want);
-        const char *w = getenv("TBC_SERVER_WGS"), *v = getenv("TBC_SERVER_WAVES"); // A/B measurement
-        if (w && atoi(w) > 0) e->wide_wgs = e->narrow_wgs = (uint32_t)atoi(w);
-        if (v && atoi(v) > 0) e->wide_waves = e->narrow_waves = (uint32_t)atoi(v);
     }
     for (int t = 0; ok && t < e->ntails; t++)
-        ok = hipStreamCreateWithPriority(&e->tail[t], hipStreamNonBlocking, high ? prio_greatest : 0) == hipSuccess &&
+        ok = hipStreamCreateWithFlags(&e->tail[t], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&e->tail_ev[t], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&e->seal_ev, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&e->ext_ev, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->staging.base, Staging::kSlots * Staging::kSlotBytes, hipHostMallocDefault) ==
                   hipSuccess;
-    // The sort stream exists only when asked for (TBC_SORT_STREAM=1): a
-    // stream beyond the hardware queues shares one with another stream.
-    if (getenv("TBC_SORT_STREAM"))
-        ok = ok && hipStreamCreateWithFlags(&e->sort_stream, hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&e->sort_last, hipEventDisableTiming) == hipSuccess;
     for (int s = 0; ok && s < Staging::kSlots; s++)
         ok = hipEventCreateWithFlags(&e->staging.ev[s], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&e->desc.base, DescRing::kSlots * DescRing::kSlotBytes, hipHostMallocDefault) ==
@@ -650,36 +619,9 @@ tbc_status tbc_engine_init(const tbc_config *config, tbc_engine **out_engine) {
     // values (64 MiB of HBM), so submitting never waits on the device to grow
     // it; a larger batch still grows it (after a stream synchronize).
     ok = ok && ensure_masks(e, kInitialMaskWords);
-    ok = ok && hipMalloc((void **)&e->d_error, 256) == hipSuccess &&
-         hipMemsetAsync(e->d_error, 0, 256, e->stream) == hipSuccess;
-    if (ok && e->server) {
-        // kChainSlots claim words, the published count on a line of its own,
-        // kChainSlots batch descriptors; all zero.
-        const uint64_t ring_bytes = 8ull * kChainSlots + 256 + sizeof(ChainBatch) * kChainSlots;
-        ok = hipStreamCreateWithFlags(&e->chain_stream, hipStreamNonBlocking) == hipSuccess &&
-             hipMalloc((void **)&e->ring_mem, ring_bytes) == hipSuccess &&
-             hipMemsetAsync(e->ring_mem, 0, ring_bytes, e->stream) == hipSuccess;
-        for (uint32_t i = 0; ok && i < kChainSlots; i++)
-            ok = hipEventCreateWithFlags(&e->slot_ev[i], hipEventDisableTiming) == hipSuccess;
-        if (ok) {
-            ChainRing &r = e->ring;
-            r.claim = (unsigned long long *)e->ring_mem;
-            r.pub = (unsigned long long *)(e->ring_mem + 8ull * kChainSlots);
-            r.batches = (ChainBatch *)(e->ring_mem + 8ull * kChainSlots + 256);
-            r.active = (uint32_t *)(e->ring_mem + 8ull * kChainSlots + 128);
-            r.closing = (unsigned long long *)(e->ring_mem + 8ull * kChainSlots + 192);
-            // An idle server wave polls 200 us (100 MHz clock) before leaving,
-            // so a running instance takes a batch published meanwhile at once
-            // (a later instance is queued behind it on the chain stream).
-            const char *l = getenv("TBC_CHAIN_LINGER_US");
-            r.linger = 100u * (uint32_t)(l && atoi(l) >= 0 ? atoi(l) : 200);
-            const char *bo = getenv("TBC_CHAIN_BACKOFF"); // A/B measurement
-            r.backoff_max = bo && atoi(bo) > 0 ? (uint32_t)atoi(bo) : 16u;
-        }
-    }
     if (!ok) {
         tbc_engine_deinit(e);
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     *out_engine = e;
     return TBC_OK;
@@ -692,19 +634,9 @@ void tbc_engine_deinit(tbc_engine *e) {
     hipStreamSynchronize(e->stream);
     for (int t = 0; t < e->ntails; t++)
         if (e->tail[t]) hipStreamSynchronize(e->tail[t]);
-    // The last server instance leaves once the ring has stayed empty.
-    if (e->chain_stream) hipStreamSynchronize(e->chain_stream);
-    for (uint32_t i = 0; i < kChainSlots; i++)
-        if (e->slot_ev[i]) hipEventDestroy(e->slot_ev[i]);
-    if (e->chain_stream) hipStreamDestroy(e->chain_stream);
-    if (e->ring_mem) hipFree(e->ring_mem);
-    if (e->sort_stream) hipStreamSynchronize(e->sort_stream);
-    for (auto &p : e->pending_sorts) e->event_pool.push_back(p.done);
     for (auto &t : e->tail_out) e->event_pool.push_back(t.done);
     for (hipEvent_t ev : e->event_pool) hipEventDestroy(ev);
     for (const auto &r : e->registered) hipHostUnregister((void *)(uintptr_t)r.first);
-    if (e->sort_last) hipEventDestroy(e->sort_last);
-    if (e->sort_stream) hipStreamDestroy(e->sort_stream);
     for (int s = 0; s < Staging::kSlots; s++)
         if (e->staging.ev[s]) hipEventDestroy(e->staging.ev[s]);
     if (e->staging.base) hipHostFree(e->staging.base);
@@ -718,13 +650,16 @@ void tbc_engine_deinit(tbc_engine *e) {
     if (e->sort_status) hipFree(e->sort_status);
     if (e->kway_scratch) hipFree(e->kway_scratch);
     if (e->copy_desc) hipFree(e->copy_desc);
-    if (e->d_error) hipFree(e->d_error);
     for (int t = 0; t < e->ntails; t++) {
         if (e->tail_ev[t]) hipEventDestroy(e->tail_ev[t]);
         if (e->tail[t]) hipStreamDestroy(e->tail[t]);
     }
     if (e->seal_ev) hipEventDestroy(e->seal_ev);
+    if (e->ext_ev) hipEventDestroy(e->ext_ev);
     hipStreamDestroy(e->stream);
+    // Errors of the drained work were the batches' to report: none is left
+    // pending for the next engine's first call.
+    (void)hipGetLastError();
     delete e;
 }
 
@@ -741,19 +676,21 @@ tbc_status tbc_grid_init(tbc_engine *e, uint64_t block_count, tbc_grid **out) {
     *out = nullptr;
     hipSetDevice(e->device);
     tbc_grid *g = new (std::nothrow) tbc_grid();
-    if (!g) return TBC_ERR_OUT_OF_MEMORY;
+    if (!g) return failed(TBC_ERR_OUT_OF_MEMORY);
     g->engine = e;
     g->block_count = block_count;
     if (hipMalloc((void **)&g->base, block_count * e->block_size) != hipSuccess) {
         delete g;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     if (hipMalloc((void **)&g->verified, block_count) != hipSuccess ||
-        hipMemsetAsync(g->verified, 0, block_count, e->stream) != hipSuccess) {
+        hipMemsetAsync(g->verified, 0, block_count, e->stream) != hipSuccess ||
+        hipMalloc((void **)&g->d_error, 256) != hipSuccess || hipMemsetAsync(g->d_error, 0, 256, e->stream) != hipSuccess) {
+        if (g->d_error) hipFree(g->d_error);
         if (g->verified) hipFree(g->verified);
         hipFree(g->base);
         delete g;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     *out = g;
     return TBC_OK;
@@ -763,6 +700,7 @@ void tbc_grid_deinit(tbc_grid *g) {
     if (!g) return;
     hipSetDevice(g->engine->device);
     sync_streams(g->engine);
+    hipFree(g->d_error);
     hipFree(g->verified);
     hipFree(g->base);
     delete g;
@@ -773,8 +711,8 @@ tbc_status tbc_grid_invalidate(tbc_grid *g) {
     if (!g) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
-    if (!join_tails(e)) return TBC_ERR_DEVICE; // no running batch marks a block after this
-    return hipMemsetAsync(g->verified, 0, g->block_count, e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    if (!join_tails(e)) return failed(TBC_ERR_DEVICE); // no running batch marks a block after this
+    return hipMemsetAsync(g->verified, 0, g->block_count, e->stream) == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_grid_block_pointer(const tbc_grid *g, uint64_t address, void **out) {
@@ -784,14 +722,14 @@ tbc_status tbc_grid_block_pointer(const tbc_grid *g, uint64_t address, void **ou
 }
 
 tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *blocks, uint32_t count) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
         if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
-    if (!join_tails(e)) return TBC_ERR_DEVICE; // no running batch reads a block being replaced
+    if (!join_tails(e)) return failed(TBC_ERR_DEVICE); // no running batch reads a block being replaced
     if (!count) return TBC_OK;
     // Validate before trusting: every staged block's verified byte is cleared
     // BEFORE any image lands (stream order), so a call that fails halfway
@@ -802,15 +740,16 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
         const uint32_t n = count - c0 < kChunk ? count - c0 : kChunk;
         uint64_t region = 0;
         const uint64_t *d_addr = stage_u64s(e, addresses + c0, n, &region);
-        if (!d_addr) return TBC_ERR_DEVICE;
+        if (!d_addr) return failed(TBC_ERR_DEVICE);
         const bool ok = launch_grid_set_verified(d_addr, n, g->verified, 0, e->stream) == 0;
         e->dev.close(region);
-        if (!ok) return TBC_ERR_DEVICE;
+        if (!ok) return failed(TBC_ERR_DEVICE);
     }
     bool direct = false;
+    note_write(e);
     for (uint32_t i = 0; i < count; i++)
         if (!stage_h2d(e, g->base + (addresses[i] - 1) * e->block_size, blocks[i], e->block_size, &direct))
-            return TBC_ERR_DEVICE;
+            return failed(TBC_ERR_DEVICE);
     // A registered source is read by DMA after the enqueue: the caller may
     // reuse its buffer once this returns, so wait for those copies (pageable
     // sources were already copied into the pinned ring).
@@ -818,29 +757,29 @@ tbc_status tbc_grid_put_blocks(tbc_grid *g, const uint64_t *addresses, const voi
         hipEvent_t ev = take_event(e);
         const bool ok = ev && hipEventRecord(ev, e->stream) == hipSuccess && hipEventSynchronize(ev) == hipSuccess;
         if (ev) e->event_pool.push_back(ev);
-        if (!ok) return TBC_ERR_DEVICE;
+        if (!ok) return failed(TBC_ERR_DEVICE);
     }
     return TBC_OK;
 }
 
 tbc_status tbc_grid_get_blocks(tbc_grid *g, const uint64_t *addresses, void *const *blocks, uint32_t count) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !blocks))) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
         if (addresses[i] == 0 || addresses[i] > g->block_count || !blocks[i]) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
     hipSetDevice(e->device);
-    if (!join_tails(e)) return TBC_ERR_DEVICE; // blocks still being sealed by a batch tail
+    if (!join_tails(e)) return failed(TBC_ERR_DEVICE); // blocks still being sealed by a batch tail
     std::vector<D2H> items(count);
     for (uint32_t i = 0; i < count; i++)
         items[i] = D2H{blocks[i], g->base + (addresses[i] - 1) * e->block_size, e->block_size};
-    return stage_d2h_many(e, items.data(), count) ? TBC_OK : TBC_ERR_DEVICE;
+    return stage_d2h_many(e, items.data(), count) ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, const void *const *host_images,
                                      uint32_t count, uint64_t previous_address, const uint64_t *previous_checksum) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(g ? g->engine : nullptr);
     if (!g || (count && (!addresses || !host_images))) return TBC_ERR_INVALID_ARGUMENT;
     tbc_engine *e = g->engine;
@@ -881,21 +820,22 @@ tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, con
     const uint64_t meta = 8ull * count + 16;
     if (meta > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
     bool direct = false;
+    note_write(e);
     for (uint32_t i = 0; i < count; i++) {
         uint32_t size;
         memcpy(&size, (const uint8_t *)host_images[i] + 96, 4);
         if (!stage_h2d(e, g->base + (addresses[i] - 1) * bs, host_images[i], sector_ceil(size), &direct))
-            return TBC_ERR_DEVICE;
+            return failed(TBC_ERR_DEVICE);
     }
     if (direct) { // registered images are read by DMA after the enqueue: done before returning
         hipEvent_t ev = take_event(e);
         const bool ok = ev && hipEventRecord(ev, e->stream) == hipSuccess && hipEventSynchronize(ev) == hipSuccess;
         if (ev) e->event_pool.push_back(ev);
-        if (!ok) return TBC_ERR_DEVICE;
+        if (!ok) return failed(TBC_ERR_DEVICE);
     }
     const int slot = st.next;
     st.next = (st.next + 1) % Staging::kSlots;
-    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return TBC_ERR_DEVICE;
+    if (st.used[slot] && hipEventSynchronize(st.ev[slot]) != hipSuccess) return failed(TBC_ERR_DEVICE);
     uint8_t *host = st.base + (uint64_t)slot * Staging::kSlotBytes;
     memcpy(host, addresses, 8ull * count);
     if (previous_checksum) memcpy(host + 8ull * count, previous_checksum, 16);
@@ -905,17 +845,17 @@ tbc_status tbc_manifest_close_blocks(tbc_grid *g, const uint64_t *addresses, con
     // the next user of the arena is later on the same stream).
     uint64_t region = 0;
     uint8_t *d = e->dev.open(meta, &region);
-    if (!d) return TBC_ERR_OUT_OF_MEMORY;
+    if (!d) return failed(TBC_ERR_OUT_OF_MEMORY);
     // The chain kernel marks the closed blocks verified (trusted like
     // compaction outputs), or refuses to link an untrusted previous block.
     bool ok = hipMemcpyAsync(d, host, meta, hipMemcpyHostToDevice, e->stream) == hipSuccess &&
               launch_manifest_close((const uint64_t *)d, count, g->base, bs, previous_address,
                                     previous_checksum ? (const uint64_t *)(d + 8ull * count) : nullptr, g->verified,
-                                    e->d_error, e->stream) == 0 &&
+                                    g->d_error, e->stream) == 0 &&
               hipEventRecord(st.ev[slot], e->stream) == hipSuccess;
     st.used[slot] = true;
     e->dev.close(region);
-    return ok ? TBC_OK : TBC_ERR_DEVICE;
+    return ok ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_memtable_init(tbc_engine *e, const tbc_tree *tree, uint32_t capacity, tbc_memtable **out) {
@@ -926,14 +866,14 @@ tbc_status tbc_memtable_init(tbc_engine *e, const tbc_tree *tree, uint32_t capac
         return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     tbc_memtable *m = new (std::nothrow) tbc_memtable();
-    if (!m) return TBC_ERR_OUT_OF_MEMORY;
+    if (!m) return failed(TBC_ERR_OUT_OF_MEMORY);
     m->engine = e;
     m->tree = *tree;
     m->capacity = capacity;
     // +16: buffers are readable past the last value (sort/merge key loads of a 16-byte value).
     if (hipMalloc((void **)&m->values, (uint64_t)capacity * tree->value_size + 16) != hipSuccess) {
         delete m;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     *out = m;
     return TBC_OK;
@@ -943,21 +883,20 @@ void tbc_memtable_deinit(tbc_memtable *m) {
     if (!m) return;
     hipSetDevice(m->engine->device);
     hipStreamSynchronize(m->engine->stream);
-    if (m->engine->sort_stream) hipStreamSynchronize(m->engine->sort_stream);
     hipFree(m->values);
     delete m;
 }
 
 tbc_status tbc_memtable_put(tbc_memtable *m, const void *values, uint32_t count) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     if (!m || (count && !values)) return TBC_ERR_INVALID_ARGUMENT;
     if ((uint64_t)m->count + count > m->capacity) return TBC_ERR_CAPACITY; // table_memory.zig:80
     if (!count) return TBC_OK;
     hipSetDevice(m->engine->device);
     const uint64_t vs = m->tree.value_size;
-    if (!wait_sorts_ptr(m->engine, m->values + m->count * vs, count * vs) ||
-        !stage_h2d(m->engine, m->values + m->count * vs, values, count * vs))
-        return TBC_ERR_DEVICE;
+    if (!stage_h2d(m->engine, m->values + m->count * vs, values, count * vs))
+        return failed(TBC_ERR_DEVICE);
+    note_write(m->engine);
     m->count += count;
     return TBC_OK;
 }
@@ -1030,7 +969,7 @@ tbc_status tbc_host_register(tbc_engine *e, void *ptr, uint64_t bytes) {
     const uint64_t lo = (uint64_t)(uintptr_t)ptr;
     for (const auto &r : e->registered)
         if (lo < r.second && r.first < lo + bytes) return TBC_ERR_INVALID_ARGUMENT; // overlaps a registered range
-    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) return TBC_ERR_DEVICE;
+    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) return failed(TBC_ERR_DEVICE);
     e->registered.push_back({lo, lo + bytes});
     return TBC_OK;
 }
@@ -1043,9 +982,9 @@ tbc_status tbc_host_unregister(tbc_engine *e, void *ptr) {
     for (size_t i = 0; i < e->registered.size(); i++)
         if (e->registered[i].first == lo) {
             // Copies from or into it may still be enqueued.
-            if (!sync_streams(e)) return TBC_ERR_DEVICE;
+            if (!sync_streams(e)) return failed(TBC_ERR_DEVICE);
             e->registered.erase(e->registered.begin() + (long)i);
-            return hipHostUnregister(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+            return hipHostUnregister(ptr) == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
         }
     return TBC_ERR_INVALID_ARGUMENT;
 }
@@ -1053,13 +992,13 @@ tbc_status tbc_host_unregister(tbc_engine *e, void *ptr) {
 tbc_status tbc_device_alloc(tbc_engine *e, uint64_t bytes, void **out_ptr) {
     if (!e || !out_ptr) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    return hipMalloc(out_ptr, bytes ? bytes : 1) == hipSuccess ? TBC_OK : TBC_ERR_OUT_OF_MEMORY;
+    return hipMalloc(out_ptr, bytes ? bytes : 1) == hipSuccess ? TBC_OK : failed(TBC_ERR_OUT_OF_MEMORY);
 }
 
 tbc_status tbc_device_free(tbc_engine *e, void *ptr) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    return hipFree(ptr) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    return hipFree(ptr) == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
@@ -1067,10 +1006,9 @@ tbc_status tbc_copy_to_device(tbc_engine *e, void *dst, const void *src, uint64_
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (!wait_seal(e) || !wait_sorts_ptr(e, dst, bytes) ||
-        hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
-        return TBC_ERR_DEVICE;
-    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    if (!wait_seal(e) || hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+        return failed(TBC_ERR_DEVICE);
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
@@ -1078,52 +1016,53 @@ tbc_status tbc_copy_to_host(tbc_engine *e, void *dst, const void *src, uint64_t 
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (!wait_seal(e) || !wait_sorts_ptr(e, src, bytes) || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
-        return TBC_ERR_DEVICE;
-    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    if (!wait_seal(e) || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        return failed(TBC_ERR_DEVICE);
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_copy_device_async(tbc_engine *e, void *dst, const void *src, uint64_t bytes) {
     if (!e || (bytes && (!dst || !src))) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    if (!wait_seal(e) || !wait_sorts_ptr(e, dst, bytes) || !wait_sorts_ptr(e, src, bytes)) return TBC_ERR_DEVICE;
+    if (!wait_seal(e)) return failed(TBC_ERR_DEVICE);
+    note_write(e);
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, e->stream) == hipSuccess ? TBC_OK
-                                                                                          : TBC_ERR_DEVICE;
+                                                                                          : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t count) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     if (!e || (count && !copies)) return TBC_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < count; i++)
         if (copies[i].bytes && (!copies[i].dst || !copies[i].src)) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    if (!wait_seal(e)) return TBC_ERR_DEVICE;
+    if (!wait_seal(e)) return failed(TBC_ERR_DEVICE);
     std::vector<CopyItem> items;
     uint64_t chunks = 0;
     const uint64_t cb = copy_chunk_bytes();
     for (uint32_t i = 0; i < count; i++) {
         const tbc_copy &c = copies[i];
         if (!c.bytes) continue;
-        if (!wait_sorts_ptr(e, c.dst, c.bytes) || !wait_sorts_ptr(e, c.src, c.bytes)) return TBC_ERR_DEVICE;
         if (((uintptr_t)c.dst | (uintptr_t)c.src | c.bytes) & 15) { // unaligned: a copy of its own, in order
             if (hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, e->stream) != hipSuccess)
-                return TBC_ERR_DEVICE;
+                return failed(TBC_ERR_DEVICE);
             continue;
         }
         items.push_back(CopyItem{c.dst, c.src, c.bytes, (uint32_t)chunks, 0});
         chunks += (c.bytes + cb - 1) / cb;
         if (chunks > 0x7fffffffu) return TBC_ERR_INVALID_ARGUMENT;
     }
+    note_write(e); // (unaligned copies above were enqueued already)
     if (items.empty()) return TBC_OK;
     const uint64_t need = sizeof(CopyItem) * items.size();
     if (need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
     if (need > e->copy_desc_size) { // grows once (a stream drain)
-        if (hipStreamSynchronize(e->stream) != hipSuccess) return TBC_ERR_DEVICE;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return failed(TBC_ERR_DEVICE);
         if (e->copy_desc) hipFree(e->copy_desc);
         e->copy_desc = nullptr;
         e->copy_desc_size = 0;
         const uint64_t want = align_up(need, 1ull << 16);
-        if (hipMalloc((void **)&e->copy_desc, want) != hipSuccess) return TBC_ERR_OUT_OF_MEMORY;
+        if (hipMalloc((void **)&e->copy_desc, want) != hipSuccess) return failed(TBC_ERR_OUT_OF_MEMORY);
         e->copy_desc_size = want;
     }
     // The descriptors go through a pinned slot (a small one when they fit),
@@ -1131,7 +1070,7 @@ tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t
     const bool small = need <= DescRing::kSlotBytes;
     int slot = 0;
     uint8_t *host = small ? e->desc.take(&slot) : e->staging.take(&slot);
-    if (!host) return TBC_ERR_DEVICE;
+    if (!host) return failed(TBC_ERR_DEVICE);
     memcpy(host, items.data(), need);
     bool ok = launch_upload(e->copy_desc, host, need, e->stream) == 0 &&
               launch_copy_batch((const CopyItem *)e->copy_desc, (uint32_t)items.size(), (uint32_t)chunks,
@@ -1139,16 +1078,16 @@ tbc_status tbc_copy_device_batch(tbc_engine *e, const tbc_copy *copies, uint32_t
     hipEvent_t &ev = small ? e->desc.ev[slot] : e->staging.ev[slot];
     ok = hipEventRecord(ev, e->stream) == hipSuccess && ok;
     (small ? e->desc.used[slot] : e->staging.used[slot]) = true;
-    return ok ? TBC_OK : TBC_ERR_DEVICE;
+    return ok ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_memset_device(tbc_engine *e, void *dst, int value, uint64_t bytes) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
     if (!bytes) return TBC_OK;
     hipSetDevice(e->device);
-    if (!wait_seal(e) || !wait_sorts_ptr(e, dst, bytes) || hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess)
-        return TBC_ERR_DEVICE;
-    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    if (!wait_seal(e) || hipMemsetAsync(dst, value, bytes, e->stream) != hipSuccess)
+        return failed(TBC_ERR_DEVICE);
+    return hipStreamSynchronize(e->stream) == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 static bool sync_streams(tbc_engine *e) {
@@ -1156,8 +1095,6 @@ static bool sync_streams(tbc_engine *e) {
     flush_tail(e, true);
     bool ok = hipStreamSynchronize(e->stream) == hipSuccess;
     for (int t = 0; t < e->ntails; t++) ok = ok && hipStreamSynchronize(e->tail[t]) == hipSuccess;
-    ok = ok && (!e->sort_stream || hipStreamSynchronize(e->sort_stream) == hipSuccess);
-    retire_sorts(e);
     return ok;
 }
 
@@ -1169,38 +1106,42 @@ tbc_status tbc_engine_stream(tbc_engine *e, void **out_stream) {
 
 tbc_status tbc_synchronize(tbc_engine *e) {
     if (!e) return TBC_ERR_INVALID_ARGUMENT;
-    if (!sync_streams(e)) return TBC_ERR_DEVICE;
-    // Errors the device recorded for calls that had already returned.
-    // (Engine stream, not the null stream: nothing here waits behind a
-    // running chain server.)
-    uint32_t err[2] = {0, 0};
-    if (hipMemcpyAsync(err, e->d_error, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+    return sync_streams(e) ? TBC_OK : failed(TBC_ERR_DEVICE);
+}
+
+tbc_status tbc_manifest_close_status(tbc_grid *g) {
+    if (!g) return TBC_ERR_INVALID_ARGUMENT;
+    tbc_engine *e = g->engine;
+    hipSetDevice(e->device);
+    // The closes are engine-stream work: once the stream has passed them,
+    // the word holds whether any of them refused to link (set by the chain
+    // kernel), reported here once.
+    uint32_t err = 0;
+    if (hipMemcpyAsync(&err, g->d_error, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
-        return TBC_ERR_DEVICE;
-    if (err[0] || err[1]) {
-        if (hipMemsetAsync(e->d_error, 0, 8, e->stream) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess)
-            return TBC_ERR_DEVICE;
-        return err[1] ? TBC_ERR_DEVICE : TBC_ERR_BLOCK_INVALID; // [1]: the chain ring lost a task
-    }
-    return TBC_OK;
+        return failed(TBC_ERR_DEVICE);
+    if (!err) return TBC_OK;
+    if (hipMemsetAsync(g->d_error, 0, 4, e->stream) != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess)
+        return failed(TBC_ERR_DEVICE);
+    return TBC_ERR_BLOCK_INVALID;
 }
 
 tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const uint64_t *lengths, uint32_t count,
                               uint8_t *checksums_out) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(e);
     if (!e || (count && (!messages || !lengths || !checksums_out))) return TBC_ERR_INVALID_ARGUMENT;
     if (!count) return TBC_OK;
     for (uint32_t i = 0; i < count; i++)
         if (lengths[i] > 0xffffffffull || (lengths[i] && !messages[i])) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    if (!join_tails(e)) return TBC_ERR_DEVICE; // the messages may be blocks a batch tail still writes
+    if (!join_tails(e)) return failed(TBC_ERR_DEVICE); // the messages may be blocks a batch tail still writes
     uint64_t rd = 0, rh = 0; // regions for this synchronous call, closed before it returns
     uint8_t *d = e->dev.open(16ull * count + 16ull * count, &rd);
     uint8_t *h = d ? e->host.open(16ull * count + 16ull * count, &rh) : nullptr;
     if (!d || !h) {
         if (d) e->dev.close(rd);
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     uint64_t *hp = (uint64_t *)h;
     uint64_t *hl = hp + count;
@@ -1215,7 +1156,7 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
         hipMemcpyAsync(h + 16ull * count, d + 16ull * count, 16ull * count, hipMemcpyDeviceToHost, e->stream) !=
             hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
-        st = TBC_ERR_DEVICE;
+        st = failed(TBC_ERR_DEVICE);
     if (st == TBC_OK) memcpy(checksums_out, h + 16ull * count, 16ull * count);
     e->dev.close(rd);
     e->host.close(rh);
@@ -1224,7 +1165,7 @@ tbc_status tbc_checksum_batch(tbc_engine *e, const void *const *messages, const 
 
 tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const uint64_t *expect_checksums,
                                const uint64_t *expect_addresses, uint32_t count, uint8_t *results_out) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(e);
     if (!e || (count && (!blocks || !expect_checksums || !expect_addresses || !results_out)))
         return TBC_ERR_INVALID_ARGUMENT;
@@ -1232,14 +1173,14 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
     for (uint32_t i = 0; i < count; i++)
         if (!blocks[i] || ((uintptr_t)blocks[i] & 15)) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    if (!join_tails(e)) return TBC_ERR_DEVICE; // the messages may be blocks a batch tail still writes
+    if (!join_tails(e)) return failed(TBC_ERR_DEVICE); // the messages may be blocks a batch tail still writes
     const uint64_t in_bytes = 32ull * count, out_off = align_up(in_bytes, 256);
     uint64_t rd = 0, rh = 0; // regions for this synchronous call, closed before it returns
     uint8_t *d = e->dev.open(out_off + count, &rd);
     uint8_t *h = d ? e->host.open(out_off + count, &rh) : nullptr;
     if (!d || !h) {
         if (d) e->dev.close(rd);
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     uint64_t *hp = (uint64_t *)h, *hx = hp + count;
     for (uint32_t i = 0; i < count; i++) {
@@ -1254,7 +1195,7 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
                                e->stream) != 0 ||
         hipMemcpyAsync(h + out_off, d + out_off, count, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
-        st = TBC_ERR_DEVICE;
+        st = failed(TBC_ERR_DEVICE);
     if (st == TBC_OK) memcpy(results_out, h + out_off, count);
     e->dev.close(rd);
     e->host.close(rh);
@@ -1262,7 +1203,7 @@ tbc_status tbc_blocks_validate(tbc_engine *e, const void *const *blocks, const u
 }
 
 static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     if (!e || (count && !jobs)) return TBC_ERR_INVALID_ARGUMENT;
     std::vector<SortItem> items(count);
     for (uint32_t k = 0; k < count; k++) {
@@ -1279,44 +1220,39 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
                             j.values_out};
     }
     hipSetDevice(e->device);
-    // The bar-end sort runs on the engine stream. A sort stream of its own
-    // (opt-in, TBC_SORT_STREAM=1) lets it overlap the next half-bar's level
-    // compactions, but with GPU_MAX_HW_QUEUES=4 (the box's default) a fifth
-    // stream shares a hardware queue with a tail and inherits its order:
-    // round 3 measured config 1 130 vs 75 ms and config 3 4.28 vs 3.78 ms.
-    static const bool own_stream = getenv("TBC_SORT_STREAM") != nullptr; // A/B measurement only
-    hipStream_t ss = own_stream ? e->sort_stream : e->stream;
+    // The bar-end sort runs on the engine stream (a sort stream of its own
+    // shared a hardware queue with a tail and measured slower: round 3,
+    // config 1 130 vs 75 ms, config 3 4.28 vs 3.78 ms).
+    hipStream_t ss = e->stream;
     const uint64_t need = sort_scratch_bytes(items.data(), count);
     const uint64_t host_need = sort_host_bytes(items.data(), count);
     if (host_need > Staging::kSlotBytes) return TBC_ERR_CAPACITY;
     if (need > e->sort_scratch_size) { // grows once per larger bar (a stream drain)
-        if (hipStreamSynchronize(e->stream) != hipSuccess || (e->sort_stream && hipStreamSynchronize(e->sort_stream) != hipSuccess))
-            return TBC_ERR_DEVICE;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return failed(TBC_ERR_DEVICE);
         if (e->sort_scratch) hipFree(e->sort_scratch);
         e->sort_scratch = nullptr;
         e->sort_scratch_size = 0;
         const uint64_t want = align_up(need + need / 8, 1ull << 24);
         if (hipMalloc((void **)&e->sort_scratch, want) != hipSuccess) {
             e->sort_scratch = nullptr;
-            return TBC_ERR_OUT_OF_MEMORY;
+            return failed(TBC_ERR_OUT_OF_MEMORY);
         }
         e->sort_scratch_size = want;
     }
     const uint64_t words = sort_status_words(items.data(), count);
     if (words > e->sort_status_words) {
-        if (hipStreamSynchronize(e->stream) != hipSuccess || (e->sort_stream && hipStreamSynchronize(e->sort_stream) != hipSuccess))
-            return TBC_ERR_DEVICE;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return failed(TBC_ERR_DEVICE);
         if (e->sort_status) hipFree(e->sort_status);
         e->sort_status = nullptr;
         e->sort_status_words = 0;
         const uint64_t want = align_up(words + words / 8, 1ull << 20);
         if (hipMalloc((void **)&e->sort_status, 8 * want) != hipSuccess) {
             e->sort_status = nullptr;
-            return TBC_ERR_OUT_OF_MEMORY;
+            return failed(TBC_ERR_OUT_OF_MEMORY);
         }
         if (hipMemsetAsync(e->sort_status, 0, 8 * want, e->stream) != hipSuccess ||
             hipStreamSynchronize(e->stream) != hipSuccess)
-            return TBC_ERR_DEVICE;
+            return failed(TBC_ERR_DEVICE);
         e->sort_status_words = want;
     }
     // The descriptors go through a pinned slot (a small one when they fit),
@@ -1324,16 +1260,9 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
     const bool small = host_need <= DescRing::kSlotBytes;
     int slot = 0;
     uint8_t *host = small ? e->desc.take(&slot) : e->staging.take(&slot);
-    if (!host) return TBC_ERR_DEVICE;
+    if (!host) return failed(TBC_ERR_DEVICE);
     hipEvent_t &slot_ev = small ? e->desc.ev[slot] : e->staging.ev[slot];
-    retire_sorts(e);
-    if (ss != e->stream) { // after everything enqueued so far (the tables' puts and landings)
-        hipEvent_t fork = take_event(e);
-        const bool ok = fork && hipEventRecord(fork, e->stream) == hipSuccess &&
-                        hipStreamWaitEvent(ss, fork, 0) == hipSuccess;
-        if (fork) e->event_pool.push_back(fork); // the wait holds the recording it saw
-        if (!ok) return TBC_ERR_DEVICE;
-    }
+    note_write(e);
     int rc = launch_sort_batch(items.data(), count, e->sort_scratch, e->sort_scratch_size, e->sort_status,
                                e->sort_status_words, &e->sort_epoch, host, ss);
     if (hipEventRecord(slot_ev, ss) != hipSuccess) rc = -1;
@@ -1343,22 +1272,7 @@ static tbc_status sort_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t c
                 hipGetErrorString(err), (int)err);
     }
     (small ? e->desc.used[slot] : e->staging.used[slot]) = true;
-    if (ss != e->stream && rc == 0) {
-        tbc_engine::PendingSort ps;
-        ps.done = take_event(e);
-        for (uint32_t k = 0; k < count; k++)
-            if (jobs[k].count)
-                for (const void *p : {(const void *)jobs[k].values, (const void *)jobs[k].values_out})
-                    if (p) // read (and written in place), or written
-                        ps.ranges.push_back({(uint64_t)(uintptr_t)p,
-                                             (uint64_t)(uintptr_t)p + (uint64_t)jobs[k].count * jobs[k].tree.value_size});
-        if (!ps.done || hipEventRecord(ps.done, ss) != hipSuccess || hipEventRecord(e->sort_last, ss) != hipSuccess)
-            rc = -1;
-        else
-            e->pending_sorts.push_back(ps);
-        e->sort_recorded = true;
-    }
-    return rc == 0 ? TBC_OK : TBC_ERR_DEVICE;
+    return rc == 0 ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 tbc_status tbc_sort_values_batch(tbc_engine *e, const tbc_sort_job *jobs, uint32_t count) {
@@ -1378,7 +1292,7 @@ tbc_status tbc_sort_values(tbc_engine *e, const tbc_tree *tree, void *values, ui
     flush_tail(e);
     tbc_status st = tbc_sort_values_async(e, tree, values, count);
     if (st != TBC_OK) return st;
-    return tbc_synchronize(e);
+    return sync_streams(e) ? TBC_OK : failed(TBC_ERR_DEVICE);
 }
 
 // Host image of kway.hip's KPair (kway_pair_bytes() checks the size).
@@ -1389,7 +1303,7 @@ struct KPairHost {
 
 tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_segment *streams,
                                  uint32_t stream_count, uint32_t descending, void *out_values, tbc_kway **out) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(e);
     Layout L;
     if (!e || !tree || !out || (stream_count && !streams) || stream_count > TBC_KWAY_STREAMS_MAX ||
@@ -1406,9 +1320,8 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
     if (n >= 0x7fffffffull) return TBC_ERR_INVALID_ARGUMENT;
     if (n && !out_values) return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
-    if (!join_sorts(e)) return TBC_ERR_DEVICE; // the streams may be tables a sort still writes
     tbc_kway *k = new (std::nothrow) tbc_kway();
-    if (!k) return TBC_ERR_OUT_OF_MEMORY;
+    if (!k) return failed(TBC_ERR_OUT_OF_MEMORY);
     k->engine = e;
     if (!n) { // nothing to merge: complete at once
         k->complete = true;
@@ -1484,7 +1397,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
     if (need > e->kway_scratch_size) { // grows once per larger merge (a stream drain)
         if (hipStreamSynchronize(e->stream) != hipSuccess) {
             delete k;
-            return TBC_ERR_DEVICE;
+            return failed(TBC_ERR_DEVICE);
         }
         if (e->kway_scratch) hipFree(e->kway_scratch);
         e->kway_scratch = nullptr;
@@ -1493,7 +1406,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
         if (hipMalloc((void **)&e->kway_scratch, want) != hipSuccess) {
             e->kway_scratch = nullptr;
             delete k;
-            return TBC_ERR_OUT_OF_MEMORY;
+            return failed(TBC_ERR_OUT_OF_MEMORY);
         }
         e->kway_scratch_size = want;
     }
@@ -1503,7 +1416,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
     uint8_t *h = e->host.open(count_bytes + desc_bytes + 256, &k->host_region);
     if (!h) {
         delete k;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     k->arena = true;
     uint32_t *splits = (uint32_t *)scratch;
@@ -1537,6 +1450,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
     k->h_count = h_counts + (2 * TBC_KWAY_STREAMS_MAX); // the final count lands here
     const uint32_t final_slot = levels.back()[0].n_out;
     k->done = take_event(e);
+    note_write(e);
     bool ok = k->done && hipMemcpyAsync(d_counts, h_counts, count_bytes + desc_bytes, hipMemcpyHostToDevice, e->stream) ==
                         hipSuccess;
     di = 0;
@@ -1560,7 +1474,7 @@ tbc_status tbc_kway_merge_submit(tbc_engine *e, const tbc_tree *tree, const tbc_
         fprintf(stderr, "tbc: k-way merge enqueue failed: %s\n", hipGetErrorString(hipGetLastError()));
         hipStreamSynchronize(e->stream);
         tbc_kway_release(k);
-        return TBC_ERR_DEVICE;
+        return failed(TBC_ERR_DEVICE);
     }
     *out = k;
     return TBC_OK;
@@ -1574,7 +1488,7 @@ tbc_status tbc_kway_poll(tbc_kway *k) {
     if (q == hipErrorNotReady) return TBC_PENDING;
     if (q != hipSuccess) fprintf(stderr, "tbc: k-way merge failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
     k->complete = true;
-    k->result = q == hipSuccess ? TBC_OK : TBC_ERR_DEVICE;
+    k->result = q == hipSuccess ? TBC_OK : failed(TBC_ERR_DEVICE);
     if (k->result == TBC_OK) k->count = *k->h_count;
     return k->result;
 }
@@ -1586,7 +1500,7 @@ tbc_status tbc_kway_wait(tbc_kway *k) {
     if (const hipError_t q = hipEventSynchronize(k->done); q != hipSuccess) {
         fprintf(stderr, "tbc: k-way merge failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
         k->complete = true;
-        k->result = TBC_ERR_DEVICE;
+        k->result = failed(TBC_ERR_DEVICE);
         return k->result;
     }
     return tbc_kway_poll(k);
@@ -1623,57 +1537,13 @@ tbc_status tbc_kway_merge(tbc_engine *e, const tbc_tree *tree, const tbc_segment
     return st;
 }
 
-// Chain server, front side (engine stream, after the batch's bodies are in
-// place): the batch published under the next sequence number. Its descriptor
-// slot (sequence % kChainSlots) is free once the batch that held it has
-// completed (its tail's slot event): a caller with kChainSlots batches in
-// flight waits for the oldest here.
-static bool publish_chains(tbc_engine *e, tbc_batch *b, const JobDesc *d_jobs, int njobs, uint32_t dblocks,
-                           JobResultDev *d_res, uint8_t *d_infos, const uint32_t *d_ready, uint32_t *d_table_cnt,
-                           unsigned long long *d_done) {
-    if (!e->server || !dblocks) return true;
-    if (dblocks > kChainMaxTasks) return false;
-    auto &f = e->slot_fifo;
-    while (!f.empty() && event_query(e->slot_ev[f.front()]) == hipSuccess) f.erase(f.begin());
-    while (f.size() >= kChainSlots) {
-        if (hipEventSynchronize(e->slot_ev[f.front()]) != hipSuccess) return false;
-        f.erase(f.begin());
-    }
-    const unsigned long long seq = e->published++;
-    b->chain_slot = (uint32_t)(seq % kChainSlots);
-    b->chain_seq = seq;
-    f.push_back(b->chain_slot);
-    ChainBatch cb;
-    cb.jobs = d_jobs;
-    cb.res = d_res;
-    cb.infos = d_infos;
-    cb.ready = d_ready;
-    cb.table_cnt = d_table_cnt;
-    cb.done = d_done;
-    cb.njobs = njobs;
-    cb.ntasks = dblocks;
-    return launch_chain_publish(e->ring, cb, seq, e->stream) == 0;
-}
-
-// Chain server, tail side (after the batch's fork): a server instance queued
-// on the chain stream (it runs at once unless one is still running, whose
-// waves take these tasks too), and the batch's tail waits for its count.
-// Without the server: the batch's own chain and index-block kernels.
-static bool tail_chains(tbc_engine *e, tbc_batch *b, hipStream_t T, const JobDesc *d_jobs, int njobs, uint32_t dblocks,
+// A batch's chains (data-block headers and checksums) and index blocks on
+// tail stream T, after its front.
+static bool tail_chains(tbc_batch *b, hipStream_t T, const JobDesc *d_jobs, int njobs, uint32_t dblocks,
                         uint32_t tables, JobResultDev *d_res, uint8_t *d_infos, const uint64_t *d_status,
-                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready,
-                        unsigned long long *d_done, bool wide, bool compact) {
-    if (!e->server)
-        return launch_blocks_tail(d_jobs, njobs, dblocks, tables, d_res, d_infos, d_status, e->masks, d_block_tile,
-                                  d_splits, d_ready, T, mark_cb, b, compact) == 0;
-    if (!dblocks) return true;
-    bool ok = hipStreamWaitEvent(e->chain_stream, b->fork, 0) == hipSuccess &&
-              launch_chain_server(e->ring, b->chain_seq, wide ? e->wide_wgs : e->narrow_wgs,
-                                  wide ? e->wide_waves : e->narrow_waves, e->chain_stream) == 0 &&
-              launch_chain_wait(d_done, dblocks, d_res, (uint32_t)njobs, T) == 0 &&
-              hipEventRecord(e->slot_ev[b->chain_slot], T) == hipSuccess;
-    mark_cb(b, "chains");
-    return ok;
+                        const uint32_t *d_block_tile, const SplitDesc *d_splits, const uint32_t *d_ready, bool compact) {
+    return launch_blocks_tail(d_jobs, njobs, dblocks, tables, d_res, d_infos, d_status, b->engine->masks, d_block_tile,
+                              d_splits, d_ready, T, mark_cb, b, compact) == 0;
 }
 
 // Grid batch, tail after its chains and index blocks: the input checks
@@ -1705,8 +1575,6 @@ static int take_tail(tbc_engine *e) {
     return ti;
 }
 
-static const bool drain_full = getenv("TBC_DRAIN_COMPACT") == nullptr; // A/B: drains on compact tables too
-
 // A grid batch's whole tail on the next tail stream, after its front. A
 // drain (the caller waits next: no front follows to share the CUs with)
 // runs the chains on the full tables, one chain per SIMD (latency regime).
@@ -1718,8 +1586,8 @@ static bool grid_tail_alone(tbc_engine *e, tbc_batch *b, bool drain) {
     b->mark_stream = T;
     mark_cb(b, "tail_wait");
     if (ok && g.half.njobs)
-        ok = tail_chains(e, b, T, g.half.jobs, g.half.njobs, g.half.dblocks, g.half.tables, g.half.res, g.half.infos,
-                         g.status, g.block_tile, g.splits, g.half.ready, g.done_ctr, g.wide, !(drain && drain_full));
+        ok = tail_chains(b, T, g.half.jobs, g.half.njobs, g.half.dblocks, g.half.tables, g.half.res, g.half.infos,
+                         g.status, g.block_tile, g.splits, g.half.ready, !drain);
     return ok && grid_tail_rest(e, b, ti);
 }
 
@@ -1750,18 +1618,18 @@ static void flush_tail(tbc_engine *e, bool drain) {
     e->deferred = nullptr;
     if (!grid_tail_alone(e, p, drain)) {
         p->complete = true;
-        p->result = TBC_ERR_DEVICE;
+        p->result = failed(TBC_ERR_DEVICE);
     }
 }
 
 static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint32_t count, bool pipeline,
                               tbc_batch **out) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     if (!e || !out || (count && !jobs_in)) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     hipSetDevice(e->device);
     tbc_batch *b = new (std::nothrow) tbc_batch();
-    if (!b) return TBC_ERR_OUT_OF_MEMORY;
+    if (!b) return failed(TBC_ERR_OUT_OF_MEMORY);
     b->engine = e;
     b->count = count;
     b->info_base.resize(count);
@@ -1918,7 +1786,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     for (uint32_t i = 0; i < count; i++) all_tiles += hj[i].tile_count;
     if (!ensure_masks(e, all_tiles * (2 * kMergeTile / 64))) {
         delete b;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     std::vector<JobDesc> sj(count);
     uint32_t tiles = 0, splits = 0, dblocks = 0, tables = 0, infos = 0;
@@ -1956,24 +1824,22 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // pipelines), or always / never with TBC_CONFIG_PIPELINE / _LATENCY.
     const bool spec_pipe = spec_regime && !(e->flags & TBC_CONFIG_LATENCY) &&
                            ((e->flags & TBC_CONFIG_PIPELINE) || !e->tail_out.empty());
-    // Grid batches may merge speculated jobs tile by tile too (k_merge_unique:
-    // bodies written once, R + W instead of the mask merge + assembly's R +
-    // 2 W), but config 1 measured slower that way (54.2 vs 52.1 ms per step,
-    // one box): its half-bars are small, and the speculation's extra
-    // launches and recompute phase cost more than the assembly they save.
-    // TBC_GRID_SPECULATION=1 turns it on (A/B and its parity tests).
-    static const bool grid_spec = getenv("TBC_GRID_SPECULATION") != nullptr;
+    // (Grid batches do not speculate: round 4 merged their UNIQUE_KEYS jobs
+    // tile by tile too — bodies written once, R + W instead of the mask merge
+    // + assembly's R + 2 W — and config 1 measured slower, 54.2 vs 52.1 ms
+    // per step: its half-bars are small, and the speculation's extra launches
+    // and recompute phase cost more than the assembly they save. That A/B
+    // path was removed in round 6.)
     bool any_unique = false;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
-        d.unique = (spec_regime || (grid_mode && grid_spec)) &&
-                   (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) && d.dblock_max > 0;
+        d.unique = spec_regime && (jobs_in[d.job_index].flags & TBC_COMPACTION_UNIQUE_KEYS) && d.dblock_max > 0;
         any_unique |= d.unique != 0;
     }
     // Pipelined: the speculated jobs' tiles of kUniqueTile positions and
     // their merge-path splits (merge.hip k_merge_unique; round 4 measured it
     // faster than one producer wave per block).
-    const bool unique_tiles = any_unique && (spec_pipe || grid_mode);
+    const bool unique_tiles = any_unique && spec_pipe;
     uint32_t utiles = 0, usplits = 0;
     for (uint32_t k = 0; k < count; k++) {
         JobDesc &d = sj[k];
@@ -1988,11 +1854,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         }
     }
 
-    // Chain server geometry (tail_chains): the front fits beside a chain
-    // workgroup when every job merges by k_merge_unique or by the
-    // timestamp-key mask merge.
-    bool wide_front = !grid_mode;
-    for (uint32_t k = 0; k < count; k++) wide_front &= sj[k].unique || sj[k].key_kind == kKeyTimestamp;
     // Device layout of the batch.
     const uint64_t sz_jobs = align_up(sizeof(JobDesc) * (uint64_t)count, 256);
     const uint64_t sz_segs = align_up(8 * seg_words + 4 * seg_words, 256);
@@ -2010,7 +1871,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     // tile status, block tiles, per-block landed counts, the assembling
     // merge's look-back words (one per tile) and its ticket counters
-    // (+ the chain server's done count and per-table block counts)
     const uint64_t sz_tiles = align_up(8ull * tiles + 8ull * dblocks + 8 + 8ull * tiles + 16 + 32 + 8 + 4ull * tables, 256);
     const uint64_t sz_res = align_up(sizeof(JobResultDev) * (uint64_t)count, 256);
     const uint64_t sz_infos = align_up(kTableInfoSize * (uint64_t)infos, 256);
@@ -2019,7 +1879,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     if (!dbase || !hbase) {
         if (dbase) e->dev.close(b->dev_region);
         delete b;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     uint8_t *d_in = dbase;
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
@@ -2030,8 +1890,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     uint32_t *d_ready = d_block_tile + dblocks;
     uint64_t *d_lookback = (uint64_t *)(uintptr_t)align_up((uint64_t)(uintptr_t)(d_ready + dblocks + 2), 8);
     uint32_t *d_ticket = (uint32_t *)(d_lookback + tiles);
-    unsigned long long *d_done = (unsigned long long *)(d_ticket + 8); // chain server: tasks finished
-    uint32_t *d_table_cnt = d_ticket + 10;                             // chain server: blocks per table
     const bool merge_bodies = false;
     JobResultDev *d_res = (JobResultDev *)(dbase + sz_in + sz_splits + sz_tiles);
     uint8_t *d_infos = dbase + sz_in + sz_splits + sz_tiles + sz_res;
@@ -2124,22 +1982,14 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
 
     hipStream_t s = e->stream;
     bool ok = true;
-    // Inputs a sort is still writing (a bar's memtables): wait for that sort.
-    retire_sorts(e);
-    if (!e->pending_sorts.empty())
-        for (uint32_t i = 0; ok && i < count; i++)
-            for (int side = 0; ok && side < 2; side++)
-                for (const auto &g : seg_in[2 * (size_t)i + side])
-                    if (g.first && !(ok = wait_sorts(e, g.first, g.first + (uint64_t)g.second * hj[i].value_size)))
-                        break;
     // A pipelined batch of speculated jobs whose inputs no batch in flight
-    // is writing and no sort is sorting: its descriptors go up and its
+    // is writing: its descriptors go up and its
     // partition runs on the tail its chains will take (idle by then: three
     // batches back), so the engine stream goes from the previous batch's
     // merge straight to this one's (config 2: ~60 us of upload, partition
     // and launch gaps per step off the engine stream).
     hipStream_t P = s;
-    if (spec_pipe && !grid_mode && !e->server && !(e->flags & TBC_CONFIG_LATENCY)) {
+    if (spec_pipe && !grid_mode && !(e->flags & TBC_CONFIG_LATENCY)) {
         bool early = count > 0;
         for (uint32_t k = 0; k < count && early; k++) early = sj[k].unique != 0;
         for (uint32_t i = 0; i < count && early; i++)
@@ -2148,15 +1998,24 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                     const uint64_t lo = g.first, hi = g.first + (uint64_t)g.second * hj[i].value_size;
                     for (const auto &t : e->tail_out)
                         for (const auto &r : t.ranges) early = early && !(lo < r.second && r.first < hi);
-                    for (const auto &ps : e->pending_sorts)
-                        for (const auto &r : ps.ranges) early = early && !(lo < r.second && r.first < hi);
                     if (!early) break;
                 }
         if (early) {
             b->prep = take_event(e);
-            if (b->prep) P = e->tail[e->next_tail];
+            if (b->prep) {
+                P = e->tail[e->next_tail];
+                // Inputs the engine stream wrote (puts, sorts, copies, earlier
+                // batches' outputs not in tail_out) are read here off that
+                // stream: P waits for the last such write.
+                ok = order_after_writes(e, P);
+            }
         }
     }
+    // This batch's engine-stream outputs, unless its tail lists them in
+    // tail_out (the pipelined and latency-regime speculated batches do).
+    const bool outputs_tracked = !grid_mode && !(flags0 & TBC_COMPACTION_COUNT_ONLY) &&
+                                 (pipeline || (any_unique && spec_regime));
+    if (!outputs_tracked) note_write(e);
     // The descriptors up; tile status, block tiles and results zeroed
     // (contiguous) by the same launch.
     ok = ok && launch_upload(d_in, h_in, sz_in, P, d_status, sz_tiles + sz_res) == 0;
@@ -2170,29 +2029,14 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && !resolve.empty())
             ok = launch_grid_resolve(d_resolve, (uint32_t)resolve.size(), (uint64_t *)(uintptr_t)dev_seg, d_checks,
                                      grid0->base, grid0->block_count, e->block_size, d_res, s) == 0;
-        // Speculated jobs (UNIQUE_KEYS) merged tile by tile straight into
-        // their blocks; the others by the mask merge and k_assemble; broken
-        // speculations recomputed by the merge path (phase 1) before the
-        // index block layout reads the final shapes.
-        if (ok && unique_tiles)
-            ok = launch_merge_unique((const JobDesc *)d_in, sj.data(), (int)count, d_usplits, d_res, d_ticket + 5, s,
-                                     mark_cb, b) == 0;
+        // The mask merge, then the bodies (k_assemble) and the index
+        // blocks' data addresses.
         if (ok && count)
             ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
                               d_block_tile, d_order, d_res, s, mark_cb, b) == 0;
-        if (ok && any_unique)
-            ok = launch_merge((const JobDesc *)d_in, sj.data(), (int)count, d_splits, d_status, e->masks,
-                              d_block_tile, d_order, d_res, s, mark_cb, b, 1) == 0;
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
-        if (ok && any_unique) {
-            ok = launch_assemble((const JobDesc *)d_in, (int)count, tiles, d_ready, d_res, d_status, e->masks,
-                                 d_splits, 1, s) == 0;
-            mark_cb(b, "recompute_assemble");
-        }
-        ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
-                                  d_table_cnt, d_done);
         b->fork = take_event(e);
         ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess;
         auto &g = b->gt;
@@ -2200,21 +2044,19 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         g.status = d_status;
         g.block_tile = d_block_tile;
         g.splits = d_splits;
-        g.done_ctr = d_done;
-        g.wide = wide_front;
         g.resolve = d_resolve;
         g.n_resolve = (uint32_t)resolve.size();
         g.n_checks = (uint32_t)n_checks;
         g.checks = d_checks;
         g.grid = grid0;
         g.copy_bytes = sz_res + sz_infos;
-        const bool pairable = e->pair_tails && !e->server && count && dblocks;
+        const bool pairable = e->pair_tails && count && dblocks;
         if (ok && pairable && e->deferred) {
             tbc_batch *p = e->deferred;
             e->deferred = nullptr;
             if (!grid_tail_pair(e, p, b)) {
                 p->complete = true;
-                p->result = TBC_ERR_DEVICE;
+                p->result = failed(TBC_ERR_DEVICE);
                 ok = false;
             }
         } else if (ok && pairable) {
@@ -2233,8 +2075,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         if (ok && count)
             ok = launch_blocks_front((const JobDesc *)d_in, (int)count, tiles, dblocks, d_ready, d_res, d_status,
                                      e->masks, d_splits, s, mark_cb, b, merge_bodies) == 0;
-        ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
-                                  d_table_cnt, d_done);
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
@@ -2243,8 +2083,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         b->mark_stream = T;
         mark_cb(b, "tail_wait");
         if (ok && count)
-            ok = tail_chains(e, b, T, (const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
-                             d_block_tile, d_splits, d_ready, d_done, wide_front, false);
+            ok = tail_chains(b, T, (const JobDesc *)d_in, (int)count, dblocks, tables, d_res, d_infos, d_status,
+                             d_block_tile, d_splits, d_ready, false);
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {
@@ -2293,8 +2133,6 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
                                 d_res, s, mark_cb, b, 1) == 0;
         ok = ok && launch_assemble(dj, (int)count, tiles, d_ready, d_res, d_status, e->masks, d_splits, 1, s) == 0;
         mark_cb(b, "recompute_assemble");
-        ok = ok && publish_chains(e, b, (const JobDesc *)d_in, (int)count, dblocks, d_res, d_infos, d_ready,
-                                  d_table_cnt, d_done);
         const int ti = e->next_tail;
         e->next_tail = (e->next_tail + 1) % e->ntails;
         hipStream_t T = e->tail[ti];
@@ -2302,8 +2140,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         ok = ok && b->fork && hipEventRecord(b->fork, s) == hipSuccess && hipStreamWaitEvent(T, b->fork, 0) == hipSuccess;
         b->mark_stream = T;
         mark_cb(b, "tail_wait");
-        ok = ok && tail_chains(e, b, T, dj, (int)count, dblocks, tables, d_res, d_infos, d_status, d_block_tile,
-                               d_splits, d_ready, d_done, wide_front, false);
+        ok = ok && tail_chains(b, T, dj, (int)count, dblocks, tables, d_res, d_infos, d_status, d_block_tile,
+                               d_splits, d_ready, false);
         ok = ok && hipMemcpyAsync(b->h_results, d_res, sz_res + sz_infos, hipMemcpyDeviceToHost, T) == hipSuccess;
         ok = ok && hipEventRecord(b->done, T) == hipSuccess && hipEventRecord(e->tail_ev[ti], T) == hipSuccess;
         if (ok) {
@@ -2374,7 +2212,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     if (!ok) {
         sync_streams(e);
         tbc_batch_release(b);
-        return TBC_ERR_DEVICE;
+        return failed(TBC_ERR_DEVICE);
     }
     *out = b;
     return TBC_OK;
@@ -2440,7 +2278,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
                         break;
                     }
             }
-            if (alias && hipStreamWaitEvent(e->stream, pend[k].done, 0) != hipSuccess) return TBC_ERR_DEVICE;
+            if (alias && hipStreamWaitEvent(e->stream, pend[k].done, 0) != hipSuccess) return failed(TBC_ERR_DEVICE);
             k++;
         }
     }
@@ -2459,7 +2297,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
             for (uint32_t k = 0; k < c.segment_count_b; k++) n[i] += c.segments_b[k].count;
             waves += (n[i] + L.vcm - 1) / L.vcm / 2;
         }
-        static const uint32_t max_groups = getenv("TBC_GROUPS") ? (uint32_t)atoi(getenv("TBC_GROUPS")) : kMaxGroups;
+        const uint32_t max_groups = kMaxGroups;
         const uint64_t min_waves = fused_max_chain_waves();
         if (waves > min_waves && max_groups > 1) groups = std::min<uint32_t>(max_groups, count);
     }
@@ -2470,7 +2308,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
     uint64_t total = 0;
     for (uint32_t i = 0; i < count; i++) total += n[i];
     tbc_batch *parent = new (std::nothrow) tbc_batch();
-    if (!parent) return TBC_ERR_OUT_OF_MEMORY;
+    if (!parent) return failed(TBC_ERR_OUT_OF_MEMORY);
     parent->engine = e;
     parent->count = count;
     parent->job_map.resize(count);
@@ -2501,7 +2339,7 @@ tbc_status tbc_compaction_submit(tbc_engine *e, const tbc_compaction *jobs_in, u
 }
 
 tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **out) {
-    (void)hipGetLastError(); // an earlier call's stale error is not this call's (launch checks read it)
+    if (!no_stale_error()) return TBC_ERR_DEVICE; // an earlier call's unreported failure
     flush_tail(e);
     if (!e || !sl || !out) return TBC_ERR_INVALID_ARGUMENT;
     *out = nullptr;
@@ -2515,7 +2353,7 @@ tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **ou
         return TBC_ERR_INVALID_ARGUMENT;
     hipSetDevice(e->device);
     tbc_batch *b = new (std::nothrow) tbc_batch();
-    if (!b) return TBC_ERR_OUT_OF_MEMORY;
+    if (!b) return failed(TBC_ERR_OUT_OF_MEMORY);
     b->engine = e;
     b->count = 1;
     b->info_base.assign(1, 0);
@@ -2574,7 +2412,7 @@ tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **ou
     if (!dbase || !hbase) {
         if (dbase) e->dev.close(b->dev_region);
         delete b;
-        return TBC_ERR_OUT_OF_MEMORY;
+        return failed(TBC_ERR_OUT_OF_MEMORY);
     }
     d.addresses = (const uint64_t *)(dbase + sz_job);
     memcpy(hbase, &d, sizeof d);
@@ -2607,15 +2445,31 @@ tbc_status tbc_compaction_seal(tbc_engine *e, const tbc_seal *sl, tbc_batch **ou
         tbc_engine::TailOutputs to;
         to.done = take_event(e);
         ok = to.done && hipEventRecord(to.done, T) == hipSuccess;
-        const uint64_t lo = (uint64_t)(uintptr_t)sl->output_blocks;
-        to.ranges.push_back({lo, lo + (uint64_t)sl->address_count * e->block_size});
+        // Only the slots this seal writes (a split rank's output_blocks is
+        // its allocation minus the slots before it: ADVICE r5): its data
+        // blocks, and the index blocks of their tables and of the sealed ones.
+        const uint64_t base = (uint64_t)(uintptr_t)sl->output_blocks, bs = e->block_size;
+        auto k_last = [&](uint64_t t) { return std::min<uint64_t>((t + 1) * L.dbcm, db) - 1; };
+        uint64_t s_lo = UINT64_MAX, s_hi = 0;
+        auto span = [&](uint64_t slot) { s_lo = std::min(s_lo, slot); s_hi = std::max(s_hi, slot + 1); };
+        if (sl->block_count) {
+            const uint64_t k0 = sl->block_first, k1 = k0 + sl->block_count - 1;
+            span(data_block_slot((uint32_t)k0, L.dbcm));
+            span(index_block_slot((uint32_t)(k1 / L.dbcm), (uint32_t)k_last(k1 / L.dbcm)));
+        }
+        if (sl->table_count) {
+            span(index_block_slot(sl->table_first, (uint32_t)k_last(sl->table_first)));
+            const uint64_t t1 = (uint64_t)sl->table_first + sl->table_count - 1;
+            span(index_block_slot((uint32_t)t1, (uint32_t)k_last(t1)));
+        }
+        if (s_hi > s_lo) to.ranges.push_back({base + s_lo * bs, base + s_hi * bs});
         if (ok) e->tail_out.push_back(std::move(to));
         else if (to.done) e->event_pool.push_back(to.done);
     }
     if (!ok) {
         sync_streams(e);
         tbc_batch_release(b);
-        return TBC_ERR_DEVICE;
+        return failed(TBC_ERR_DEVICE);
     }
     *out = b;
     return TBC_OK;
@@ -2656,7 +2510,7 @@ tbc_status tbc_batch_poll(tbc_batch *b) {
     if (q != hipSuccess) {
         fprintf(stderr, "tbc: batch failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
         b->complete = true;
-        b->result = TBC_ERR_DEVICE;
+        b->result = failed(TBC_ERR_DEVICE);
         return b->result;
     }
     return batch_finish(b);
@@ -2683,7 +2537,7 @@ tbc_status tbc_batch_wait(tbc_batch *b) {
     if (q != hipSuccess) {
         fprintf(stderr, "tbc: batch failed on the device: %s (%d)\n", hipGetErrorString(q), (int)q);
         b->complete = true;
-        b->result = TBC_ERR_DEVICE;
+        b->result = failed(TBC_ERR_DEVICE);
         return b->result;
     }
     return batch_finish(b);
@@ -2697,7 +2551,7 @@ tbc_status tbc_batch_result(tbc_batch *b, uint32_t index, tbc_compaction_result 
         const auto m = b->job_map[index];
         return tbc_batch_result(b->children[m.first], m.second, out, table_infos, table_info_capacity);
     }
-    if (b->result == TBC_ERR_DEVICE) return TBC_ERR_DEVICE;
+    if (b->result == TBC_ERR_DEVICE) return failed(TBC_ERR_DEVICE);
     const JobResultDev &r = b->h_results[index];
     out->value_count = r.value_count;
     out->data_block_count = r.data_block_count;
@@ -2724,7 +2578,7 @@ tbc_status tbc_batch_speculation(tbc_batch *b, uint32_t index, uint32_t *out) {
         const auto m = b->job_map[index];
         return tbc_batch_speculation(b->children[m.first], m.second, out);
     }
-    if (b->result == TBC_ERR_DEVICE) return TBC_ERR_DEVICE;
+    if (b->result == TBC_ERR_DEVICE) return failed(TBC_ERR_DEVICE);
     *out = b->h_results[index].spec;
     return TBC_OK;
 }
@@ -2763,7 +2617,7 @@ tbc_status tbc_batch_kernel_times(tbc_batch *b, const char **names, double *us, 
     uint32_t n = 0;
     for (int m = 1; m < b->nmarks && n < capacity; m++) {
         float ms = 0;
-        if (hipEventElapsedTime(&ms, b->marks[m - 1], b->marks[m]) != hipSuccess) return TBC_ERR_DEVICE;
+        if (hipEventElapsedTime(&ms, b->marks[m - 1], b->marks[m]) != hipSuccess) return failed(TBC_ERR_DEVICE);
         if (names) names[n] = b->mark_names[m];
         if (us) us[n] = ms * 1000.0;
         n++;

@@ -119,10 +119,7 @@ __device__ __forceinline__ uint32_t merge_path_split_wave(const JobDesc &j, uint
 // us), the unique merges' at 4,096.
 constexpr uint32_t kWaveSplitsMax = 4096;
 constexpr uint32_t kWaveSplitsMaxMask = 12288;
-static uint32_t wave_splits_max() { // A/B: TBC_WAVE_SPLITS
-    static const uint32_t v = getenv("TBC_WAVE_SPLITS") ? (uint32_t)atoi(getenv("TBC_WAVE_SPLITS")) : kWaveSplitsMaxMask;
-    return v;
-}
+static uint32_t wave_splits_max() { return kWaveSplitsMaxMask; }
 
 template <int KIND, bool Wave>
 __device__ __forceinline__ uint32_t split_at(const JobDesc &j, uint32_t d) {

@@ -521,7 +521,13 @@ __device__ __forceinline__ void sort_pass_tiles(PassShared &sh, const SortSeg *s
         // Null counter (one tile per workgroup): the tile is the workgroup's
         // index. Workgroups are dispatched in index order on each XCD, so the
         // lowest undispatched tile's XCD only holds tiles below it, which
-        // wait only on tiles further below: they finish and it is dispatched.
+        // wait only on tiles further below: they finish and it is dispatched
+        // (other kernels' workgroups on its CUs, e.g. chains on a tail
+        // stream, never wait on this sort, so they leave too). HIP does not
+        // promise that dispatch order; were it broken, a look-back wait
+        // would reach its bound (2^24 sleeps, below) and mark the batch
+        // broken, and k_sort_rescue re-sorts its tables: slower, still in
+        // order, never a hang. TBC_SORT_TICKETS=1 keeps the tickets always.
         // (Config 1's passes 30.2 -> 24.9 us: the ticket's device-scope
         // atomic, one per tile on one word, cost ~5 us per pass.)
         if (tid == 0) sh.next = tile_counter ? atomicAdd(&tile_counter[p], 1u) : (first ? blockIdx.x : ntiles);

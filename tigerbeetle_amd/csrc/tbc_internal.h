@@ -175,41 +175,6 @@ struct ResolveItem {
     uint32_t pad;
 };
 
-// Chain server (aegis.hip k_chain_server, round 5). A batch's data blocks are
-// chain tasks: its front publishes them into one device ring shared by every
-// batch in flight, and the server's waves — any number of batches' chains at
-// once, as many as its workgroups hold — finish each block (AEGIS body and
-// header checksums, header, index entry) and the last block of a table seals
-// its index block and TableInfo. A batch is complete when `done` reaches its
-// task count (k_chain_wait on a tail stream).
-struct ChainBatch {
-    const JobDesc *jobs;
-    JobResultDev *res;
-    uint8_t *infos;          // TableInfo slots (info_base of each job)
-    const uint32_t *ready;   // per data block: values the front landed (k_assemble), or null
-    uint32_t *table_cnt;     // per output table (batch-wide numbering): its finished data blocks
-    unsigned long long *done; // tasks finished (every claimed task counts once, after its outputs)
-    int32_t njobs;
-    uint32_t ntasks;         // data blocks of the batch (upper bound: dblock_max per job)
-};
-static_assert(sizeof(ChainBatch) == 56, "ChainBatch layout");
-constexpr uint32_t kChainSlots = 256; // batches in flight (ChainRing.batches)
-
-struct ChainRing {
-    // Per descriptor slot, the claim word of the batch in it: sequence
-    // (63..40) | tasks (39..20) | tasks claimed (19..0). Tasks are implicit:
-    // task t of a batch is its data block t, so a claim is one fetch_add of
-    // 2 (no retry storm on one word). The publisher writes the word last.
-    unsigned long long *claim;
-    unsigned long long *pub;   // batches published (sequence numbers 0 .. pub - 1)
-    uint32_t *active;          // waves of the running instance holding tasks
-    unsigned long long *closing; // the instance (its first_seq + 1) that has decided to leave
-    ChainBatch *batches;       // kChainSlots descriptors (batch sequence % kChainSlots)
-    uint32_t linger;           // 100 MHz ticks an idle wave polls before it leaves
-    uint32_t backoff_max;      // an idle wave's longest pause between polls (units of s_sleep 63, ~1.7 us)
-};
-constexpr uint32_t kChainMaxTasks = (1u << 19) - 1; // a batch's data blocks (20-bit count fields)
-
 // Slot (= index into the acquire-order address list / output arena) of data
 // block `k`: every earlier table consumed dbcm data blocks plus one index block.
 __host__ __device__ inline uint32_t data_block_slot(uint32_t k, uint32_t dbcm) { return k + k / dbcm; }
@@ -419,16 +384,6 @@ int launch_index_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_tables,
 // their index entries, then its index blocks from the entries in place.
 int launch_seal(const JobDesc *d_job, uint32_t blocks, uint32_t tables, JobResultDev *d_results, uint8_t *d_infos,
                 void *stream);
-// Chain server: publish batch `seq` (its cb.ntasks data blocks, after its
-// front, on the engine stream); a server instance (`wgs` workgroups of
-// `waves` chain waves, on the chain stream; every batch before first_seq is
-// claimed already; it leaves once nothing has been claimable for r.linger);
-// the wait for a batch's chains and seals (its tail stream; on a time-out
-// every job of the batch is marked with an invariant error).
-int launch_chain_publish(const ChainRing &r, const ChainBatch &cb, unsigned long long seq, void *stream);
-int launch_chain_server(const ChainRing &r, unsigned long long first_seq, uint32_t wgs, uint32_t waves, void *stream);
-int launch_chain_wait(const unsigned long long *done, uint32_t target, JobResultDev *d_results, uint32_t njobs,
-                      void *stream);
 // The bodies of the jobs the merge decided (k_assemble; phase 0 / 1 as
 // phase_skips).
 int launch_assemble(const JobDesc *d_jobs, int njobs, uint32_t total_tiles, uint32_t *d_ready,
@@ -441,7 +396,7 @@ int launch_grid_validate(const InputCheck *d_checks, uint32_t count, uint8_t *d_
 int launch_grid_mark(const JobDesc *d_jobs, int njobs, uint8_t *d_verified, const JobResultDev *d_results,
                      void *stream);
 // The chain-wave count above which a batch is in the throughput regime
-// (aegis.hip; TBC_FUSED_MAX_WAVES overrides it for A/B measurement).
+// (aegis.hip).
 uint32_t fused_max_chain_waves();
 // ManifestLog.close_block of `count` staged manifest blocks (grid addresses in
 // d_addresses): body checksums, then the header chain in order.

@@ -168,6 +168,12 @@ class Grid:
               "tbc_grid_get_blocks")
         return out[:n]
 
+    def manifest_close_status(self) -> None:
+        """tbc_manifest_close_status: wait for the manifest closes enqueued on
+        this grid; raise TbcError(TBC_ERR_BLOCK_INVALID) once if one refused
+        to link onto an untrusted previous block."""
+        check(lib().tbc_manifest_close_status(self.handle), "tbc_manifest_close_status")
+
     def invalidate(self) -> None:
         """tbc_grid_invalidate: a restart's cold cache (every block validated before use)."""
         check(lib().tbc_grid_invalidate(self.handle), "tbc_grid_invalidate")

@@ -371,7 +371,9 @@ class GridManifestStore:
 
     def checksum(self, address: int) -> int:
         """A closed block's header checksum (what the checkpoint's
-        references record for the log's newest block, manifest_log.zig:783-809)."""
+        references record for the log's newest block, manifest_log.zig:783-809).
+        Raises if a close of this grid was refused (tbc_manifest_close_status)."""
+        self.grid.manifest_close_status()
         blk = self.grid.get_blocks([address])[0]
         return int.from_bytes(blk[:16].tobytes(), "little")
 

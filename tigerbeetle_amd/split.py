@@ -328,13 +328,22 @@ class TorchExchange:
         import torch
         return torch.cuda.ExternalStream(engine.stream_handle(), device=self.device)
 
+    def _alloc(self, n: int, dtype):
+        """A device tensor the engine stream writes: allocated (on torch's
+        stream) and made ready before any engine-stream work touches it —
+        the engine stream does not wait for torch's streams."""
+        import torch
+        t = torch.empty(n, dtype=dtype, device=self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        return t
+
     def count_buffer(self, engine, scratch: dict):
         """Where the count merge stores its count (device, u64)."""
         if self.on_device:
             import torch
             t = scratch.get("count_t")
             if t is None:
-                t = scratch["count_t"] = torch.zeros(2, dtype=torch.int64, device=self.device)
+                t = scratch["count_t"] = self._alloc(2, torch.int64)
             return _Ptr(t.data_ptr())
         buf = scratch.get("count_buf")
         if buf is None:
@@ -344,10 +353,10 @@ class TorchExchange:
     def gather_counts(self, engine, count_batch, count_buf, scratch: dict) -> list:
         import torch
         if self.on_device:
+            out = scratch.get("counts_t")
+            if out is None:
+                out = scratch["counts_t"] = self._alloc(self.world, torch.int64)
             with torch.cuda.stream(self._stream(engine)):
-                out = scratch.get("counts_t")
-                if out is None:
-                    out = scratch["counts_t"] = torch.zeros(self.world, dtype=torch.int64, device=self.device)
                 self.dist.all_gather_into_tensor(out, scratch["count_t"][:1])
                 return [int(x) for x in out.cpu()]  # the step's one host wait
         count_batch.wait()
@@ -365,8 +374,8 @@ class TorchExchange:
         if self.on_device:
             mine, out = scratch.get(key + "_mine"), scratch.get(key + "_out")
             if mine is None or mine.numel() < nbytes:
-                mine = scratch[key + "_mine"] = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
-                out = scratch[key + "_out"] = torch.zeros(self.world * nbytes, dtype=torch.uint8, device=self.device)
+                mine = scratch[key + "_mine"] = self._alloc(nbytes, torch.uint8)
+                out = scratch[key + "_out"] = self._alloc(self.world * nbytes, torch.uint8)
             copies, off = [], 0
             for ptr, n in segments:
                 copies.append((mine.data_ptr() + off, ptr, n))
