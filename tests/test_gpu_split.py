@@ -117,23 +117,32 @@ def _run_rank(name, rank, world, exchange, max_engine_waits=None):
         return True, f"rank {rank}: blocks {res.blocks} tables {res.tables} OK ({len(slots)} slots)"
 
 
+_WAITS = None
+
+
 def _count_engine_waits():
-    """Count the engine's host waits from now on; returns a function that
-    stops counting and gives the count."""
+    """Count this thread's engine host waits (Batch.wait, synchronize,
+    downloads) from now on; returns a function that stops counting and gives
+    the count. The methods are wrapped once per process; each thread counts
+    only its own calls (ranks may be threads of one process)."""
+    import threading
     from tigerbeetle_amd import engine as E
-    n = [0]
-    saved = {(cls, m): getattr(cls, m) for cls, m in ((E.Batch, "wait"), (E.Engine, "synchronize"),
-                                                       (E.DeviceBuffer, "download"))}
-    for (cls, m), f in saved.items():
-        def counted(*a, _f=f, **k):
-            n[0] += 1
-            return _f(*a, **k)
-        setattr(cls, m, counted)
+    global _WAITS
+    if _WAITS is None:
+        _WAITS = threading.local()
+        for cls, m in ((E.Batch, "wait"), (E.Engine, "synchronize"), (E.DeviceBuffer, "download")):
+            f = getattr(cls, m)
+
+            def counted(*a, _f=f, **k):
+                if getattr(_WAITS, "on", False):
+                    _WAITS.n += 1
+                return _f(*a, **k)
+            setattr(cls, m, counted)
+    _WAITS.on, _WAITS.n = True, 0
 
     def stop():
-        for (cls, m), f in saved.items():
-            setattr(cls, m, f)
-        return n[0]
+        _WAITS.on = False
+        return _WAITS.n
     return stop
 
 
@@ -383,6 +392,7 @@ def test_split_device_exchange_stream_order(name, world):
     from tigerbeetle_amd import split
     d = _StreamDist(world)
     results = [None] * world
+    _count_engine_waits()()  # wrap the wait methods once, before the rank threads start
 
     def run(r):
         d.local.rank = r

@@ -226,6 +226,41 @@ int launch_partition_blocks(const JobDesc *d_jobs, int njobs, uint32_t total_dbl
 // tombstones are dropped. A broken job is marked (JobResultDev.spec) and
 // recomputed through the merge path by the batch's phase 1.
 // --------------------------------------------------------------------------
+// UniqueSplit.below / .above of the boundary after A[0, i) and B[0, jb).
+template <int KIND>
+__device__ __forceinline__ void split_bounds(const JobDesc &j, uint32_t i, uint32_t jb, UniqueSplit &s) {
+    constexpr int KL = KeyLimbs<KIND>::value;
+    const uint32_t vs = j.value_size, ts = j.timestamp_offset;
+    auto key_at = [&](const Stream &st, uint32_t idx) {
+        return load_key<KIND>(elem_ptr(st, seg_search(st, idx), idx, vs), ts);
+    };
+    Key<KL> lo, hi;
+    bool have_lo = false, have_hi = false;
+    if (i > 0) {
+        lo = key_at(j.a, i - 1);
+        have_lo = true;
+    }
+    if (jb > 0) {
+        const Key<KL> k = key_at(j.b, jb - 1);
+        if (!have_lo || key_lt(k, lo)) lo = k;
+        have_lo = true;
+    }
+    if (i < j.a.n) {
+        hi = key_at(j.a, i);
+        have_hi = true;
+    }
+    if (jb < j.b.n) {
+        const Key<KL> k = key_at(j.b, jb);
+        if (!have_hi || key_lt(hi, k)) hi = k;
+        have_hi = true;
+    }
+#pragma unroll
+    for (int l = 0; l < 3; l++) {
+        s.below[l] = l < KL && have_lo ? lo.l[l] : 0ull;
+        s.above[l] = l < KL ? (have_hi ? hi.l[l] : ~0ull) : 0ull;
+    }
+}
+
 template <bool Wave>
 __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, int njobs, uint32_t nsplits,
                                                           UniqueSplit *usplits, JobResultDev *res) {
@@ -257,6 +292,12 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
     s.b_ptr = nb ? gld<uint64_t>(j.b.seg_ptr + s.seg_b) : 0;
     s.b_lo = nb ? gld<uint32_t>(j.b.seg_pre + s.seg_b) : 0;
     s.b_hi = nb ? gld<uint32_t>(j.b.seg_pre + s.seg_b + 1) : 0;
+    switch (j.key_kind) {
+    case kKeyTimestamp: split_bounds<kKeyTimestamp>(j, lo, jb, s); break;
+    case kKeyIdU128: split_bounds<kKeyIdU128>(j, lo, jb, s); break;
+    case kKeyCompositeU64: split_bounds<kKeyCompositeU64>(j, lo, jb, s); break;
+    default: split_bounds<kKeyCompositeU128>(j, lo, jb, s); break;
+    }
     usplits[g] = s;
     if (t == 0) { // speculative results (write_blocks' shape for n values, compaction.zig:806-850)
         JobResultDev &r = res[j.job_index];
@@ -268,14 +309,43 @@ __global__ __launch_bounds__(256) void k_partition_unique(const JobDesc *jobs, i
     }
 }
 
-// LDS of a k_merge_unique workgroup: the tile's broken flag, then the MOST
-// SIGNIFICANT 64 bits of every entry's key (entries [0, na + 1) = A[ia0 - 1
-// .. ia1), [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1]): 16.4 KiB for 2,048
-// positions whatever the key width, so a workgroup fits beside an AEGIS chain
-// workgroup's T-tables on one CU. Keys equal in those bits are compared in
-// full from the values (global, L2-hot: the tile has just read them).
+// LDS of a k_merge_unique workgroup: the tile's broken flag, then a 32-bit
+// window of every entry's key (entries [0, na + 1) = A[ia0 - 1 .. ia1),
+// [na + 1, na + nb + 3) = B[jb0 - 1 .. jb1]): the key's 32 bits right below
+// the leading bits every key of the tile shares (UniqueSplit.below/.above),
+// so keys compare by their windows and, when those are equal, in full from
+// the values (global, L2-hot: the tile has just read them). 8.2 KiB for
+// 2,048 positions whatever the key width (round 5 kept the top 64 bits:
+// 16.4 KiB), so TWO workgroups fit beside an AEGIS chain workgroup's 136 KiB
+// of a CU's 160.
 constexpr uint32_t kUniqueRow = kUniqueTile + 3;
-static inline uint32_t unique_lds_bytes() { return 16 + kUniqueRow * 8; }
+static inline uint32_t unique_lds_bytes() { return 16 + kUniqueRow * 4; }
+
+// Leading bits common to the keys `lo` <= `hi` (most significant limb last).
+template <int KL> __device__ __forceinline__ uint32_t common_prefix(const uint64_t *lo, const uint64_t *hi) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int l = KL - 1; l >= 0; l--) {
+        const uint64_t x = lo[l] ^ hi[l];
+        if (x) return p + (uint32_t)__builtin_clzll(x);
+        p += 64;
+    }
+    return p;
+}
+
+// Bits [p, p + 32) of the key counted from its most significant bit (zeros
+// past its least significant one). For keys sharing their first p bits the
+// windows order as the keys do, up to ties.
+template <int KL> __device__ __forceinline__ uint32_t key_window(const Key<KL> &k, uint32_t p) {
+    const uint32_t t = p >> 6, sh = p & 63;
+    uint64_t top = 0;
+#pragma unroll
+    for (int l = 0; l < KL; l++) {
+        if ((uint32_t)(KL - 1 - l) == t) top |= k.l[l] << sh;
+        if (sh && (uint32_t)(KL - 2 - l) == t) top |= k.l[l] >> (64 - sh);
+    }
+    return (uint32_t)(top >> 32);
+}
 
 // Element idx of a stream whose split resolved segment [lo, hi) at ptr: in
 // that segment, or (a tile crossing an input block boundary) found by walking
@@ -319,7 +389,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     constexpr uint32_t T = kUniqueTile, NT = kUniqueThreads, E = T / NT;
     static_assert(T == E * NT, "whole elements per thread");
     uint32_t &s_bad = *(uint32_t *)lds;
-    uint64_t *s_hi = (uint64_t *)(lds + 16);
+    uint32_t *s_win = (uint32_t *)(lds + 16);
     const uint32_t tid = threadIdx.x;
     const uint32_t na_all = j.a.n, nb_all = j.b.n, n = na_all + nb_all;
     const uint32_t d0 = t * T, d1 = d0 + T < n ? d0 + T : n;
@@ -369,29 +439,33 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
         }
     }
+    // The leading bits every key the tile compares shares (uniform: from
+    // the tile's two boundaries, scalar loads).
+    const uint32_t pre = common_prefix<KL>(s0.below, usplits[j.usplit_base + t + 1].above);
+    uint32_t win[E];
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
-        if (e < m) s_hi[e < na ? 1 + e : e + 2] = key_of(q).l[KL - 1];
+        win[q] = e < m ? key_window(key_of(q), pre) : 0u;
+        if (e < m) s_win[e < na ? 1 + e : e + 2] = win[q];
     }
-    // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (absent: all ones,
-    // never compared in full).
+    // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (absent: never compared).
     if (tid < 3) {
         const bool bside = tid != 0;
         const Stream &st = bside ? j.b : j.a;
         const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
         const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
-        uint64_t hi = ~0ull;
-        if (bi >= 0 && bi < (int64_t)st.n) hi = load_key<KIND>(bside ? elem_b((uint32_t)bi) : elem_a((uint32_t)bi), ts).l[KL - 1];
-        s_hi[e] = hi;
+        uint32_t w = ~0u;
+        if (bi >= 0 && bi < (int64_t)st.n)
+            w = key_window(load_key<KIND>(bside ? elem_b((uint32_t)bi) : elem_a((uint32_t)bi), ts), pre);
+        s_win[e] = w;
     }
     __syncthreads();
-    // Order of entry e against key k: -1 below, 0 equal, 1 above; the most
-    // significant limb from LDS, the rest (rarely) in full.
-    auto cmp = [&](uint32_t e, const Key<KL> &k) -> int {
-        const uint64_t h = s_hi[e];
-        if (h != k.l[KL - 1]) return h < k.l[KL - 1] ? -1 : 1;
-        if constexpr (KL == 1) return 0;
+    // Order of entry e against key k (window wk): -1 below, 0 equal, 1
+    // above; by the windows, and (rarely) in full when they are equal.
+    auto cmp = [&](uint32_t e, const Key<KL> &k, uint32_t wk) -> int {
+        const uint32_t h = s_win[e];
+        if (h != wk) return h < wk ? -1 : 1;
         const Key<KL> f = full_key(e);
         return key_lt(f, k) ? -1 : (key_eq(f, k) ? 0 : 1);
     };
@@ -402,20 +476,21 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         const uint32_t e = tid + q * NT;
         if (e >= m) continue;
         const Key<KL> k = key_of(q);
+        const uint32_t wk = win[q];
         uint32_t pos;
         if (e < na) {
             // |{B in the tile < k}|: lower bound over entries [eb + 1, eb + 1 + nb).
             uint32_t lo = 0, hi = nb;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (cmp(eb + 1 + mid, k) < 0) lo = mid + 1;
+                if (cmp(eb + 1 + mid, k, wk) < 0) lo = mid + 1;
                 else hi = mid;
             }
             pos = e + lo;
             // The B at the lower bound (inside the tile, or the first after it).
             const bool b_there = lo < nb || jb1 < nb_all;
-            bad |= b_there && cmp(eb + 1 + lo, k) == 0;
-            bad |= (ia0 + e > 0) && cmp(e, k) == 0;
+            bad |= b_there && cmp(eb + 1 + lo, k, wk) == 0;
+            bad |= (ia0 + e > 0) && cmp(e, k, wk) == 0;
             bad |= drop && (in_regs ? (word_of(v0[q], v1[q], ts) >> 63) != 0 : load_tomb(src[q], ts) != 0);
         } else {
             const uint32_t b = e - na;
@@ -423,11 +498,11 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             uint32_t lo = 0, hi = na;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (cmp(1 + mid, k) <= 0) lo = mid + 1;
+                if (cmp(1 + mid, k, wk) <= 0) lo = mid + 1;
                 else hi = mid;
             }
             pos = b + lo;
-            bad |= (jb0 + b > 0) && cmp(eb + b, k) == 0;
+            bad |= (jb0 + b > 0) && cmp(eb + b, k, wk) == 0;
         }
         const uint32_t g = d0 + pos;
         const uint32_t kb = g / vcm;
@@ -457,29 +532,21 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     }
 }
 
-// `per_wg` consecutive tiles per workgroup (fewer, longer-lived workgroups).
+// One tile per workgroup, the tiles [first, first + gridDim.x) of one key
+// kind (a batch's jobs are grouped by kind, so each kind's tiles are
+// contiguous; a launch per kind keeps each kernel's registers its own).
 // Wide: the tiles of jobs whose values exceed 32 bytes (the other launch
-// takes the rest).
-template <bool Wide>
-__global__ __launch_bounds__(kUniqueThreads) void k_merge_unique(const JobDesc *jobs, int njobs, uint32_t total,
-                                                                 const UniqueSplit *usplits, JobResultDev *res,
-                                                                 uint32_t per_wg) {
+// takes the rest). At most 80 VGPRs (6 waves per SIMD): two workgroups fit
+// beside a chain workgroup (82 VGPRs, 2 waves per SIMD) on one CU.
+template <int KIND, bool Wide>
+__global__ __launch_bounds__(kUniqueThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_merge_unique(
+    const JobDesc *jobs, int njobs, uint32_t first, const UniqueSplit *usplits, JobResultDev *res) {
     extern __shared__ __attribute__((aligned(16))) uint8_t unique_lds[];
-    for (uint32_t i = 0; i < per_wg; i++) {
-        const uint32_t g = blockIdx.x * per_wg + i;
-        if (g >= total) return;
-        const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
-        const JobDesc &j = jobs[ji];
-        if (!j.unique || g - j.utile_base >= j.utile_count || (j.value_size > 32) != Wide) continue; // uniform
-        const uint32_t t = g - j.utile_base;
-        if (i) __syncthreads(); // the previous tile's LDS readers are done
-        switch (j.key_kind) {
-        case kKeyTimestamp: merge_unique_tile<kKeyTimestamp, Wide>(unique_lds, j, t, usplits, res); break;
-        case kKeyIdU128: merge_unique_tile<kKeyIdU128, Wide>(unique_lds, j, t, usplits, res); break;
-        case kKeyCompositeU64: merge_unique_tile<kKeyCompositeU64, Wide>(unique_lds, j, t, usplits, res); break;
-        default: merge_unique_tile<kKeyCompositeU128, Wide>(unique_lds, j, t, usplits, res); break;
-        }
-    }
+    const uint32_t g = first + blockIdx.x;
+    const int ji = find_job(jobs, njobs, g, [](const JobDesc &d) { return d.utile_base; });
+    const JobDesc &j = jobs[ji];
+    if (!j.unique || g - j.utile_base >= j.utile_count || (j.value_size > 32) != Wide) return; // uniform
+    merge_unique_tile<KIND, Wide>(unique_lds, j, g - j.utile_base, usplits, res);
 }
 
 int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs, SplitDesc *d_usplits,
@@ -512,18 +579,37 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
     if (!join()) return -1;
     if (mark) mark(mark_ctx, "partition_unique");
     (void)d_ticket;
-    const uint32_t pw = 1; // one tile per workgroup (2 and 4 measured slower)
-    bool narrow = false, wide = false;
-    for (int i = 0; i < njobs; i++)
-        if (h_jobs[i].unique) (h_jobs[i].value_size > 32 ? wide : narrow) = true;
-    if (narrow)
-        hipLaunchKernelGGL(k_merge_unique<false>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
-                           unique_lds_bytes(), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results,
-                           pw);
-    if (wide)
-        hipLaunchKernelGGL(k_merge_unique<true>, dim3((ntiles + pw - 1) / pw), dim3(kUniqueThreads),
-                           unique_lds_bytes(), s, d_jobs, njobs, ntiles, (const UniqueSplit *)d_usplits, d_results,
-                           pw);
+    // One launch per key kind and width (jobs are grouped by key kind).
+    for (int i = 0; i < njobs;) {
+        int k = i;
+        while (k + 1 < njobs && h_jobs[k + 1].key_kind == h_jobs[i].key_kind) k++;
+        const uint32_t t0 = h_jobs[i].utile_base, t1 = h_jobs[k].utile_base + h_jobs[k].utile_count;
+        bool narrow = false, wide = false;
+        for (int q = i; q <= k; q++)
+            if (h_jobs[q].unique) (h_jobs[q].value_size > 32 ? wide : narrow) = true;
+        for (int w = 0; w < 2 && t1 > t0; w++) {
+            if (!(w ? wide : narrow)) continue;
+            const dim3 grid(t1 - t0), block(kUniqueThreads);
+            const uint32_t lds = unique_lds_bytes();
+#define TBC_MU(K)                                                                                                      \
+    do {                                                                                                               \
+        if (w)                                                                                                         \
+            hipLaunchKernelGGL((k_merge_unique<K, true>), grid, block, lds, s, d_jobs, njobs, t0,                     \
+                               (const UniqueSplit *)d_usplits, d_results);                                             \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_merge_unique<K, false>), grid, block, lds, s, d_jobs, njobs, t0,                    \
+                               (const UniqueSplit *)d_usplits, d_results);                                             \
+    } while (0)
+            switch (h_jobs[i].key_kind) {
+            case kKeyTimestamp: TBC_MU(kKeyTimestamp); break;
+            case kKeyIdU128: TBC_MU(kKeyIdU128); break;
+            case kKeyCompositeU64: TBC_MU(kKeyCompositeU64); break;
+            default: TBC_MU(kKeyCompositeU128); break;
+            }
+#undef TBC_MU
+        }
+        i = k + 1;
+    }
     if (hipGetLastError() != hipSuccess) return -1;
     if (mark) mark(mark_ctx, "merge_unique");
     return 0;

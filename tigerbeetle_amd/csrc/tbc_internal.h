@@ -107,8 +107,14 @@ struct SplitDesc {
 
 // A k_merge_unique tile boundary: the merge-path split plus the input
 // segment each side's first element lies in, resolved (pointer and element
-// range), so a tile's loads start without walking the segment tables. Three
-// SplitDesc slots of the batch scratch per boundary.
+// range), so a tile's loads start without walking the segment tables; and
+// two keys around it: `below` = the smaller of A[i - 1], B[j - 1] that exist
+// (zero if neither) and `above` = the larger of A[i], B[j] that exist (all
+// ones if neither). Merge path orders everything before a boundary before
+// everything after it, so every key a tile compares (its own and its three
+// neighbour entries) lies in [below of its first boundary, above of its
+// last]: they share those two keys' leading bits (merge.hip k_merge_unique).
+// Six SplitDesc slots of the batch scratch.
 struct UniqueSplit {
     uint32_t i;            // A elements before the boundary
     uint32_t seg_a, seg_b; // segments of A[max(i-1, 0)] and B[max(d-i-1, 0)]
@@ -116,8 +122,9 @@ struct UniqueSplit {
     uint64_t a_ptr, b_ptr; // their first elements
     uint32_t a_lo, a_hi;   // element range [lo, hi) of segment seg_a
     uint32_t b_lo, b_hi;
+    uint64_t below[3], above[3]; // keys, least significant limb first
 };
-static_assert(sizeof(UniqueSplit) == 3 * sizeof(SplitDesc), "three split slots");
+static_assert(sizeof(UniqueSplit) == 6 * sizeof(SplitDesc), "six split slots");
 
 // One entry of the batch's tile order: tiles of the jobs of one key kind,
 // interleaved round-robin (job index into the batch's JobDesc array, tile).
