@@ -553,7 +553,7 @@ def main() -> None:
     ap.add_argument("--depth", type=int, default=3,
                     help="steps in flight: step k+D-1 is enqueued before step k is waited for, and the outputs "
                          "rotate over D sets (a replica's consecutive half-bars write freshly acquired blocks)")
-    ap.add_argument("--pipeline", choices=["auto", "on", "off"], default="auto",
+    ap.add_argument("--pipeline", choices=["auto", "on", "off"], default="on",
                     help="UNIQUE_KEYS batches: the engine's choice (auto), always pipelined, or always fused")
     args = ap.parse_args()
     njobs = args.jobs or configs.DEFAULT_JOBS.get(args.config, 1)
