@@ -1867,7 +1867,8 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     // unique-tile splits (pipelined speculated batches)
     const uint64_t sz_splits =
         align_up(sizeof(SplitDesc) * ((uint64_t)splits + (any_unique ? dblocks : 0)) + sizeof(UniqueSplit) * usplits,
-                 256);
+                 256) +
+        align_up(sizeof(SplitSeg) * (uint64_t)splits, 256);
     // tile status + block_tile + per-block assembled-value counts (throughput regime)
     // tile status, block tiles, per-block landed counts, the assembling
     // merge's look-back words (one per tile) and its ticket counters
@@ -1885,6 +1886,7 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
     SplitDesc *d_splits = (SplitDesc *)(dbase + sz_in);
     SplitDesc *d_bsplits = any_unique ? d_splits + splits : nullptr;
     SplitDesc *d_usplits = usplits ? d_splits + splits + dblocks : nullptr;
+    SplitSeg *d_ssegs = (SplitSeg *)(dbase + sz_in + sz_splits - align_up(sizeof(SplitSeg) * (uint64_t)splits, 256));
     uint64_t *d_status = (uint64_t *)(dbase + sz_in + sz_splits);
     uint32_t *d_block_tile = (uint32_t *)(d_status + tiles);
     uint32_t *d_ready = d_block_tile + dblocks;
@@ -1931,7 +1933,10 @@ static tbc_status submit_impl(tbc_engine *e, const tbc_compaction *jobs_in, uint
         memcpy(haddr + ap, c.addresses, 8ull * c.address_count);
         ap += c.address_count;
     }
-    for (uint32_t k = 0; k < count; k++) sj[k].spec_any = d_ticket + 4;
+    for (uint32_t k = 0; k < count; k++) {
+        sj[k].spec_any = d_ticket + 4;
+        sj[k].split_segs = d_ssegs + sj[k].split_base;
+    }
     memcpy(h_in, sj.data(), sizeof(JobDesc) * count);
     InputCheck *hchecks = (InputCheck *)(h_in + sz_jobs + sz_segs + sz_addr + sz_order);
     InputCheck *d_checks = (InputCheck *)(d_in + sz_jobs + sz_segs + sz_addr + sz_order);

@@ -158,6 +158,16 @@ __global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int 
     s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
     s.pad = 0;
     splits[gsplit] = s;
+    // The segments the tile starting here reads, resolved (k_merge_tile).
+    SplitSeg g;
+    auto fill = [](const Stream &st, uint32_t seg, uint64_t *ptr, uint32_t *pre) {
+        for (uint32_t k = 0; k < 2; k++) ptr[k] = seg + k < st.nseg ? gld<uint64_t>(st.seg_ptr + seg + k) : 0;
+        for (uint32_t k = 0; k < 3; k++)
+            pre[k] = st.nseg && seg + k <= st.nseg ? gld<uint32_t>(st.seg_pre + seg + k) : 0xffffffffu;
+    };
+    fill(j.a, s.seg_a, g.a_ptr, g.a_pre);
+    fill(j.b, s.seg_b, g.b_ptr, g.b_pre);
+    j.split_segs[t] = g;
 }
 
 // Speculated jobs (TBC_COMPACTION_UNIQUE_KEYS): with every value surviving,
@@ -623,14 +633,11 @@ int launch_merge_unique(const JobDesc *d_jobs, const JobDesc *h_jobs, int njobs,
 // output offsets, and the producer waves of k_data_blocks walk the masks to
 // assemble each output block's body.
 // --------------------------------------------------------------------------
-constexpr uint32_t kSegWindow = 16;
 constexpr uint32_t kMaskWords = kMergeTile / 64; // per mask kind per tile
 
 template <int KL> struct TileShared {
     uint64_t key[KL][kMergeTile + 3]; // A[i0-1 .. i1] then B[j0 .. j1]
     uint8_t tomb[kMergeTile + 4];
-    uint32_t seg_pre[2][kSegWindow + 1];
-    uint64_t seg_ptr[2][kSegWindow];
     uint32_t wave_sums[kMergeThreads / 64];
 };
 
@@ -657,15 +664,9 @@ __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *o
     const bool secondary = j.usage == 1;
     const bool drop = j.drop_tombstones != 0;
 
-    // Segment windows (the few input data blocks this tile touches).
-    if (tid < 2 * (kSegWindow + 1)) {
-        const uint32_t side = tid / (kSegWindow + 1), k = tid % (kSegWindow + 1);
-        const Stream &s = side == 0 ? j.a : j.b;
-        const uint32_t seg = (side == 0 ? s0.seg_a : s0.seg_b) + k;
-        sh.seg_pre[side][k] = seg <= s.nseg && s.nseg ? gld<uint32_t>(s.seg_pre + seg) : 0xffffffffu;
-        if (k < kSegWindow) sh.seg_ptr[side][k] = seg < s.nseg ? gld<uint64_t>(s.seg_ptr + seg) : 0;
-    }
-    __syncthreads();
+    // The segments around the tile, resolved by the partition (no segment
+    // table round trip and no barrier before the key loads).
+    const SplitSeg sg = j.split_segs[t];
 
     // Load keys: entries [0, ea) = A[i0-1 .. i1], entries [ea, ea+eb) = B[j0 .. j1].
     const uint32_t ea = na + 2, eb = nb + 1;
@@ -677,18 +678,15 @@ __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *o
         const uint8_t *p = nullptr;
         if (e < ea + eb) {
             const bool is_a = e < ea;
-            const uint32_t side = is_a ? 0 : 1;
             const Stream &s = is_a ? j.a : j.b;
             const int64_t idx = is_a ? (int64_t)i0 - 1 + e : (int64_t)j0 + (e - ea);
             if (idx >= 0 && idx < (int64_t)s.n) {
-                uint32_t k = 0;
-                while (k + 1 < kSegWindow && sh.seg_pre[side][k + 1] <= (uint32_t)idx) k++;
-                if (k + 1 == kSegWindow && sh.seg_pre[side][k + 1] <= (uint32_t)idx) {
-                    const uint32_t seg = seg_search(s, (uint32_t)idx); // tiny segments: global fallback
-                    p = elem_ptr(s, seg, (uint32_t)idx, vs);
-                } else {
-                    p = (const uint8_t *)sh.seg_ptr[side][k] + (size_t)((uint32_t)idx - sh.seg_pre[side][k]) * vs;
-                }
+                const uint32_t x = (uint32_t)idx;
+                const uint64_t *ptr = is_a ? sg.a_ptr : sg.b_ptr;
+                const uint32_t *pre = is_a ? sg.a_pre : sg.b_pre;
+                if (x < pre[1]) p = (const uint8_t *)ptr[0] + (size_t)(x - pre[0]) * vs;
+                else if (x < pre[2]) p = (const uint8_t *)ptr[1] + (size_t)(x - pre[1]) * vs;
+                else p = elem_ptr(s, seg_search(s, x), x, vs); // blocks under 2,051 values: the table
             }
         }
         ptrs[r] = p;
@@ -904,8 +902,13 @@ static int launch_kind(uint32_t phase, const JobDesc *d_jobs, const JobDesc *h_j
     bool any = false;
     for (int k = first; k < first + count; k++) any |= phase == 0 ? !h_jobs[k].unique : h_jobs[k].unique != 0;
     if (!any) return 0;
+    // The recomputation leaves at once while no speculation broke, but every
+    // workgroup needs a CU with room for its tile's LDS first: beside the
+    // chain workgroups of earlier batches few CUs have it, so a grid of 1,024
+    // waited up to 0.3 ms for slots (config 2, round 6 trace); 64 workgroups
+    // striding over the tiles when a speculation did break.
     if (ntiles && phase)
-        hipLaunchKernelGGL((k_merge_tile_redo<KIND>), dim3(std::min<uint32_t>(ntiles, 1024)), dim3(kMergeThreads), 0,
+        hipLaunchKernelGGL((k_merge_tile_redo<KIND>), dim3(std::min<uint32_t>(ntiles, 64)), dim3(kMergeThreads), 0,
                            s, d_jobs, d_order, tile_off, (const SplitDesc *)d_splits, d_status, d_masks, d_res, ntiles);
     else if (ntiles)
         hipLaunchKernelGGL((k_merge_tile<KIND>), dim3(ntiles), dim3(kMergeThreads), 0, s, d_jobs, d_order, tile_off,

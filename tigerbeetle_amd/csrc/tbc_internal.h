@@ -89,6 +89,20 @@ struct JobDesc {
     uint64_t out_offset;
     uint32_t block_lo, table_lo;
     uint32_t seal, pad2;
+    // Mask-merge tiles (merge.hip k_merge_tile): the input segments around
+    // each tile boundary, resolved by the partition (tile_count + 1 of them).
+    struct SplitSeg *split_segs;
+};
+
+// The input segments a mask-merge tile reads, resolved by the partition at
+// its first boundary: for each side, the segment holding its first entry
+// (A[i - 1], or A[0]; B[j], or B's last) and the next one — pointers and
+// prefix counts (pre[2] = the end of the second) — so a tile computes its
+// entries' addresses without a segment-table round trip (entries past the
+// second segment, only with blocks under 2,051 values, search the table).
+struct SplitSeg {
+    uint64_t a_ptr[2], b_ptr[2];
+    uint32_t a_pre[3], b_pre[3];
 };
 
 // Merged positions per tile of k_merge_unique (four per thread): the most
