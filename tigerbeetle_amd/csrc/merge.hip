@@ -691,21 +691,26 @@ __device__ __forceinline__ void merge_tile(const JobDesc *jobs, const TileRef *o
         }
         ptrs[r] = p;
     }
+    // Every entry's loads are issued before any is waited for: loads behind
+    // a branch each ended in their own wait (one HBM round trip per entry,
+    // kPerLoad in sequence); an absent entry reads a value the tile has.
+    // (a stand-in: the first value of a side the tile reads, one exists)
+    const uint8_t *any = (const uint8_t *)(sg.a_ptr[0] ? sg.a_ptr[0] : sg.b_ptr[0]);
+    Key<KL> kr[kPerLoad];
+    uint32_t tr[kPerLoad];
+#pragma unroll
+    for (uint32_t r = 0; r < kPerLoad; r++) {
+        const uint8_t *p = ptrs[r] ? ptrs[r] : any;
+        kr[r] = load_key<KIND>(p, ts);
+        tr[r] = load_tomb(p, ts);
+    }
 #pragma unroll
     for (uint32_t r = 0; r < kPerLoad; r++) {
         const uint32_t e = tid + r * kMergeThreads;
         if (e >= ea + eb) continue;
-        Key<KL> k;
 #pragma unroll
-        for (int l = 0; l < KL; l++) k.l[l] = ~0ull;
-        uint32_t tb = 0;
-        if (ptrs[r]) {
-            k = load_key<KIND>(ptrs[r], ts);
-            if (e < ea) tb = load_tomb(ptrs[r], ts);
-        }
-#pragma unroll
-        for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
-        if (e < ea) sh.tomb[e] = (uint8_t)tb;
+        for (int l = 0; l < KL; l++) sh.key[l][e] = ptrs[r] ? kr[r].l[l] : ~0ull;
+        if (e < ea) sh.tomb[e] = ptrs[r] ? (uint8_t)tr[r] : (uint8_t)0;
     }
     __syncthreads();
 
