@@ -739,6 +739,15 @@ __device__ __forceinline__ bool key_before(const uint64_t a[3], uint32_t ia, con
     return ia < ib;
 }
 
+// One value of C 16-byte chunks: every load issued before the first store.
+template <uint32_t C> __device__ __forceinline__ void copy_value(uint8_t *dst, const uint8_t *src) {
+    u32x4 v[C];
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++) v[c] = gld<u32x4>(src + 16 * c);
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++) gst<u32x4>(dst + 16 * c, v[c]);
+}
+
 __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32_t *tile_seg, const uint64_t *words0,
                                                      const uint64_t *words1) {
     const uint32_t tile = blockIdx.x / (kSortTile / kFinishItems);
@@ -750,8 +759,21 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
         if (!S.oop || first >= n) return;
         const uint32_t last = first + kFinishItems < n ? first + kFinishItems : n;
         const uint32_t chunks = (last - first) * (vs >> 4);
-        for (uint32_t c = tid; c < chunks; c += 256)
-            gst<u32x4>(S.values + (size_t)first * vs + 16 * c, gld<u32x4>(S.copy + (size_t)first * vs + 16 * c));
+        const uint8_t *src = S.copy + (size_t)first * vs;
+        uint8_t *dst = S.values + (size_t)first * vs;
+        for (uint32_t c0 = 0; c0 < chunks; c0 += 8 * 256) { // eight loads in flight per lane, then their stores
+            u32x4 v[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t c = c0 + q * 256 + tid;
+                v[q] = gld<u32x4>(src + 16 * (size_t)(c < chunks ? c : chunks - 1));
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t c = c0 + q * 256 + tid;
+                if (c < chunks) gst<u32x4>(dst + 16 * (size_t)c, v[q]);
+            }
+        }
         return;
     }
     const uint64_t *wv = (S.final_buf ? words1 : words0) + S.item_base; // the table's sorted words
@@ -763,12 +785,18 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
         const uint32_t jl = tid / cpv, part = tid % cpv;
         if (jl >= vpr) return;
         for (uint32_t j0 = first; j0 < last; j0 += 8 * vpr) {
-            u32x4 v[8];
+            // Loads issued unconditionally (indices clamped into the range),
+            // so that all eight words, then all eight values, are in flight
+            // together: loads behind a branch each ended in their own wait.
+            uint32_t from[8];
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++) {
                 const uint32_t j = j0 + q * vpr + jl;
-                if (j < last) v[q] = gld<u32x4>(S.copy + (size_t)(uint32_t)(wv[j] & imask) * vs + 16 * part);
+                from[q] = (uint32_t)(wv[j < last ? j : last - 1] & imask);
             }
+            u32x4 v[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) v[q] = gld<u32x4>(S.copy + (size_t)from[q] * vs + 16 * part);
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++) {
                 const uint32_t j = j0 + q * vpr + jl;
@@ -779,7 +807,25 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
     }
     const uint32_t sh = S.ib + 8 * S.top;
     for (uint32_t i = first + tid; i < last; i += 256) {
+        // The word and both neighbours at once: most runs of equal top
+        // digits are one item long (the plan predicted so), and such an item
+        // is copied straight to its place, every chunk's load before a store.
         const uint64_t wi = wv[i], ti = wi >> sh;
+        const uint64_t wp = wv[i > 0 ? i - 1 : i], wn = wv[i + 1 < n ? i + 1 : i];
+        if ((i == 0 || (wp >> sh) != ti) && (i + 1 >= n || (wn >> sh) != ti)) {
+            const uint8_t *src = S.copy + (size_t)(uint32_t)(wi & imask) * vs;
+            uint8_t *dst = S.values + (size_t)i * vs;
+            switch (vs >> 4) { // uniform
+            case 1: copy_value<1>(dst, src); break;
+            case 2: copy_value<2>(dst, src); break;
+            case 4: copy_value<4>(dst, src); break;
+            case 8: copy_value<8>(dst, src); break;
+            default: // 256 bytes and up (powers of two)
+                for (uint32_t b = 0; b < vs; b += 256) copy_value<16>(dst + b, src + b);
+                break;
+            }
+            continue;
+        }
         // run bounds [lo, hi) of equal top digits around i
         uint32_t lo = i, hi = i + 1;
         while (lo > 0 && (wv[lo - 1] >> sh) == ti && i - lo < kRunMax) lo--;
