@@ -1753,10 +1753,21 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
             const uint32_t nblk = (obase + S - 1) / vcm - kfirst + 1;
             if (fast && tid < nblk)
                 s_blk[tid] = (uint64_t)(uintptr_t)(block_ptr(j, data_block_slot(kfirst + tid, j.dbcm)) + kHeaderSize);
-            // Stage: wave wv takes words w0 + wv + 4i.
-            for (uint32_t w = w0 + wv; w < w0 + W / 2; w += 4) {
+            // Stage: wave wv takes words w0 + wv + 4i, all of its mask words
+            // loaded at once (one round trip, not one per word).
+            constexpr uint32_t kWaveWords = W / 2 / 4;
+            uint64_t smv[kWaveWords], amv[kWaveWords];
+#pragma unroll
+            for (uint32_t i = 0; i < kWaveWords; i++) {
+                const uint32_t w = w0 + wv + 4 * i;
+                smv[i] = gld<uint64_t>(m + w);
+                amv[i] = gld<uint64_t>(m + W + w);
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kWaveWords; i++) {
+                const uint32_t w = w0 + wv + 4 * i;
                 if (t * kMergeTile + 64 * w >= n) break;
-                const uint64_t sm = gld<uint64_t>(m + w), am = gld<uint64_t>(m + W + w);
+                const uint64_t sm = smv[i], am = amv[i];
                 if (sm == 0) continue;
                 const uint64_t valid = valid_of(w);
                 const uint32_t ab = a0 + s_pre[1][w], bb = b0 + s_pre[2][w];

@@ -175,29 +175,41 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     __syncthreads();
     uint64_t o[kMaxLimbs] = {0, 0, 0}, a[kMaxLimbs] = {~0ull, ~0ull, ~0ull};
     uint32_t uns = 0;
-    for (uint32_t r = 0; r < kSortRounds; r++) {
+    // Out of place, the caller's input is the gather's source: keys only,
+    // the next row's loaded while a row is folded in (as k_sort_pack).
+    const uint32_t left = n - lt * kSortTile; // > 0: the tile is in the table
+    const uint32_t rows = left >= kSortTile ? kSortRounds : (left + kSortThreads - 1) / kSortThreads;
+    if (S.oop) {
+        uint64_t k[3], kx[3];
+        row_load(S, lt * kSortTile + tid, k, kx);
+        for (uint32_t r = 0; r < rows; r++) {
+            const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
+            uint64_t k2[3] = {0, 0, 0}, kx2[3] = {0, 0, 0}, kn[3];
+            if (r + 1 < rows) row_load(S, li + kSortThreads, k2, kx2);
+            row_next(li, n, k, kx, kn);
+            if (li < n) {
+                for (uint32_t l = 0; l < kl; l++) {
+                    o[l] |= k[l];
+                    a[l] &= k[l];
+                }
+                if (li + 1 < n) {
+                    int cmp = 0;
+                    for (uint32_t l = 0; l < kl; l++)
+                        if (k[l] != kn[l]) cmp = k[l] > kn[l] ? 1 : -1;
+                    uns |= cmp > 0 ? 1u : 0u;
+                }
+            }
+            for (uint32_t l = 0; l < 3; l++) {
+                k[l] = k2[l];
+                kx[l] = kx2[l];
+            }
+        }
+    }
+    for (uint32_t r = 0; !S.oop && r < rows; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-        if (lt * kSortTile + r * kSortThreads >= n) break; // wave-uniform (whole row past the end)
         const bool in = li < n;
         // The row's first 128 bytes of every value are loaded with its keys
-        // (one round trip), then stored; longer values loop. Out of place,
-        // the caller's input is the gather's source: keys only.
-        if (S.oop) {
-            uint64_t k[3], kn[3];
-            row_keys(S, li, k, kn);
-            if (!in) continue;
-            for (uint32_t l = 0; l < kl; l++) {
-                o[l] |= k[l];
-                a[l] &= k[l];
-            }
-            if (li + 1 < n) {
-                int cmp = 0;
-                for (uint32_t l = 0; l < kl; l++)
-                    if (k[l] != kn[l]) cmp = k[l] > kn[l] ? 1 : -1;
-                uns |= cmp > 0 ? 1u : 0u;
-            }
-            continue;
-        }
+        // (one round trip), then stored; longer values loop.
         u32x4 v[8];
         if (in) {
 #pragma unroll
