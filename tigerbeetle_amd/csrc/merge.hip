@@ -150,21 +150,48 @@ __global__ __launch_bounds__(256) void k_partition_all(const JobDesc *jobs, int 
     case kKeyCompositeU64: lo = split_at<kKeyCompositeU64, Wave>(j, d); break;
     default: lo = split_at<kKeyCompositeU128, Wave>(j, d); break;
     }
-    if (Wave && (threadIdx.x & 63) != 0) return;
+    // The segments the tile starting here reads, resolved for k_merge_tile:
+    // two value pointers and three prefix counts per side, their loads
+    // issued together (clamped into the tables, then masked).
+    auto fill = [](const Stream &st, uint32_t seg, uint64_t *ptr, uint32_t *pre) {
+        const uint32_t ns = st.nseg;
+        if (!ns) {
+            ptr[0] = ptr[1] = 0;
+            pre[0] = pre[1] = pre[2] = 0xffffffffu;
+            return;
+        }
+        uint64_t p[2];
+        uint32_t q[3];
+        for (uint32_t k = 0; k < 2; k++) p[k] = gld<uint64_t>(st.seg_ptr + (seg + k < ns ? seg + k : ns - 1));
+        for (uint32_t k = 0; k < 3; k++) q[k] = gld<uint32_t>(st.seg_pre + (seg + k <= ns ? seg + k : ns));
+        for (uint32_t k = 0; k < 2; k++) ptr[k] = seg + k < ns ? p[k] : 0;
+        for (uint32_t k = 0; k < 3; k++) pre[k] = seg + k <= ns ? q[k] : 0xffffffffu;
+    };
+    const uint32_t jb = d - lo;
+    if constexpr (Wave) { // lane 0 resolves side A, lane 1 side B, at once
+        const uint32_t lane = threadIdx.x & 63;
+        if (lane > 1) return;
+        const bool bside = lane == 1;
+        const Stream &st = bside ? j.b : j.a;
+        const uint32_t cnt = bside ? nb : na, idx = bside ? (jb < nb ? jb : nb - 1) : (lo > 0 ? lo - 1 : 0);
+        const uint32_t seg = cnt ? seg_search(st, idx) : 0;
+        uint64_t ptr[2];
+        uint32_t pre[3];
+        fill(st, seg, ptr, pre);
+        SplitSeg &g = j.split_segs[t];
+        for (uint32_t k = 0; k < 2; k++) (bside ? g.b_ptr : g.a_ptr)[k] = ptr[k];
+        for (uint32_t k = 0; k < 3; k++) (bside ? g.b_pre : g.a_pre)[k] = pre[k];
+        const uint32_t seg_b = (uint32_t)__shfl((int)seg, 1, 64);
+        if (!bside) splits[gsplit] = SplitDesc{lo, seg, seg_b, 0};
+        return;
+    }
     SplitDesc s;
     s.i = lo;
     s.seg_a = na ? seg_search(j.a, lo > 0 ? lo - 1 : 0) : 0;
-    const uint32_t jb = d - lo;
     s.seg_b = nb ? seg_search(j.b, jb < nb ? jb : nb - 1) : 0;
     s.pad = 0;
     splits[gsplit] = s;
-    // The segments the tile starting here reads, resolved (k_merge_tile).
     SplitSeg g;
-    auto fill = [](const Stream &st, uint32_t seg, uint64_t *ptr, uint32_t *pre) {
-        for (uint32_t k = 0; k < 2; k++) ptr[k] = seg + k < st.nseg ? gld<uint64_t>(st.seg_ptr + seg + k) : 0;
-        for (uint32_t k = 0; k < 3; k++)
-            pre[k] = st.nseg && seg + k <= st.nseg ? gld<uint32_t>(st.seg_pre + seg + k) : 0xffffffffu;
-    };
     fill(j.a, s.seg_a, g.a_ptr, g.a_pre);
     fill(j.b, s.seg_b, g.b_ptr, g.b_pre);
     j.split_segs[t] = g;
@@ -438,13 +465,20 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
         }
         return k;
     };
+    // Every element's pointer first (a tile crossing an input block walks
+    // the segment table), then every value load: a load whose address waits
+    // on a pointer load waited on all loads before it too, so loads issued
+    // element by element went out one round trip at a time.
 #pragma unroll
     for (uint32_t q = 0; q < E; q++) {
         const uint32_t e = tid + q * NT;
         const bool is_a = e < na;
         src[q] = e < m ? (is_a ? elem_a(ia0 + e) : elem_b(jb0 + (e - na))) : nullptr;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
         v0[q] = v1[q] = u32x4{0, 0, 0, 0};
-        if (!Wide && e < m) {
+        if (!Wide && src[q]) {
             v0[q] = gld<u32x4>(src[q]);
             if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
         }
