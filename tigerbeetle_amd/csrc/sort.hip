@@ -109,14 +109,31 @@ struct SortBatch {
     uint32_t broken; // a pass hit a wait bound (a broken invariant): k_sort_rescue re-sorts every moved table
 };
 
+// key_from_value by kind (keys.h load_key), in two halves: key_raw issues
+// the loads (three words, unconditionally: every offset lies inside a value
+// of >= 16 bytes) and key_fix forms the limbs. Any use of a loaded word next
+// to its load -- a branch by kind that masked it, a select against a default
+// -- made the wave wait for that load right there, so a row "prefetched"
+// this way was not in flight while the previous row was packed.
+struct KeyRaw {
+    uint64_t w[3];
+};
+__device__ __forceinline__ KeyRaw key_raw(uint32_t kind, const uint8_t *v, uint32_t ts_off) {
+    const uint32_t o0 = kind == kKeyTimestamp ? ts_off : kind == kKeyIdU128 ? 0u : kind == kKeyCompositeU64 ? 8u : 16u;
+    const uint32_t o1 = kind == kKeyIdU128 ? 8u : 0u;
+    KeyRaw r;
+    r.w[0] = gld<uint64_t>(v + o0);
+    r.w[1] = gld<uint64_t>(v + o1);
+    r.w[2] = gld<uint64_t>(v + 8);
+    return r;
+}
+__device__ __forceinline__ void key_fix(uint32_t kind, const KeyRaw &r, uint64_t k[3]) {
+    k[0] = kind == kKeyIdU128 ? r.w[0] : r.w[0] & ~kTombstoneBit;
+    k[1] = kind == kKeyTimestamp ? 0ull : r.w[1];
+    k[2] = kind == kKeyCompositeU128 ? r.w[2] : 0ull;
+}
 __device__ __forceinline__ void key_of(uint32_t kind, const uint8_t *v, uint32_t ts_off, uint64_t k[3]) {
-    k[1] = k[2] = 0;
-    switch (kind) {
-    case kKeyTimestamp: k[0] = gld<uint64_t>(v + ts_off) & ~kTombstoneBit; break;
-    case kKeyIdU128: k[0] = gld<uint64_t>(v); k[1] = gld<uint64_t>(v + 8); break;
-    case kKeyCompositeU64: k[0] = gld<uint64_t>(v + 8) & ~kTombstoneBit; k[1] = gld<uint64_t>(v); break;
-    default: k[0] = gld<uint64_t>(v + 16) & ~kTombstoneBit; k[1] = gld<uint64_t>(v); k[2] = gld<uint64_t>(v + 8); break;
-    }
+    key_fix(kind, key_raw(kind, v, ts_off), k);
 }
 
 __host__ __device__ __forceinline__ uint64_t low_mask(uint32_t bits) { return bits >= 64 ? ~0ull : (1ull << bits) - 1; }
@@ -141,23 +158,39 @@ __device__ __forceinline__ uint32_t *seg_hist(uint32_t *hist, uint32_t s) { retu
 
 // The key and the next item's key (the next lane's; lane 63 loads its
 // neighbour, which may sit in the next tile) of every lane of a row.
-// Both loads are issued before either is used (one memory round trip per row):
-// row_load issues them, row_next forms the neighbours once they are in.
-__device__ __forceinline__ void row_load(const SortSeg &S, uint32_t li, uint64_t k[3], uint64_t kx[3]) {
-    k[0] = k[1] = k[2] = kx[0] = kx[1] = kx[2] = 0;
-    if (li < S.n) key_of(S.kind, S.src + (size_t)li * S.vs, S.ts_off, k);
-    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.src + (size_t)(li + 1) * S.vs, S.ts_off, kx);
+// row_issue issues both loads (indices clamped into the table: a lane past
+// the end re-reads the last item, and callers use only lanes inside it);
+// row_form makes the keys and the neighbours once they are in.
+struct RowRaw {
+    KeyRaw k, kx;
+};
+__device__ __forceinline__ RowRaw row_issue(const SortSeg &S, uint32_t li) {
+    const uint32_t n = S.n, i0 = li < n ? li : n - 1;
+    const uint32_t i1 = ((threadIdx.x & 63) == 63 && li + 1 < n) ? li + 1 : i0;
+    RowRaw r;
+    r.k = key_raw(S.kind, S.src + (size_t)i0 * S.vs, S.ts_off);
+    r.kx = key_raw(S.kind, S.src + (size_t)i1 * S.vs, S.ts_off);
+    return r;
 }
-__device__ __forceinline__ void row_next(uint32_t li, uint32_t n, const uint64_t k[3], const uint64_t kx[3],
+__device__ __forceinline__ void row_form(const SortSeg &S, uint32_t li, const RowRaw &r, uint64_t k[3],
                                          uint64_t kn[3]) {
+    uint64_t kx[3];
+    key_fix(S.kind, r.k, k);
+    key_fix(S.kind, r.kx, kx);
     for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
-    if ((threadIdx.x & 63) == 63 && li + 1 < n)
+    if ((threadIdx.x & 63) == 63 && li + 1 < S.n)
         for (uint32_t l = 0; l < 3; l++) kn[l] = kx[l];
 }
+// In place (extract's copying path): the keys of a row used at once, only
+// lane 63 loading its neighbour.
 __device__ __forceinline__ void row_keys(const SortSeg &S, uint32_t li, uint64_t k[3], uint64_t kn[3]) {
-    uint64_t kx[3];
-    row_load(S, li, k, kx);
-    row_next(li, S.n, k, kx, kn);
+    uint64_t kx[3] = {0, 0, 0};
+    k[0] = k[1] = k[2] = 0;
+    if (li < S.n) key_of(S.kind, S.src + (size_t)li * S.vs, S.ts_off, k);
+    if ((threadIdx.x & 63) == 63 && li + 1 < S.n) key_of(S.kind, S.src + (size_t)(li + 1) * S.vs, S.ts_off, kx);
+    for (uint32_t l = 0; l < 3; l++) kn[l] = __shfl_down(k[l], 1, 64);
+    if ((threadIdx.x & 63) == 63 && li + 1 < S.n)
+        for (uint32_t l = 0; l < 3; l++) kn[l] = kx[l];
 }
 
 // --------------------------------------------------------------------------
@@ -180,13 +213,12 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
     const uint32_t left = n - lt * kSortTile; // > 0: the tile is in the table
     const uint32_t rows = left >= kSortTile ? kSortRounds : (left + kSortThreads - 1) / kSortThreads;
     if (S.oop) {
-        uint64_t k[3], kx[3];
-        row_load(S, lt * kSortTile + tid, k, kx);
+        RowRaw cur = row_issue(S, lt * kSortTile + tid);
         for (uint32_t r = 0; r < rows; r++) {
             const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
-            uint64_t k2[3] = {0, 0, 0}, kx2[3] = {0, 0, 0}, kn[3];
-            if (r + 1 < rows) row_load(S, li + kSortThreads, k2, kx2);
-            row_next(li, n, k, kx, kn);
+            const RowRaw nxt = row_issue(S, r + 1 < rows ? li + kSortThreads : li); // the last row re-reads itself
+            uint64_t k[3], kn[3];
+            row_form(S, li, cur, k, kn);
             if (li < n) {
                 for (uint32_t l = 0; l < kl; l++) {
                     o[l] |= k[l];
@@ -199,10 +231,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_extract(SortSeg *segs, co
                     uns |= cmp > 0 ? 1u : 0u;
                 }
             }
-            for (uint32_t l = 0; l < 3; l++) {
-                k[l] = k2[l];
-                kx[l] = kx2[l];
-            }
+            cur = nxt;
         }
     }
     for (uint32_t r = 0; !S.oop && r < rows; r++) {
@@ -380,14 +409,13 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
     const uint32_t rows = left >= kSortTile ? kSortRounds : (left + kSortThreads - 1) / kSortThreads;
     // The next row's keys load while a row is packed (round 3, one box, with
     // S out of scratch: config 3's pack 119 -> 100 us; two rows ahead: 98).
-    uint64_t k[3], kx[3];
-    row_load(S, lt * kSortTile + tid, k, kx);
+    RowRaw cur = row_issue(S, lt * kSortTile + tid);
     for (uint32_t r = 0; r < rows; r++) {
         const uint32_t li = lt * kSortTile + r * kSortThreads + tid;
         const bool in = li < n;
-        uint64_t k2[3] = {0, 0, 0}, kx2[3] = {0, 0, 0}, kn[3];
-        if (r + 1 < rows) row_load(S, li + kSortThreads, k2, kx2);
-        row_next(li, n, k, kx, kn);
+        const RowRaw nxt = row_issue(S, r + 1 < rows ? li + kSortThreads : li); // the last row re-reads itself
+        uint64_t k[3], kn[3];
+        row_form(S, li, cur, k, kn);
         const uint64_t p = pack_bits(runs, nr, k);
         if (in) gst<uint64_t>(words + S.item_base + li, p << ib | li);
         for (uint32_t j = 0; j < nd; j++) hist_add(s_hist[j], (uint32_t)(p >> (8 * j)) & 255u, in);
@@ -398,10 +426,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pack(SortSeg *segs, const
                 if ((p & m) > (q & m)) viol |= 1u << j;
             }
         }
-        for (uint32_t l = 0; l < 3; l++) {
-            k[l] = k2[l];
-            kx[l] = kx2[l];
-        }
+        cur = nxt;
     }
     if (viol) atomicOr(&s_viol, viol);
     __syncthreads();
