@@ -117,11 +117,22 @@ __global__ __launch_bounds__(kPairThreads) void k_kpair_tile(const KPair *pairs,
     const uint32_t j0 = d0 - i0, j1 = d1 - i1;
     const uint32_t ea = i1 - i0, eb = j1 - j0;
     // LDS: A[i0 .. i1) at [0, ea), B[j0 .. j1) at [ea, ea + eb), the previous merged key at kPairTile + 1.
-    for (uint32_t e = tid; e < ea + eb; e += kPairThreads) {
-        const uint8_t *v = e < ea ? P.a + (size_t)(i0 + e) * vs : P.b + (size_t)(j0 + e - ea) * vs;
-        const auto k = load_key<KIND>(v, ts);
+    // Every entry's key loaded before any is stored (a load whose use sat in
+    // the same loop iteration was waited for there: kPairPer round trips in
+    // sequence); entries past the tile re-read its last one.
+    Key<KL> kr[kPairPer];
 #pragma unroll
-        for (int l = 0; l < KL; l++) sh.key[l][e] = k.l[l];
+    for (uint32_t r = 0; r < kPairPer; r++) {
+        const uint32_t e0 = tid + r * kPairThreads, e = e0 < ea + eb ? e0 : ea + eb - 1;
+        const uint8_t *v = e < ea ? P.a + (size_t)(i0 + e) * vs : P.b + (size_t)(j0 + e - ea) * vs;
+        kr[r] = load_key<KIND>(v, ts);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kPairPer; r++) {
+        const uint32_t e = tid + r * kPairThreads;
+        if (e < ea + eb)
+#pragma unroll
+            for (int l = 0; l < KL; l++) sh.key[l][e] = kr[r].l[l];
     }
     if (tid == 0) {
         // The merged predecessor of position d0 is the later of A[i0-1] and
@@ -297,8 +308,8 @@ __global__ __launch_bounds__(kPairThreads) void k_kpair_scatter(const KPair *pai
             u32x4 v[4];
 #pragma unroll
             for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t c = c0 + lane + 64 * u;
-                if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[wv][c / cpv] + 16 * (c % cpv));
+                const uint32_t c = c0 + lane + 64 * u < total ? c0 + lane + 64 * u : total - 1; // loads unconditional
+                v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[wv][c / cpv] + 16 * (c % cpv));
             }
 #pragma unroll
             for (uint32_t u = 0; u < 4; u++) {
