@@ -441,8 +441,14 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     const uint32_t reg_bytes = vs < 32 ? vs : 32u;
     const bool in_regs = !Wide && (KIND == kKeyTimestamp ? ts : (kMaxOff > ts ? kMaxOff : ts)) + 8 <= reg_bytes;
     if (tid == 0) s_bad = 0;
-    auto elem_a = [&](uint32_t i) { return unique_elem(j.a, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, i, vs); };
-    auto elem_b = [&](uint32_t i) { return unique_elem(j.b, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, i, vs); };
+    // The job's fields the stores below need, read once: the output stores
+    // could alias the descriptor, so every use after one re-read it.
+    const Stream sa = j.a, sb = j.b;
+    const uint32_t dbcm = j.dbcm, bsize = j.block_size;
+    uint8_t *const grid_base = j.grid_base, *const out_blocks = j.out_blocks;
+    const uint64_t *const addresses = j.addresses;
+    auto elem_a = [&](uint32_t i) { return unique_elem(sa, s0.seg_a, s0.a_ptr, s0.a_lo, s0.a_hi, i, vs); };
+    auto elem_b = [&](uint32_t i) { return unique_elem(sb, s0.seg_b, s0.b_ptr, s0.b_lo, s0.b_hi, i, vs); };
     // Entry e's full key (A entries 0..na, B entries eb..eb+nb+1), from the input.
     auto full_key = [&](uint32_t e) {
         const uint8_t *p = e < eb ? elem_a(ia0 - 1 + e) : elem_b(jb0 - 1 + (e - eb));
@@ -496,7 +502,7 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     // The boundary entries: A[ia0 - 1], B[jb0 - 1], B[jb1] (absent: never compared).
     if (tid < 3) {
         const bool bside = tid != 0;
-        const Stream &st = bside ? j.b : j.a;
+        const Stream &st = bside ? sb : sa;
         const int64_t bi = tid == 0 ? (int64_t)ia0 - 1 : tid == 1 ? (int64_t)jb0 - 1 : (int64_t)jb1;
         const uint32_t e = tid == 0 ? 0u : tid == 1 ? eb : eb + nb + 1;
         uint32_t w = ~0u;
@@ -549,8 +555,10 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             bad |= (jb0 + b > 0) && cmp(eb + b, k, wk) == 0;
         }
         const uint32_t g = d0 + pos;
-        const uint32_t kb = g / vcm;
-        uint8_t *dst = block_ptr(j, data_block_slot(kb, j.dbcm)) + kHeaderSize + (size_t)(g - kb * vcm) * vs;
+        const uint32_t kb = g / vcm, slot = data_block_slot(kb, dbcm);
+        uint8_t *blk = grid_base ? grid_base + (size_t)(gld<uint64_t>(addresses + slot) - 1) * bsize
+                                 : out_blocks + (size_t)slot * bsize; // block_ptr
+        uint8_t *dst = blk + kHeaderSize + (size_t)(g - kb * vcm) * vs;
         if constexpr (Wide) {
             asm volatile("" ::: "memory"); // one element's chunks live at a time
             constexpr uint32_t kChunks = 8;   // 128 bytes
