@@ -458,9 +458,12 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
     // (their keys are taken from there when they lie in them).
     const uint8_t *src[E];
     u32x4 v0[E], v1[E];
+    Key<KL> kw[Wide ? E : 1]; // Wide: every element's key, loaded together below
     auto key_of = [&](uint32_t q) {
         Key<KL> k;
-        if (in_regs) {
+        if constexpr (Wide) {
+            k = kw[q];
+        } else if (in_regs) {
 #pragma unroll
             for (int l = 0; l < KL; l++) {
                 k.l[l] = word_of(v0[q], v1[q], key_limb_off<KIND>(l, ts));
@@ -488,6 +491,11 @@ __device__ __forceinline__ void merge_unique_tile(uint8_t *lds, const JobDesc &j
             v0[q] = gld<u32x4>(src[q]);
             if (vs >= 32) v1[q] = gld<u32x4>(src[q] + 16);
         }
+    }
+    if constexpr (Wide) { // keys loaded together (each read next to its use waited for it alone)
+        const uint8_t *fb = src[0] ? src[0] : (const uint8_t *)(uintptr_t)(s0.a_ptr ? s0.a_ptr : s0.b_ptr);
+#pragma unroll
+        for (uint32_t q = 0; q < E; q++) kw[q] = load_key<KIND>(src[q] ? src[q] : fb, ts);
     }
     // The leading bits every key the tile compares shares (uniform: from
     // the tile's two boundaries, scalar loads).
