@@ -306,15 +306,20 @@ __global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs) {
     SortSeg &S = segs[blockIdx.x];
     S.nbytes = S.ndig = S.nruns = 0;
     if (!S.unsorted) return;
+    // The fields read below, once: S is written as it is filled in, so every
+    // read after a write to it was a fresh load waited for alone.
+    const uint32_t kl = S.kl, n = S.n;
+    uint64_t vary[kMaxLimbs];
+    for (uint32_t l = 0; l < kMaxLimbs; l++) vary[l] = l < kl ? S.key_or[l] ^ S.key_and[l] : 0;
     uint32_t nb = 0;
-    for (uint32_t l = 0; l < S.kl; l++)
+    for (uint32_t l = 0; l < kl; l++)
         for (uint32_t b = 0; b < 8; b++)
-            if (((S.key_or[l] ^ S.key_and[l]) >> (8 * b)) & 255) S.byte_src[nb++] = (uint8_t)(8 * l + b);
+            if ((vary[l] >> (8 * b)) & 255) S.byte_src[nb++] = (uint8_t)(8 * l + b);
     S.nbytes = nb;
     // Runs (limb, lowest bit, width), most significant first.
     uint32_t nr = 0;
-    for (int l = (int)S.kl - 1; l >= 0; l--) {
-        uint64_t m = S.key_or[l] ^ S.key_and[l];
+    for (int l = (int)kl - 1; l >= 0; l--) {
+        uint64_t m = vary[l];
         while (m) {
             const uint32_t hi = 63 - __builtin_clzll(m);
             const uint64_t gaps = ~m & low_mask(hi + 1); // clear bits at or below hi
@@ -343,12 +348,12 @@ __global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs) {
         }
         nr--;
     }
-    const uint32_t ib = 32 - __builtin_clz(S.n - 1); // S.n >= 2
+    const uint32_t ib = 32 - __builtin_clz(n - 1); // n >= 2
     uint32_t v = 0;
     for (uint32_t r = 0; r < nr; r++) v += rw[r];
-    S.trunc = 0;
+    uint32_t trunc = 0;
     while (v > 64 - ib) { // drop the lowest bits
-        S.trunc = 1;
+        trunc = 1;
         const uint32_t cut = v - (64 - ib);
         if (rw[nr - 1] <= cut) {
             v -= rw[--nr];
@@ -363,6 +368,7 @@ __global__ __launch_bounds__(64) void k_sort_layout(SortSeg *segs) {
         at -= rw[r];
         S.run[r] = rl[r] | (uint32_t)rs[r] << 8 | (uint32_t)rw[r] << 16 | at << 24;
     }
+    S.trunc = trunc;
     S.nruns = nr;
     S.ib = ib;
     S.kbits = v;
@@ -486,6 +492,7 @@ __global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *
         if (nd > first) atomicOr(&batch->active, (1u << (nd - first)) - 1u); // pass q runs if some table has > q
     }
     uint32_t *out = bins + (size_t)s * kMaxPasses * kRadix;
+    const uint32_t item_base = S.item_base; // read once: the stores below may alias S
     for (uint32_t m = active; m; m &= m - 1) {
         const uint32_t p = __builtin_ctz(m);
         const uint32_t c = h[p * kRadix + d];
@@ -498,7 +505,7 @@ __global__ __launch_bounds__(kRadix) void k_sort_plan(SortSeg *segs, SortBatch *
         __syncthreads();
         uint32_t off = 0;
         for (uint32_t w = 0; w < wave; w++) off += wsum[w];
-        out[p * kRadix + d] = S.item_base + off + incl - c;
+        out[p * kRadix + d] = item_base + off + incl - c;
         __syncthreads();
     }
 }
