@@ -1798,9 +1798,9 @@ __global__ __launch_bounds__(256) void k_assemble(const JobDesc *jobs, int njobs
                 uint32_t rem = obase + sl - (kfirst + k) * vcm;
                 u32x4 v[8];
 #pragma unroll
-                for (uint32_t u = 0; u < 8; u++) {
-                    const uint32_t c = c0 + tid + 256 * u;
-                    if (c < total) v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[c >> cpv_log] + 16 * (c & qmask));
+                for (uint32_t u = 0; u < 8; u++) { // unconditional (clamped): all eight source reads, then all loads
+                    const uint32_t c = c0 + tid + 256 * u < total ? c0 + tid + 256 * u : total - 1;
+                    v[u] = gld<u32x4>((const uint8_t *)(uintptr_t)s_src[c >> cpv_log] + 16 * (c & qmask));
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < 8; u++) {
