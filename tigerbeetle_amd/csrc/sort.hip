@@ -792,6 +792,19 @@ template <uint32_t C> __device__ __forceinline__ void copy_value(uint8_t *dst, c
     for (uint32_t c = 0; c < C; c++) gst<u32x4>(dst + 16 * c, v[c]);
 }
 
+// One value of vs bytes (a power of two >= 16; uniform across the wave).
+__device__ __forceinline__ void copy_any(uint8_t *dst, const uint8_t *src, uint32_t vs) {
+    switch (vs >> 4) {
+    case 1: copy_value<1>(dst, src); break;
+    case 2: copy_value<2>(dst, src); break;
+    case 4: copy_value<4>(dst, src); break;
+    case 8: copy_value<8>(dst, src); break;
+    default: // 256 bytes and up
+        for (uint32_t b = 0; b < vs; b += 256) copy_value<16>(dst + b, src + b);
+        break;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32_t *tile_seg, const uint64_t *words0,
                                                      const uint64_t *words1) {
     const uint32_t tile = blockIdx.x / (kSortTile / kFinishItems);
@@ -857,17 +870,7 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
         const uint64_t wi = wv[i], ti = wi >> sh;
         const uint64_t wp = wv[i > 0 ? i - 1 : i], wn = wv[i + 1 < n ? i + 1 : i];
         if ((i == 0 || (wp >> sh) != ti) && (i + 1 >= n || (wn >> sh) != ti)) {
-            const uint8_t *src = S.copy + (size_t)(uint32_t)(wi & imask) * vs;
-            uint8_t *dst = S.values + (size_t)i * vs;
-            switch (vs >> 4) { // uniform
-            case 1: copy_value<1>(dst, src); break;
-            case 2: copy_value<2>(dst, src); break;
-            case 4: copy_value<4>(dst, src); break;
-            case 8: copy_value<8>(dst, src); break;
-            default: // 256 bytes and up (powers of two)
-                for (uint32_t b = 0; b < vs; b += 256) copy_value<16>(dst + b, src + b);
-                break;
-            }
+            copy_any(S.values + (size_t)i * vs, S.copy + (size_t)(uint32_t)(wi & imask) * vs, vs);
             continue;
         }
         // run bounds [lo, hi) of equal top digits around i
@@ -890,8 +893,7 @@ __global__ __launch_bounds__(256) void k_sort_finish(SortSeg *segs, const uint32
             rank += key_before(q, other, k, me) ? 1u : 0u;
         }
         const uint32_t to = lo + rank;
-        for (uint32_t b = 0; b < vs; b += 16)
-            gst<u32x4>(S.values + (size_t)to * vs + b, gld<u32x4>(S.copy + (size_t)me * vs + b));
+        copy_any(S.values + (size_t)to * vs, S.copy + (size_t)me * vs, vs);
     }
 }
 
